@@ -1,0 +1,300 @@
+"""ctypes binding of libacinoset_hip.so (the C ABI in include/acinoset_hip.h).
+
+There is no CPU fallback: if the shared library is missing, or no gfx950 device is
+visible, every call raises `NativeUnavailable` loudly.
+
+`torch` is imported (if installed) BEFORE the library is loaded, so that the process
+has a single HIP runtime: torch bundles its own libamdhip64.so.7 and the library's
+NEEDED entry then binds to that already-loaded copy.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from typing import Optional
+
+import numpy as np
+
+try:  # one HIP runtime per process (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the product
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('ACINOSET_HIP_LIB', os.path.join(_HERE, 'libacinoset_hip.so'))
+
+ACS_DEVICE_PTRS = 1
+ACS_CAM_STRIDE = 20
+STATUS_NAMES = ('running', 'gtol', 'ftol', 'xtol', 'stalled', 'maxiter', 'noobs')
+
+# exported symbols (checked by tests against include/acinoset_hip.h)
+SYMBOLS = (
+    'acs_ctx_create', 'acs_ctx_destroy', 'acs_last_error', 'acs_ctx_set_stream', 'acs_ctx_sync',
+    'acs_abi_version', 'acs_device_count', 'acs_sba_default_opts', 'acs_project_fisheye',
+    'acs_sba_residuals', 'acs_sba_points', 'acs_sba_points_dense', 'acs_redescending_loss', 'acs_fk',
+    'acs_fte_default_opts', 'acs_fte_solve', 'acs_fte_eval', 'acs_triangulate_pairs',
+)
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class SbaOpts(C.Structure):
+    _fields_ = [('max_iters', C.c_int32), ('reserved', C.c_int32), ('f_scale', C.c_double),
+                ('ftol', C.c_double), ('xtol', C.c_double), ('gtol', C.c_double)]
+
+
+class Report(C.Structure):
+    _fields_ = [('n_problems', C.c_int64), ('status_counts', C.c_int64 * 7), ('iters_max', C.c_int64),
+                ('iters_sum', C.c_int64), ('nfev_sum', C.c_int64), ('cost_before', C.c_double),
+                ('cost_after', C.c_double)]
+
+    def as_dict(self):
+        return dict(n_problems=self.n_problems,
+                    status_counts={STATUS_NAMES[i]: int(self.status_counts[i]) for i in range(7)},
+                    iters_max=self.iters_max, iters_sum=self.iters_sum, nfev_sum=self.nfev_sum,
+                    cost_before=self.cost_before, cost_after=self.cost_after)
+
+
+class FteOpts(C.Structure):
+    _fields_ = [('max_iters', C.c_int32), ('window', C.c_int32), ('ftol', C.c_double), ('xtol', C.c_double),
+                ('gtol', C.c_double), ('lambda0', C.c_double), ('redesc_a', C.c_double),
+                ('redesc_b', C.c_double), ('redesc_c', C.c_double)]
+
+
+class FteReport(C.Structure):
+    _fields_ = [('status', C.c_int32), ('iters', C.c_int32), ('n_accepted', C.c_int32), ('reserved', C.c_int32),
+                ('cost_before', C.c_double), ('cost_after', C.c_double), ('cost_meas', C.c_double),
+                ('cost_model', C.c_double), ('grad_max', C.c_double), ('lambda_final', C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != 'reserved'}
+
+
+_lib = None
+_lock = threading.Lock()
+_P = C.c_void_p
+_D = C.POINTER(C.c_double)
+
+
+def _declare(lib):
+    i32, i64, u32, dbl = C.c_int32, C.c_int64, C.c_uint32, C.c_double
+    sig = {
+        'acs_ctx_create': (C.c_int, [C.c_int, C.POINTER(_P)]),
+        'acs_ctx_destroy': (C.c_int, [_P]),
+        'acs_last_error': (C.c_char_p, [_P]),
+        'acs_ctx_set_stream': (C.c_int, [_P, _P]),
+        'acs_ctx_sync': (C.c_int, [_P]),
+        'acs_abi_version': (C.c_int, []),
+        'acs_device_count': (C.c_int, [C.POINTER(C.c_int)]),
+        'acs_sba_default_opts': (None, [C.POINTER(SbaOpts)]),
+        'acs_project_fisheye': (C.c_int, [_P, _P, i32, _P, _P, i64, i32, _P, u32]),
+        'acs_sba_residuals': (C.c_int, [_P, _P, i32, _P, _P, _P, i64, _P, i64, _P, u32]),
+        'acs_sba_points': (C.c_int, [_P, _P, i32, _P, _P, _P, i64, _P, i64, C.POINTER(SbaOpts), _P, _P,
+                                     C.POINTER(Report), u32]),
+        'acs_sba_points_dense': (C.c_int, [_P, _P, i32, _P, _P, i64, _P, C.POINTER(SbaOpts), C.POINTER(Report),
+                                           u32]),
+        'acs_redescending_loss': (C.c_int, [_P, _P, i64, dbl, dbl, dbl, _P, _P, u32]),
+        'acs_fk': (C.c_int, [_P, _P, i64, _P, i64, _P, _P, _P, _P, i64, i32, i32, _P, _P, u32]),
+        'acs_fte_default_opts': (None, [C.POINTER(FteOpts)]),
+        'acs_fte_solve': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, dbl, _P, i32, i32, _P, _P,
+                                    C.POINTER(FteOpts), C.POINTER(FteReport), u32]),
+        'acs_fte_eval': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, dbl, _P, i32, i32, _P, _P,
+                                   _P, _P, _P, u32]),
+        'acs_triangulate_pairs': (C.c_int, [_P, _P, i32, _P, _P, _P, _P, i64, _P, u32]),
+    }
+    for name, (res, args) in sig.items():
+        if not hasattr(lib, name):
+            continue
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def load_library():
+    """Load libacinoset_hip.so (no GPU needed). Raises NativeUnavailable if missing."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeUnavailable(
+                    f'{LIB_PATH} not found: build it with `python -c "import __graft_entry__ as g; g.build()"` '
+                    '(hipcc --offload-arch=gfx950). There is no CPU fallback.')
+            lib = C.CDLL(LIB_PATH)
+            _declare(lib)
+            _lib = lib
+    return _lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    return C.c_void_p(a.ctypes.data)
+
+
+def _c64(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+def pack_cameras(K, D, R, t) -> np.ndarray:
+    """(C,3,3),(C,4[,1]),(C,3,3),(C,3[,1]) -> (C, 20) camera records (header: camera block)."""
+    K = np.asarray(K, np.float64).reshape(-1, 3, 3)
+    n = len(K)
+    D = np.asarray(D, np.float64).reshape(n, 4)
+    R = np.asarray(R, np.float64).reshape(n, 3, 3)
+    t = np.asarray(t, np.float64).reshape(n, 3)
+    cams = np.empty((n, ACS_CAM_STRIDE))
+    cams[:, 0] = K[:, 0, 0]
+    cams[:, 1] = K[:, 1, 1]
+    cams[:, 2] = K[:, 0, 2]
+    cams[:, 3] = K[:, 1, 2]
+    cams[:, 4:8] = D
+    cams[:, 8:17] = R.reshape(n, 9)
+    cams[:, 17:20] = t
+    return cams
+
+
+class Context:
+    """One HIP device + stream (acs_ctx). Methods take numpy arrays (host pointers)
+    unless `device_ptrs=True`, in which case they take raw device addresses (ints)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = _P()
+        rc = self.lib.acs_ctx_create(int(device), C.byref(h))
+        if rc != 0:
+            n = C.c_int(0)
+            self.lib.acs_device_count(C.byref(n))
+            raise NativeUnavailable(f'acs_ctx_create(device={device}) failed with {rc}: {n.value} HIP device(s) '
+                                    'visible; a gfx950 (MI355X) device is required and there is no CPU fallback.')
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.lib.acs_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.acs_last_error(self.h)
+            raise RuntimeError(f'{what} failed ({rc}): {msg.decode() if msg else ""}')
+
+    def set_stream(self, stream_handle: int):
+        self.check(self.lib.acs_ctx_set_stream(self.h, C.c_void_p(stream_handle or 0)), 'acs_ctx_set_stream')
+
+    def sync(self):
+        self.check(self.lib.acs_ctx_sync(self.h), 'acs_ctx_sync')
+
+    # ---- a1 -------------------------------------------------------------------------
+    def project(self, cams, pts, cam_idx=None, fte_form=False):
+        cams = _c64(cams)
+        pts = _c64(pts).reshape(-1, 3)
+        n = len(pts)
+        ci = None if cam_idx is None else np.ascontiguousarray(np.broadcast_to(cam_idx, (n,)), np.int32)
+        out = np.empty((n, 2))
+        self.check(self.lib.acs_project_fisheye(self.h, _ptr(cams), len(cams), _ptr(pts), _ptr(ci), n,
+                                                int(bool(fte_form)), _ptr(out), 0), 'acs_project_fisheye')
+        return out
+
+    # ---- a2 -------------------------------------------------------------------------
+    def sba_residuals(self, cams, uv, pt_idx, cam_idx, pts):
+        cams = _c64(cams)
+        uv = _c64(uv).reshape(-1, 2)
+        pi = np.ascontiguousarray(pt_idx, np.int32)
+        ci = np.ascontiguousarray(cam_idx, np.int32)
+        pts = _c64(pts).reshape(-1, 3)
+        out = np.empty(2 * len(uv))
+        self.check(self.lib.acs_sba_residuals(self.h, _ptr(cams), len(cams), _ptr(uv), _ptr(pi), _ptr(ci), len(uv),
+                                              _ptr(pts), len(pts), _ptr(out), 0), 'acs_sba_residuals')
+        return out
+
+    # ---- a4 -------------------------------------------------------------------------
+    @staticmethod
+    def sba_opts(f_scale=50.0, max_iters=100, ftol=1e-15, xtol=1e-10, gtol=1e-10):
+        return SbaOpts(int(max_iters), 0, float(f_scale), float(ftol), float(xtol), float(gtol))
+
+    def sba_points(self, cams, uv, pt_idx, cam_idx, pts0, opts=None, residuals=True):
+        cams = _c64(cams)
+        uv = _c64(uv).reshape(-1, 2)
+        pi = np.ascontiguousarray(pt_idx, np.int32)
+        ci = np.ascontiguousarray(cam_idx, np.int32)
+        pts = _c64(pts0).reshape(-1, 3).copy()
+        rb = np.empty(2 * len(uv)) if residuals else None
+        ra = np.empty(2 * len(uv)) if residuals else None
+        rep = Report()
+        opts = opts or self.sba_opts()
+        self.check(self.lib.acs_sba_points(self.h, _ptr(cams), len(cams), _ptr(uv), _ptr(pi), _ptr(ci), len(uv),
+                                           _ptr(pts), len(pts), C.byref(opts), _ptr(rb), _ptr(ra), C.byref(rep), 0),
+                   'acs_sba_points')
+        return pts, rb, ra, rep.as_dict()
+
+    def sba_points_dense(self, cams, uv, mask, pts0, opts=None):
+        cams = _c64(cams)
+        C_ = len(cams)
+        uv = _c64(uv).reshape(-1, C_, 2)
+        mask = np.ascontiguousarray(mask, np.uint8).reshape(-1, C_)
+        pts = _c64(pts0).reshape(-1, 3).copy()
+        rep = Report()
+        opts = opts or self.sba_opts()
+        self.check(self.lib.acs_sba_points_dense(self.h, _ptr(cams), C_, _ptr(uv), _ptr(mask), len(pts), _ptr(pts),
+                                                 C.byref(opts), C.byref(rep), 0), 'acs_sba_points_dense')
+        return pts, rep.as_dict()
+
+    def sba_points_dense_dev(self, cams_p, n_cams, uv_p, mask_p, n_pts, pts_p, opts=None, report=False):
+        """Device-pointer variant (inputs resident in HBM; asynchronous unless report)."""
+        opts = opts or self.sba_opts()
+        rep = Report() if report else None
+        self.check(self.lib.acs_sba_points_dense(self.h, C.c_void_p(cams_p), n_cams, C.c_void_p(uv_p),
+                                                 C.c_void_p(mask_p), n_pts, C.c_void_p(pts_p), C.byref(opts),
+                                                 C.byref(rep) if rep is not None else None, ACS_DEVICE_PTRS),
+                   'acs_sba_points_dense')
+        return rep.as_dict() if rep is not None else None
+
+    # ---- a9 -------------------------------------------------------------------------
+    def redescending_loss(self, err, a=3.0, b=10.0, c=20.0, deriv=False):
+        e = _c64(err).ravel()
+        out = np.empty_like(e)
+        d = np.empty_like(e) if deriv else None
+        self.check(self.lib.acs_redescending_loss(self.h, _ptr(e), len(e), a, b, c, _ptr(out), _ptr(d), 0),
+                   'acs_redescending_loss')
+        return (out, d) if deriv else out
+
+    # ---- a7 -------------------------------------------------------------------------
+    def fk(self, table, x, dx=None, ddx=None, tau=None, intermode=0, directions=False, jac=False):
+        x = _c64(x).reshape(-1, table.P)
+        n = len(x)
+        dx = None if dx is None else _c64(dx).reshape(n, table.P)
+        ddx = None if ddx is None else _c64(ddx).reshape(n, table.P)
+        tau = None if tau is None else _c64(np.broadcast_to(tau, (n,)))
+        Lo = table.L + (2 if directions else 0)
+        out = np.empty((n, Lo, 3))
+        J = np.empty((n, table.L, 3, table.P)) if jac else None
+        ints = np.ascontiguousarray(table.ints, np.int32)
+        reals = np.ascontiguousarray(table.reals, np.float64)
+        self.check(self.lib.acs_fk(self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), _ptr(x), _ptr(dx),
+                                   _ptr(ddx), _ptr(tau), n, int(intermode), int(bool(directions)), _ptr(out),
+                                   _ptr(J), 0), 'acs_fk')
+        return (out, J) if jac else out
+
+
+_default_ctx = None
+
+
+def default_context() -> Context:
+    """Process-wide context on the device selected by LOCAL_RANK (default 0)."""
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(int(os.environ.get('ACINOSET_DEVICE', os.environ.get('LOCAL_RANK', 0))))
+    return _default_ctx

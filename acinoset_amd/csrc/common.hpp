@@ -1,0 +1,163 @@
+// common.hpp — context, device workspace, error plumbing and the fisheye camera model
+// shared by every translation unit of libacinoset_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "acinoset_hip.h"
+
+// ------------------------------------------------------------------------------------
+// Context
+// ------------------------------------------------------------------------------------
+enum WsSlot {
+  WS_CAMS = 0, WS_UV, WS_MASK, WS_CAMID, WS_PTS, WS_PTIDX, WS_CAMIDX, WS_OUT0, WS_OUT1,
+  WS_PERPT_F0, WS_PERPT_F1, WS_PERPT_I, WS_REPORT, WS_SORT0, WS_SORT1, WS_SORT2, WS_SORT3,
+  WS_TMP0, WS_TMP1, WS_TMP2, WS_TMP3, WS_TMP4, WS_TMP5, WS_TMP6, WS_TMP7,
+  WS_FTE0, WS_FTE1, WS_FTE2, WS_FTE3, WS_FTE4, WS_FTE5, WS_FTE6, WS_FTE7, WS_FTE8, WS_FTE9,
+  WS_FTE10, WS_FTE11, WS_FTE12, WS_FTE13, WS_FTE14, WS_FTE15,
+  WS_NSLOTS
+};
+
+struct acs_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  void* ws[WS_NSLOTS] = {};
+  size_t ws_bytes[WS_NSLOTS] = {};
+  int n_cu = 256;
+};
+
+int acs_fail(acs_ctx* ctx, int code, const char* fmt, ...);
+
+#define ACS_HIP(ctx, call)                                                                 \
+  do {                                                                                     \
+    hipError_t _e = (call);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      return acs_fail((ctx), ACS_E_HIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(_e), \
+                      __FILE__, __LINE__);                                                 \
+  } while (0)
+
+#define ACS_CHECK(ctx, cond, ...)                                                          \
+  do {                                                                                     \
+    if (!(cond)) return acs_fail((ctx), ACS_E_INVALID, __VA_ARGS__);                       \
+  } while (0)
+
+// Grow-only device workspace slot. Returns nullptr (and sets the error) on failure.
+void* acs_ws(acs_ctx* ctx, int slot, size_t bytes);
+
+// Host<->device staging: with ACS_DEVICE_PTRS the pointer is used as is.
+int acs_stage_in(acs_ctx* ctx, int slot, const void* src, size_t bytes, uint32_t flags, void** dev);
+int acs_stage_out(acs_ctx* ctx, void* dst, const void* dev, size_t bytes, uint32_t flags);
+// Output buffer: the caller's device pointer, or a workspace slot to copy back later.
+void* acs_out_buf(acs_ctx* ctx, int slot, void* dst, size_t bytes, uint32_t flags);
+
+static inline int acs_grid(int64_t n, int block) { return (int)((n + block - 1) / block); }
+
+// ------------------------------------------------------------------------------------
+// Fisheye camera model (cv::fisheye::projectPoints with alpha = 0; src/lib/calib.py:132,
+// restated by the reference itself in src/core/fte.py:80-96). Camera record layout:
+// [fx fy cx cy k1 k2 k3 k4 R00..R22 t0 t1 t2] (ACS_CAM_STRIDE = 20 doubles).
+// ------------------------------------------------------------------------------------
+struct ProjOut {
+  double u, v;
+  double J[6];  // d(u,v)/dX, row-major 2x3
+};
+
+template <bool JAC, bool FTE_FORM = false>
+__device__ __forceinline__ void fisheye_project(const double* __restrict__ c, double X0, double X1,
+                                                double X2, ProjOut& o) {
+  const double Y0 = fma(c[8], X0, fma(c[9], X1, fma(c[10], X2, c[17])));
+  const double Y1 = fma(c[11], X0, fma(c[12], X1, fma(c[13], X2, c[18])));
+  const double Y2 = fma(c[14], X0, fma(c[15], X1, fma(c[16], X2, c[19])));
+  const double a = Y0 / Y2;
+  const double b = Y1 / Y2;
+  const double r2 = a * a + b * b;
+  const double k1 = c[4], k2 = c[5], k3 = c[6], k4 = c[7];
+  double r = FTE_FORM ? sqrt(r2 + 1e-12) : sqrt(r2);
+  const double th = atan(r);
+  const double th2 = th * th;
+  const double poly = 1.0 + th2 * (k1 + th2 * (k2 + th2 * (k3 + th2 * k4)));
+  const double thd = th * poly;
+  const bool big = FTE_FORM ? true : (r > 1e-8);
+  const double s = big ? thd / r : 1.0;
+  o.u = c[0] * (a * s) + c[2];
+  o.v = c[1] * (b * s) + c[3];
+  if (JAC) {
+    // s'(r)/r = (thd'(th) r / (1 + r^2) - thd) / r^3   (0 below OpenCV's guard)
+    const double dthd = 1.0 + th2 * (3.0 * k1 + th2 * (5.0 * k2 + th2 * (7.0 * k3 + th2 * 9.0 * k4)));
+    double spr;
+    if (FTE_FORM) {
+      // r = sqrt(a^2+b^2+eps): dr/da = a/r, same formula with this r
+      spr = (dthd * r / (1.0 + r * r) - thd) / (r * r * r);
+    } else {
+      spr = (r2 > 1e-16) ? (dthd * r / (1.0 + r2) - thd) / (r * r2) : 0.0;
+    }
+    const double duda = c[0] * (s + a * a * spr);
+    const double dudb = c[0] * (a * b * spr);
+    const double dvda = c[1] * (a * b * spr);
+    const double dvdb = c[1] * (s + b * b * spr);
+    const double iz = 1.0 / Y2;
+    // d(u,v)/dY = J_uv_ab * [[iz, 0, -a iz], [0, iz, -b iz]]
+    const double u0 = duda * iz, u1 = dudb * iz, u2 = -(duda * a + dudb * b) * iz;
+    const double v0 = dvda * iz, v1 = dvdb * iz, v2 = -(dvda * a + dvdb * b) * iz;
+    // times R
+    o.J[0] = u0 * c[8] + u1 * c[11] + u2 * c[14];
+    o.J[1] = u0 * c[9] + u1 * c[12] + u2 * c[15];
+    o.J[2] = u0 * c[10] + u1 * c[13] + u2 * c[16];
+    o.J[3] = v0 * c[8] + v1 * c[11] + v2 * c[14];
+    o.J[4] = v0 * c[9] + v1 * c[12] + v2 * c[15];
+    o.J[5] = v0 * c[10] + v1 * c[13] + v2 * c[16];
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Redescending loss (src/lib/misc.py:329-343): value, d/de and d2/de2.
+// ------------------------------------------------------------------------------------
+struct LossOut {
+  double f, d1, d2;
+};
+
+__device__ __forceinline__ LossOut redescending(double err, double a, double b, double c) {
+  const double E = fabs(err);
+  const double sa = 1.0 / (1.0 + exp(-(E - a)));
+  const double sb = 1.0 / (1.0 + exp(-(E - b)));
+  const double sc = 1.0 / (1.0 + exp(-(E - c)));
+  const double da = sa * (1.0 - sa), db = sb * (1.0 - sb), dc = sc * (1.0 - sc);
+  const double dda = da * (1.0 - 2.0 * sa), ddb = db * (1.0 - 2.0 * sb), ddc = dc * (1.0 - 2.0 * sc);
+  const double lin = a * E - 0.5 * a * a;
+  const double K3 = a * b - 0.5 * a * a;
+  const double cb = c - b;
+  const double w = (c - E) / cb;
+  const double q = K3 + (0.5 * a * cb) * (1.0 - w * w);
+  const double q1 = a * (c - E) / cb;
+  const double q2 = -a / cb;
+  const double K4 = K3 + 0.5 * a * cb;
+  LossOut o;
+  o.f = (1.0 - sa) * 0.5 * E * E + (sa - sb) * lin + (sb - sc) * q + sc * K4;
+  const double dE = -0.5 * da * E * E + (1.0 - sa) * E + (da - db) * lin + (sa - sb) * a +
+                    (db - dc) * q + (sb - sc) * q1 + dc * K4;
+  const double ddE = -0.5 * dda * E * E - 2.0 * da * E + (1.0 - sa) + (dda - ddb) * lin +
+                     2.0 * (da - db) * a + (ddb - ddc) * q + 2.0 * (db - dc) * q1 + (sb - sc) * q2 +
+                     ddc * K4;
+  const double sg = err > 0.0 ? 1.0 : (err < 0.0 ? -1.0 : 0.0);
+  o.d1 = dE * sg;
+  o.d2 = ddE;
+  return o;
+}
+
+// Butterfly sum inside an aligned group of G lanes. IEEE addition is commutative, so
+// every lane of the group ends with bit-identical sums.
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, G);
+  return v;
+}

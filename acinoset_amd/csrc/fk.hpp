@@ -1,0 +1,240 @@
+// fk.hpp — table-driven forward kinematics + analytic FK Jacobian, evaluated
+// cooperatively by the lanes of one workgroup for one frame, all state in LDS.
+//
+// Restates get_3d_marker_coords (src/lib/misc.py:144-326): joint frames
+// M_j = R_j_I = RI_j^T with RI_j = R_a(t_a) R_b(t_b) ... RI_parent (rot_x/y/z of
+// misc.py:381-420 are passive rotations, so each factor's transpose is an active
+// rotation A); nodes p_k = p_base + M_frame @ offset.
+// Jacobian: for a rotation parameter alpha of joint j, d p_k / d alpha =
+// omega_alpha x (p_k - p_origin(j)) where omega_alpha = M_parent(j) A_{n-1}..A_{r+1} e_axis
+// is the world-frame rotation axis; translations give e_axis; the neck length l_1
+// gives M_frame e_x. Table layout: acinoset_amd/kinematics.py::build_table.
+#pragma once
+#include "common.hpp"
+
+#define FK_MAXP 32
+#define FK_MAXJ 16
+#define FK_MAXN 32
+#define FK_HDR 8
+
+enum { PK_TRANS = 0, PK_ROT = 1, PK_LEN = 2, PK_WORLD = 3 };
+
+struct SkelView {
+  int J, K, P, L, head;
+  const int* joints;   // J*8: parent, nrot, ax0..2, p0..2
+  const int* jorigin;  // J
+  const int* nodes;    // K*4: base, frame, offset_param, is_world
+  const int* outn;     // L
+  const int* pk;       // P*4: kind, a, b, c
+  const int* deriv;    // K*P
+  const double* off;   // K*3
+};
+
+__device__ __forceinline__ SkelView skel_view(const int* I, const double* R) {
+  SkelView s;
+  s.J = I[0];
+  s.K = I[1];
+  s.P = I[2];
+  s.L = I[3];
+  s.head = I[4];
+  const int* q = I + FK_HDR;
+  s.joints = q;
+  q += 8 * s.J;
+  s.jorigin = q;
+  q += s.J;
+  s.nodes = q;
+  q += 4 * s.K;
+  s.outn = q;
+  q += s.L;
+  s.pk = q;
+  q += 4 * s.P;
+  s.deriv = q;
+  s.off = R;
+  return s;
+}
+
+struct FkShared {
+  double sn[FK_MAXP], cs[FK_MAXP], xp[FK_MAXP];
+  double G[FK_MAXJ][9];
+  double M[FK_MAXJ][9];
+  double pos[FK_MAXN][3];
+  double om[FK_MAXP][3];
+};
+
+// y = A_axis(angle) @ x for the active rotation A = rot_axis(angle)^T
+__device__ __forceinline__ void act_rot_vec(int axis, double s, double c, const double* x, double* y) {
+  if (axis == 0) {  // rot_x^T = [[1,0,0],[0,c,-s],[0,s,c]]
+    y[0] = x[0];
+    y[1] = c * x[1] - s * x[2];
+    y[2] = s * x[1] + c * x[2];
+  } else if (axis == 1) {  // rot_y^T = [[c,0,s],[0,1,0],[-s,0,c]]
+    y[0] = c * x[0] + s * x[2];
+    y[1] = x[1];
+    y[2] = -s * x[0] + c * x[2];
+  } else {  // rot_z^T = [[c,-s,0],[s,c,0],[0,0,1]]
+    y[0] = c * x[0] - s * x[1];
+    y[1] = s * x[0] + c * x[1];
+    y[2] = x[2];
+  }
+}
+
+__device__ __forceinline__ void mat3_mul(const double* A, const double* B, double* C) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+// Evaluate one frame. `x` may live in global or shared memory. Caller must
+// __syncthreads() before reading sh (positions / M / om). Positions exclude any
+// shutter-delay shift (callers add it).
+__device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int tid, int nth) {
+  for (int p = tid; p < s.P; p += nth) {
+    double v = x[p];
+    sh.xp[p] = v;
+    sincos(v, &sh.sn[p], &sh.cs[p]);
+  }
+  __syncthreads();
+  for (int j = tid; j < s.J; j += nth) {
+    const int* jt = s.joints + 8 * j;
+    const int nrot = jt[1];
+    // G = A_{n-1} ... A_0 (apply A_0 first): build column by column from identity
+    double Gm[9];
+#pragma unroll
+    for (int col = 0; col < 3; ++col) {
+      double v[3] = {col == 0 ? 1.0 : 0.0, col == 1 ? 1.0 : 0.0, col == 2 ? 1.0 : 0.0};
+      for (int r = 0; r < nrot; ++r) {
+        double w[3];
+        const int p = jt[5 + r];
+        act_rot_vec(jt[2 + r], sh.sn[p], sh.cs[p], v, w);
+        v[0] = w[0];
+        v[1] = w[1];
+        v[2] = w[2];
+      }
+      Gm[col] = v[0];
+      Gm[3 + col] = v[1];
+      Gm[6 + col] = v[2];
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) sh.G[j][i] = Gm[i];
+  }
+  __syncthreads();
+  for (int j = tid; j < s.J; j += nth) {
+    double Mm[9], T[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Mm[i] = sh.G[j][i];
+    int k = s.joints[8 * j];
+    while (k >= 0) {  // M_j = G_root ... G_parent G_j
+      mat3_mul(sh.G[k], Mm, T);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Mm[i] = T[i];
+      k = s.joints[8 * k];
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) sh.M[j][i] = Mm[i];
+  }
+  __syncthreads();
+  const int* pk = s.pk;
+  for (int k = tid; k < s.K; k += nth) {
+    double p0 = 0.0, p1 = 0.0, p2 = 0.0;
+    int node = k;
+    while (true) {
+      const int* nd = s.nodes + 4 * node;
+      const int base = nd[0];
+      if (base == -2) {  // world node (lure): params of PK_WORLD kind
+        for (int q = 0; q < s.P; ++q) {
+          if (pk[4 * q] == PK_WORLD) {
+            const int ax = pk[4 * q + 1];
+            if (ax == 0) p0 += sh.xp[q];
+            if (ax == 1) p1 += sh.xp[q];
+            if (ax == 2) p2 += sh.xp[q];
+          }
+        }
+        break;
+      }
+      if (base == -1) {  // head root: (x_0, y_0, z_0)
+        for (int q = 0; q < s.P; ++q) {
+          if (pk[4 * q] == PK_TRANS) {
+            const int ax = pk[4 * q + 1];
+            if (ax == 0) p0 += sh.xp[q];
+            if (ax == 1) p1 += sh.xp[q];
+            if (ax == 2) p2 += sh.xp[q];
+          }
+        }
+        break;
+      }
+      const double* Mf = sh.M[nd[1]];
+      double o0 = s.off[3 * node], o1 = s.off[3 * node + 1], o2 = s.off[3 * node + 2];
+      if (nd[2] >= 0) o0 = sh.xp[nd[2]];
+      p0 += Mf[0] * o0 + Mf[1] * o1 + Mf[2] * o2;
+      p1 += Mf[3] * o0 + Mf[4] * o1 + Mf[5] * o2;
+      p2 += Mf[6] * o0 + Mf[7] * o1 + Mf[8] * o2;
+      node = base;
+    }
+    sh.pos[k][0] = p0;
+    sh.pos[k][1] = p1;
+    sh.pos[k][2] = p2;
+  }
+  for (int q = tid; q < s.P; q += nth) {
+    if (pk[4 * q] != PK_ROT) {
+      sh.om[q][0] = sh.om[q][1] = sh.om[q][2] = 0.0;
+      continue;
+    }
+    const int j = pk[4 * q + 1], r = pk[4 * q + 2];
+    const int* jt = s.joints + 8 * j;
+    const int nrot = jt[1];
+    double v[3] = {0.0, 0.0, 0.0};
+    v[jt[2 + r]] = 1.0;
+    for (int rr = r + 1; rr < nrot; ++rr) {
+      double w[3];
+      const int p = jt[5 + rr];
+      act_rot_vec(jt[2 + rr], sh.sn[p], sh.cs[p], v, w);
+      v[0] = w[0];
+      v[1] = w[1];
+      v[2] = w[2];
+    }
+    const int par = jt[0];
+    if (par >= 0) {
+      const double* Mp = sh.M[par];
+      sh.om[q][0] = Mp[0] * v[0] + Mp[1] * v[1] + Mp[2] * v[2];
+      sh.om[q][1] = Mp[3] * v[0] + Mp[4] * v[1] + Mp[5] * v[2];
+      sh.om[q][2] = Mp[6] * v[0] + Mp[7] * v[1] + Mp[8] * v[2];
+    } else {
+      sh.om[q][0] = v[0];
+      sh.om[q][1] = v[1];
+      sh.om[q][2] = v[2];
+    }
+  }
+}
+
+// d pos[node] / d x[q] (3-vector). Valid after fk_frame + __syncthreads().
+__device__ __forceinline__ void fk_dpos(const SkelView& s, const FkShared& sh, int node, int q, double* d) {
+  d[0] = d[1] = d[2] = 0.0;
+  if (!s.deriv[node * s.P + q]) return;
+  const int* pk = s.pk + 4 * q;
+  switch (pk[0]) {
+    case PK_TRANS:
+    case PK_WORLD:
+      d[pk[1]] = 1.0;
+      break;
+    case PK_LEN: {
+      const int owner = pk[1];
+      const double* Mf = sh.M[s.nodes[4 * owner + 1]];
+      d[0] = Mf[0];
+      d[1] = Mf[3];
+      d[2] = Mf[6];
+      break;
+    }
+    case PK_ROT: {
+      const int o = s.jorigin[pk[1]];
+      const double r0 = sh.pos[node][0] - sh.pos[o][0];
+      const double r1 = sh.pos[node][1] - sh.pos[o][1];
+      const double r2 = sh.pos[node][2] - sh.pos[o][2];
+      const double* w = sh.om[q];
+      d[0] = w[1] * r2 - w[2] * r1;
+      d[1] = w[2] * r0 - w[0] * r2;
+      d[2] = w[0] * r1 - w[1] * r0;
+      break;
+    }
+  }
+}

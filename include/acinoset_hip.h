@@ -1,0 +1,135 @@
+/*
+ * acinoset_hip.h — C ABI of the MI355X-native AcinoSet SBA/FTE core
+ * (libacinoset_hip.so, HIP kernels for gfx950).
+ *
+ * The reference has no FFI layer: its seams are Python call signatures. Every entry
+ * point below replaces the numeric body of one of those seams (cited per function);
+ * the Python drop-ins in acinoset_amd/lib and acinoset_amd/core bind them via ctypes
+ * (INTEGRATION.md shows the binding a reference maintainer would add).
+ *
+ * Conventions
+ *  - All functions return an int status: ACS_OK (0) or a negative ACS_E_* code; the
+ *    message is in acs_last_error(ctx).
+ *  - Array arguments are HOST pointers (copied into context-owned device buffers and
+ *    back) unless ACS_DEVICE_PTRS is set in `flags`, in which case every array pointer
+ *    of that call is a device pointer and the call is asynchronous on the context
+ *    stream (results valid after acs_ctx_sync or a later synchronous call).
+ *  - float64 everywhere (the reference is float64 throughout: src/lib/utils.py:68-71).
+ *  - Camera block: ACS_CAM_STRIDE doubles per camera:
+ *      [fx, fy, cx, cy, k1, k2, k3, k4, R00..R22 (row-major), t0, t1, t2]
+ *    = K[0,0], K[1,1], K[0,2], K[1,2] of the scene JSON 'k', 'd' (4), 'r' (3x3), 't' (3)
+ *    (src/lib/utils.py:55-74). Skew K[0,1] is ignored, as by cv::fisheye (alpha = 0).
+ *  - One context = one HIP device + one stream; calls on a context are not thread-safe.
+ */
+#ifndef ACINOSET_HIP_H
+#define ACINOSET_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACS_ABI_VERSION 1
+#define ACS_CAM_STRIDE 20
+
+/* status codes */
+#define ACS_OK 0
+#define ACS_E_INVALID -1   /* bad argument / shape */
+#define ACS_E_HIP -2       /* HIP runtime error */
+#define ACS_E_NOMEM -3     /* device allocation failed */
+#define ACS_E_NODEV -4     /* no usable gfx950 device */
+
+/* flags */
+#define ACS_DEVICE_PTRS 1u  /* array arguments are device pointers; call is async */
+
+/* per-problem convergence status (acs_report.status_counts index / oracle/sba.py) */
+#define ACS_STATUS_RUNNING 0
+#define ACS_STATUS_GTOL 1
+#define ACS_STATUS_FTOL 2
+#define ACS_STATUS_XTOL 3
+#define ACS_STATUS_STALLED 4
+#define ACS_STATUS_MAXITER 5
+#define ACS_STATUS_NOOBS 6
+#define ACS_N_STATUS 7
+
+typedef struct acs_ctx acs_ctx;
+
+typedef struct {
+  int32_t max_iters;  /* LM iterations (accepted + rejected) per problem; default 100 */
+  int32_t reserved;
+  double f_scale;     /* Cauchy soft-threshold in px; reference default 50 (src/lib/sba.py:181) */
+  double ftol;        /* relative cost decrease; reference passes 1e-15 (src/lib/sba.py:189) */
+  double xtol;        /* relative step; default 1e-10 */
+  double gtol;        /* max |gradient|; default 1e-10 */
+} acs_sba_opts;
+
+typedef struct {
+  int64_t n_problems;                   /* points (SBA) or 1 (FTE) */
+  int64_t status_counts[ACS_N_STATUS];  /* problems ending in each ACS_STATUS_* */
+  int64_t iters_max;                    /* max LM iterations over problems */
+  int64_t iters_sum;                    /* total LM iterations */
+  int64_t nfev_sum;                     /* total cost evaluations */
+  double cost_before;                   /* sum of robust cost at x0 */
+  double cost_after;                    /* sum of robust cost at the solution */
+} acs_report;
+
+/* ---- context -------------------------------------------------------------------- */
+int acs_ctx_create(int device, acs_ctx** out);
+int acs_ctx_destroy(acs_ctx* ctx);
+const char* acs_last_error(const acs_ctx* ctx);
+int acs_ctx_set_stream(acs_ctx* ctx, void* hip_stream);  /* NULL = context's own stream */
+int acs_ctx_sync(acs_ctx* ctx);
+int acs_abi_version(void);
+int acs_device_count(int* n);
+void acs_sba_default_opts(acs_sba_opts* o);
+
+/* ---- a1: fisheye projection (src/lib/calib.py:132-136, src/core/fte.py:80-96) -------
+ * uv[i] = project(cams[cam_idx[i]], pts[i]); cam_idx may be NULL (all camera 0).
+ * fte_form != 0 uses the FTE restatement r = sqrt(a^2 + b^2 + 1e-12) (fte.py:88)
+ * instead of OpenCV's r > 1e-8 guard.                                                 */
+int acs_project_fisheye(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* pts,
+                        const int32_t* cam_idx, int64_t n, int32_t fte_form, double* uv_out,
+                        uint32_t flags);
+
+/* ---- a2: SBA residual vector (cost_func_points_only, src/lib/sba.py:149-153) -------
+ * resid[2i+d] = project(cams[cam_idx[i]], pts[pt_idx[i]])[d] - uv[2i+d]              */
+int acs_sba_residuals(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
+                      const int32_t* pt_idx, const int32_t* cam_idx, int64_t n_obs,
+                      const double* pts, int64_t n_pts, double* resid_out, uint32_t flags);
+
+/* ---- a3/a4: points-only SBA (bundle_adjust_points_only, src/lib/sba.py:181-195) -----
+ * Observation list as the reference passes it (points_2d, point_3d_indices,
+ * camera_indices; any order, duplicates allowed). pts (n_pts x 3) is the initial
+ * estimate on input and the solution on output. resid_before / resid_after (2*n_obs,
+ * may be NULL) are the reference's residuals['before'/'after']. report may be NULL.  */
+int acs_sba_points(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
+                   const int32_t* pt_idx, const int32_t* cam_idx, int64_t n_obs, double* pts,
+                   int64_t n_pts, const acs_sba_opts* opts, double* resid_before,
+                   double* resid_after, acs_report* report, uint32_t flags);
+
+/* ---- dense observation-tensor SBA (the core.sba layout, src/core/sba.py:41-43) ------
+ * Point p = one (frame, marker); uv is (n_pts, n_cams, 2), mask (n_pts, n_cams) u8
+ * (1 = valid observation). Same solver as acs_sba_points.                             */
+int acs_sba_points_dense(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
+                         const uint8_t* mask, int64_t n_pts, double* pts,
+                         const acs_sba_opts* opts, acs_report* report, uint32_t flags);
+
+/* ---- a9: redescending loss (src/lib/misc.py:329-343), elementwise ------------------ */
+int acs_redescending_loss(acs_ctx* ctx, const double* err, int64_t n, double a, double b, double c,
+                          double* out, double* dout /* d loss/d err, may be NULL */, uint32_t flags);
+
+/* ---- a7: forward kinematics (get_3d_marker_coords, src/lib/misc.py:144-326) ----------
+ * Skeleton tables come from acinoset_amd.kinematics.build_table (int/real blobs).
+ * x, dx, ddx: (n, P); tau: (n,) or NULL; intermode 0 pos / 1 vel / 2 acc;
+ * out: (n, L + 2*directions, 3); jac (n, L, 3, P) may be NULL.                        */
+int acs_fk(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
+           int64_t n_reals, const double* x, const double* dx, const double* ddx, const double* tau,
+           int64_t n, int32_t intermode, int32_t directions, double* out, double* jac,
+           uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACINOSET_HIP_H */

@@ -1,0 +1,161 @@
+"""Oracle: points-only sparse bundle adjustment.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Reference: `bundle_adjust_points_only` (`src/lib/sba.py:181-195`) minimises, with
+scipy `least_squares(method='trf', loss='cauchy', f_scale=50)`, the residual vector of
+`cost_func_points_only` (`src/lib/sba.py:149-153`): reprojection minus observation,
+(u, v) interleaved per observation. With the cameras fixed, the Jacobian is
+block-diagonal per 3D point (`create_bundle_adjustment_jacobian_sparsity_matrix`,
+`src/lib/sba.py:11-22`), so the problem is a batch of independent 3-parameter robust
+least-squares problems (the reference output equals the
+per-point minimiser to <= 4e-8 m).
+
+This module minimises each point's cost  F = 0.5 f^2 sum log1p((r/f)^2)  with the same
+safeguarded Levenberg-Marquardt the HIP kernel runs (IRLS Gauss-Newton normal matrix
+H = sum w J^T J, w = 1/(1 + (r/f)^2); Marquardt damping H + lam*diag(H); accept only on
+strict cost decrease). Spec shared with `acinoset_amd/csrc/sba.hip`:
+
+    lam0 = 1e-3; accept: lam = max(lam/10, 1e-15); reject: lam *= 10
+    stop: |g|_inf <= gtol | accepted and (dF <= ftol*F or |dx| <= xtol*(xtol+|x|))
+          | rejected and |dx| <= xtol*(xtol+|x|) | lam > 1e16 | iters >= max_iters
+"""
+import numpy as np
+
+from .fisheye import project, project_jac
+
+# status codes (same values as include/acinoset_hip.h ACS_STATUS_*)
+RUNNING, GTOL, FTOL, XTOL, STALLED, MAXITER, NOOBS = 0, 1, 2, 3, 4, 5, 6
+
+
+def cost_func_points_only(params, n_points, point_3d_indices, camera_indices, k_arr, d_arr, r_arr, t_arr,
+                          points_2d):
+    """`src/lib/sba.py:149-153`, vectorised: (2*n_obs,) interleaved residuals."""
+    obj = np.asarray(params, np.float64).reshape(n_points, 3)
+    pi = np.asarray(point_3d_indices)
+    ci = np.asarray(camera_indices)
+    uv = project(obj[pi], k_arr[ci], d_arr[ci], r_arr[ci], t_arr[ci])
+    return (uv - np.asarray(points_2d, np.float64)).ravel()
+
+
+def _group(point_idx, n_pts):
+    """Ragged obs -> padded (n_pts, kmax) index table (-1 = pad), obs order kept."""
+    order = np.argsort(point_idx, kind='stable')
+    counts = np.bincount(point_idx, minlength=n_pts)
+    kmax = max(int(counts.max()) if counts.size else 0, 1)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    rank = np.arange(len(order)) - np.repeat(starts, counts)
+    table = -np.ones((n_pts, kmax), np.int64)
+    table[point_idx[order], rank] = order
+    return table
+
+
+def sba_points(points_2d, points_3d, point_idx, cam_idx, K, D, R, t, f_scale=50.0, max_iters=100,
+               ftol=1e-15, xtol=1e-10, gtol=1e-10, return_info=False):
+    """Batched per-point LM. Returns optimised points (n_pts, 3) [, info dict]."""
+    uvobs = np.asarray(points_2d, np.float64)
+    x = np.array(points_3d, np.float64).reshape(-1, 3)
+    n_pts = len(x)
+    point_idx = np.asarray(point_idx, np.int64)
+    cam_idx = np.asarray(cam_idx, np.int64)
+    tab = _group(point_idx, n_pts)                     # (n, k)
+    valid = tab >= 0
+    o = np.where(valid, tab, 0)
+    ci = cam_idx[o]
+    Kc, Dc, Rc, tc = K[ci], D[ci], R[ci], t[ci]
+    meas = uvobs[o]                                     # (n, k, 2)
+    f2 = f_scale * f_scale
+
+    def cost(xx):
+        uv = project(np.repeat(xx[:, None], tab.shape[1], 1).reshape(-1, 3), Kc.reshape(-1, 3, 3),
+                     Dc.reshape(-1, 4, 1), Rc.reshape(-1, 3, 3), tc.reshape(-1, 3, 1)).reshape(meas.shape)
+        r = np.where(valid[..., None], uv - meas, 0.0)
+        return 0.5 * f2 * np.log1p(r * r / f2).sum((1, 2))
+
+    def linearize(xx):
+        uv, J = project_jac(np.repeat(xx[:, None], tab.shape[1], 1).reshape(-1, 3), Kc.reshape(-1, 3, 3),
+                            Dc.reshape(-1, 4, 1), Rc.reshape(-1, 3, 3), tc.reshape(-1, 3, 1))
+        uv = uv.reshape(meas.shape)
+        J = J.reshape(meas.shape + (3,))
+        r = np.where(valid[..., None], uv - meas, 0.0)
+        z = r * r / f2
+        w = np.where(valid[..., None], 1.0 / (1.0 + z), 0.0)
+        H = np.einsum('nkd,nkdi,nkdj->nij', w, J, J)
+        g = np.einsum('nkd,nkd,nkdi->ni', w, r, J)
+        F = 0.5 * f2 * np.log1p(z).sum((1, 2))
+        return F, H, g
+
+    has = valid.sum(1) > 0
+    status = np.where(has, RUNNING, NOOBS)
+    iters = np.zeros(n_pts, np.int64)
+    nfev = np.ones(n_pts, np.int64)
+    lam = np.full(n_pts, 1e-3)
+    F, H, g = linearize(x)
+    cost_before = F.copy()
+    for _ in range(max_iters):
+        act = status == RUNNING
+        if not act.any():
+            break
+        gmax = np.abs(g).max(1)
+        done = act & (gmax <= gtol)
+        status[done] = GTOL
+        act &= ~done
+        if not act.any():
+            break
+        A = H.copy()
+        A[:, [0, 1, 2], [0, 1, 2]] *= (1.0 + lam)[:, None]
+        try:
+            L = np.linalg.cholesky(A[act])
+            ok = np.ones(act.sum(), bool)
+        except np.linalg.LinAlgError:
+            L = np.zeros((act.sum(), 3, 3))
+            ok = np.zeros(act.sum(), bool)
+            for j, Aj in enumerate(A[act]):
+                try:
+                    L[j] = np.linalg.cholesky(Aj)
+                    ok[j] = True
+                except np.linalg.LinAlgError:
+                    pass
+        ia = np.nonzero(act)[0]
+        dx = np.zeros((n_pts, 3))
+        y = np.linalg.solve(np.where(ok[:, None, None], L, np.eye(3)), -g[ia][..., None])
+        step = np.linalg.solve(np.swapaxes(np.where(ok[:, None, None], L, np.eye(3)), 1, 2), y)[..., 0]
+        dx[ia] = np.where(ok[:, None], step, 0.0)
+        xn = x + dx
+        Fn = np.where(act, cost(np.where(act[:, None], xn, x)), F)
+        nfev += act
+        iters += act
+        accept = act & np.zeros(n_pts, bool)
+        accept[ia] = ok & (Fn[ia] < F[ia])
+        reject = act & ~accept
+        small = np.linalg.norm(dx, axis=1) <= xtol * (xtol + np.linalg.norm(x, axis=1))
+        ftol_hit = accept & ((F - Fn) <= ftol * F)
+        x = np.where(accept[:, None], xn, x)
+        lam = np.where(accept, np.maximum(lam * 0.1, 1e-15), np.where(reject, lam * 10.0, lam))
+        if accept.any():
+            F2, H2, g2 = linearize(x)
+            F = np.where(accept, F2, F)
+            H = np.where(accept[:, None, None], H2, H)
+            g = np.where(accept[:, None], g2, g)
+        status[accept & ftol_hit] = FTOL
+        status[accept & ~ftol_hit & small] = XTOL
+        status[reject & small] = XTOL
+        status[reject & ~small & (lam > 1e16)] = STALLED
+    status[status == RUNNING] = MAXITER
+    if return_info:
+        return x, dict(status=status, iters=iters, nfev=nfev, cost_before=cost_before, cost_after=F)
+    return x
+
+
+def bundle_adjust_points_only(points_2d, points_3d, point_3d_indices, camera_indices, k_arr, d_arr, r_arr,
+                              t_arr, project_func=None, f_scale=50):
+    """Oracle with the reference signature/return of `src/lib/sba.py:181`."""
+    n_points = len(points_3d)
+    x0 = np.asarray(points_3d, np.float64).ravel()
+    f0 = cost_func_points_only(x0, n_points, point_3d_indices, camera_indices, k_arr, d_arr, r_arr, t_arr,
+                               points_2d)
+    pts = sba_points(points_2d, points_3d, point_3d_indices, camera_indices, k_arr, d_arr, r_arr, t_arr,
+                     f_scale=f_scale)
+    f1 = cost_func_points_only(pts.ravel(), n_points, point_3d_indices, camera_indices, k_arr, d_arr, r_arr,
+                               t_arr, points_2d)
+    return pts, dict(before=f0, after=f1)

@@ -1,0 +1,197 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE code.
+
+Runs in the build container only (the reference is not on the GPU box). The
+reference's own `src/lib/sba.py`, `src/lib/utils.py`, `src/lib/calib.py`,
+`src/lib/metric.py` and `src/lib/misc.py` are imported from /root/reference/src;
+the four OpenCV calls go through `_cv2shim` (cv2 is not installed).
+
+Inputs come from the build's seeded synthetic generator (`acinoset_amd.synth`).
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_SRC = os.environ.get('ACINOSET_REF_SRC', '/root/reference/src')
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+import _cv2shim  # noqa: E402
+
+_cv2shim.install()
+sys.path.insert(0, REF_SRC)
+
+from lib import misc as ref_misc      # noqa: E402  (reference)
+from lib import sba as ref_sba        # noqa: E402
+from lib import utils as ref_utils    # noqa: E402
+from lib import calib as ref_calib    # noqa: E402
+from lib import metric as ref_metric  # noqa: E402
+
+from acinoset_amd import synth        # noqa: E402
+
+
+def _df_arrays(df, markers):
+    mi = {m: i for i, m in enumerate(markers)}
+    return dict(df_frame=df['frame'].to_numpy(np.int64), df_camera=df['camera'].to_numpy(np.int64),
+                df_marker=np.array([mi[m] for m in df['marker']], np.int64),
+                df_x=df['x'].to_numpy(np.float64), df_y=df['y'].to_numpy(np.float64),
+                df_likelihood=df['likelihood'].to_numpy(np.float64))
+
+
+def sba_fixture(name, n_frames, cams, thresh=0.5, seed=0):
+    scene = synth.load_scene_file().subset(cams)
+    seq = synth.make_sequence(n_frames, scene, mode='default_nolure', seed=seed)
+    df = seq.to_df()
+    df = df.query(f'likelihood > {thresh}')                    # src/core/sba.py:41
+    df = df[df['frame'].between(0, n_frames - 1)].reset_index(drop=True)
+    scene_path = os.path.join('/tmp', f'golden_{name}_scene.json')
+    scene.to_json(scene_path)
+
+    captured = {}
+    orig = ref_sba.bundle_adjust_points_only
+
+    def spy(points_2d, points_3d, point_3d_indices, camera_indices, *a, **k):
+        captured.update(points_2d=np.array(points_2d, np.float64), points_3d=np.array(points_3d, np.float64),
+                        point_indices=np.array(point_3d_indices, np.int64),
+                        camera_indices=np.array(camera_indices, np.int64))
+        return orig(points_2d, points_3d, point_3d_indices, camera_indices, *a, **k)
+
+    ref_sba.bundle_adjust_points_only = spy
+    t0 = time.time()
+    try:
+        pts_df, res = ref_sba._sba_points(scene_path, df, ref_calib.triangulate_points_fisheye,
+                                          ref_calib.project_points_fisheye)
+    finally:
+        ref_sba.bundle_adjust_points_only = orig
+    dt = time.time() - t0
+    markers = seq.markers
+    mi = {m: i for i, m in enumerate(markers)}
+    out = dict(K=scene.K, D=scene.D, R=scene.R, t=scene.t, res=np.array(scene.res),
+               thresh=thresh, n_frames=n_frames, ref_seconds=dt, **_df_arrays(df, markers),
+               pts_frame=pts_df['frame'].to_numpy(np.int64),
+               pts_marker=np.array([mi[m] for m in pts_df['marker']], np.int64),
+               pts_out=pts_df[['x', 'y', 'z']].to_numpy(np.float64),
+               resid_before=np.asarray(res['before'], np.float64),
+               resid_after=np.asarray(res['after'], np.float64), **captured)
+    # parity metric: src/lib/metric.py:36 on the SBA output (cast to float)
+    camera_params = (scene.K, scene.D, scene.R, scene.t, scene.res, len(cams))
+    err = ref_metric.residual_error(df, pts_df, markers, camera_params)
+    allres = []
+    for c in range(len(cams)):
+        e = err[str(c)]
+        if e is not None and len(e):
+            allres.append(e['pixel_residual'].astype(float).to_numpy())
+    out['metric_pixel_residual'] = np.concatenate(allres) if allres else np.zeros(0)
+    np.savez_compressed(os.path.join(HERE, f'{name}.npz'), **out)
+    print(f'{name}: {len(out["points_2d"])} obs, {len(out["points_3d"])} pts, ref solve {dt:.2f}s')
+
+
+def triangulation_fixture():
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(8, scene, mode='default_nolure', seed=11)
+    df = seq.to_df().query('likelihood > 0.5').reset_index(drop=True)
+    pts = ref_utils.get_pairwise_3d_points_from_df(df, scene.K, scene.D.reshape((-1, 4)), scene.R, scene.t,
+                                                   ref_calib.triangulate_points_fisheye, verbose=False)
+    mi = {m: i for i, m in enumerate(seq.markers)}
+    # single-pair triangulation and undistortion samples
+    a = df[df['camera'] == 0]
+    b = df[df['camera'] == 1]
+    j = a.merge(b, on=['frame', 'marker'], suffixes=('_a', '_b'))
+    pa = j[['x_a', 'y_a']].to_numpy(np.float64)
+    pb = j[['x_b', 'y_b']].to_numpy(np.float64)
+    tri01 = ref_calib.triangulate_points_fisheye(pa, pb, scene.K[0], scene.D[0], scene.R[0], scene.t[0],
+                                                 scene.K[1], scene.D[1], scene.R[1], scene.t[1])
+    np.savez_compressed(os.path.join(HERE, 'triangulation.npz'), K=scene.K, D=scene.D, R=scene.R, t=scene.t,
+                        **_df_arrays(df, seq.markers),
+                        out_frame=pts['frame'].to_numpy(np.int64),
+                        out_marker=np.array([mi[m] for m in pts['marker']], np.int64),
+                        out_xyz=pts[['x', 'y', 'z']].to_numpy(np.float64),
+                        pair_a=pa, pair_b=pb, pair_xyz=np.asarray(tri01, np.float64))
+    print('triangulation:', len(pts), 'points')
+
+
+def fk_fixture():
+    rng = np.random.default_rng(123)
+    out = {}
+    for mode in ('default', 'head', 'upper_body', 'head_stabilize'):
+        P = len(ref_misc.get_pose_params(mode))
+        n = 16
+        x = rng.normal(0, 0.4, (n, P))
+        x[:, :3] += [1.9, 6.4, 0.6]
+        dx = rng.normal(0, 2.0, (n, P))
+        ddx = rng.normal(0, 20.0, (n, P))
+        tau = rng.uniform(-0.01, 0.01, n)
+        for inter in ('pos', 'vel', 'acc'):
+            for dirs in (False, True):
+                if mode != 'default' and dirs is False and inter != 'pos':
+                    pass
+                res = np.array([ref_misc.get_3d_marker_coords({'x': x[i], 'dx': dx[i], 'ddx': ddx[i]}, tau[i],
+                                                              directions=dirs, mode=mode, intermode=inter)
+                                for i in range(n)], np.float64)
+                out[f'{mode}_{inter}_{int(dirs)}'] = res
+        out[f'{mode}_x'] = x
+        out[f'{mode}_dx'] = dx
+        out[f'{mode}_ddx'] = ddx
+        out[f'{mode}_tau'] = tau
+    np.savez_compressed(os.path.join(HERE, 'fk.npz'), **out)
+    print('fk: done')
+
+
+def loss_fixture():
+    e = np.concatenate([np.linspace(-30, 30, 1201), np.array([0.0, 1e-6, -1e-6, 0.0589, 2.9999, 3.0, 10.0, 20.0, 25.0])])
+    v = np.array([ref_misc.redescending_loss(x, 3, 10, 20) for x in e], np.float64)
+    np.savez_compressed(os.path.join(HERE, 'loss.npz'), err=e, loss=v, a=3.0, b=10.0, c=20.0)
+    print('loss: done')
+
+
+def extrinsics_fixture(n_frames=4):
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(n_frames, scene, mode='default_nolure', seed=21, outliers=0.0)
+    df = seq.to_df().query('likelihood > 0.5').reset_index(drop=True)
+    pts3 = ref_utils.get_pairwise_3d_points_from_df(df, scene.K, scene.D.reshape((-1, 4)), scene.R, scene.t,
+                                                    ref_calib.triangulate_points_fisheye, verbose=False)
+    pts3['point_index'] = pts3.index
+    m = df.merge(pts3, how='inner', on=['frame', 'marker'], suffixes=('_cam', ''))
+    p2 = m[['x_cam', 'y_cam']].to_numpy(np.float64)
+    pi = m['point_index'].to_numpy(np.int64)
+    ci = m['camera'].to_numpy(np.int64)
+    p3 = pts3[['x', 'y', 'z']].to_numpy(np.float64)
+    # perturb the extrinsics a little so there is something to adjust
+    rng = np.random.default_rng(5)
+    R = scene.R.copy()
+    t = scene.t.copy()
+    for c in range(1, len(R)):
+        rv = _cv2shim._rodrigues(R[c])[0].ravel() + rng.normal(0, 2e-3, 3)
+        R[c] = _cv2shim._rodrigues(rv)[0]
+        t[c] = t[c] + rng.normal(0, 5e-3, (3, 1))
+    t0 = time.time()
+    obj, r_out, t_out, res = ref_sba.bundle_adjust_points_and_extrinsics(
+        p2, p3, pi, ci, scene.K, scene.D, R, t, ref_calib.project_points_fisheye)
+    dt = time.time() - t0
+    np.savez_compressed(os.path.join(HERE, 'sba_extrinsics.npz'), K=scene.K, D=scene.D, R0=R, t0=t,
+                        points_2d=p2, points_3d=p3, point_indices=pi, camera_indices=ci,
+                        obj_out=np.asarray(obj), R_out=np.asarray(r_out), t_out=np.asarray(t_out),
+                        resid_before=np.asarray(res['before']), resid_after=np.asarray(res['after']),
+                        ref_seconds=dt)
+    print(f'extrinsics: {len(p2)} obs, {len(p3)} pts, ref {dt:.1f}s')
+
+
+if __name__ == '__main__':
+    which = sys.argv[1:] or ['loss', 'fk', 'tri', 'cfg1', 'cfg2', 'ext']
+    if 'loss' in which:
+        loss_fixture()
+    if 'fk' in which:
+        fk_fixture()
+    if 'tri' in which:
+        triangulation_fixture()
+    if 'cfg1' in which:
+        sba_fixture('sba_cfg1', 10, [0, 1])
+    if 'cfg2' in which:
+        sba_fixture('sba_cfg2', 100, list(range(6)))
+    if 'ext' in which:
+        extrinsics_fixture()

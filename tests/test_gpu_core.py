@@ -1,0 +1,134 @@
+"""GPU parity: projection, residual vector, loss, FK and points-only SBA through the
+C ABI, against the oracle and the reference's golden vectors.
+
+Tolerances (float64 on both sides):
+  * projection / residuals: 1e-9 px; loss: 1e-12; FK: 1e-12 m; FK Jacobian: 1e-10
+  * SBA points vs oracle: 1e-9 m max (same LM spec, same minimiser)
+  * SBA points vs reference (scipy TRF, stops at xtol=1e-8): 1e-5 m max, 1e-6 m RMS
+    (north_star contract: 1e-4 m RMS)
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import fisheye, kinematics as okin, sba as osba
+from acinoset_amd import _native, kinematics as pkin, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _cams(g):
+    return _native.pack_cameras(g['K'], g['D'], g['R'], g['t'])
+
+
+def test_projection_matches_oracle(ctx):
+    g = golden('sba_cfg2')
+    rng = np.random.default_rng(0)
+    X = g['points_3d'] + rng.normal(0, 0.05, g['points_3d'].shape)
+    ci = rng.integers(0, 6, len(X)).astype(np.int32)
+    uv = ctx.project(_cams(g), X, ci)
+    ref = fisheye.project(X, g['K'][ci], g['D'][ci], g['R'][ci], g['t'][ci])
+    np.testing.assert_allclose(uv, ref, rtol=0, atol=1e-9)
+    uvf = ctx.project(_cams(g), X, ci, fte_form=True)
+    reff = fisheye.project(X, g['K'][ci], g['D'][ci], g['R'][ci], g['t'][ci], fte_form=True)
+    np.testing.assert_allclose(uvf, reff, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize('name', ['sba_cfg1', 'sba_cfg2'])
+def test_residuals_match_reference(ctx, name):
+    g = golden(name)
+    r = ctx.sba_residuals(_cams(g), g['points_2d'], g['point_indices'], g['camera_indices'], g['points_3d'])
+    np.testing.assert_allclose(r, g['resid_before'], rtol=0, atol=1e-9)
+
+
+def test_loss_matches_reference(ctx):
+    g = golden('loss')
+    v, d = ctx.redescending_loss(g['err'], 3.0, 10.0, 20.0, deriv=True)
+    np.testing.assert_allclose(v, g['loss'], rtol=1e-13, atol=1e-13)
+    d1, _ = okin.loss_derivs(g['err'])
+    np.testing.assert_allclose(d, d1, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize('mode', ['default', 'head', 'upper_body', 'head_stabilize'])
+@pytest.mark.parametrize('inter', ['pos', 'vel', 'acc'])
+@pytest.mark.parametrize('dirs', [0, 1])
+def test_fk_matches_reference(ctx, mode, inter, dirs):
+    g = golden('fk')
+    t = pkin.build_table(mode)
+    im = {'pos': 0, 'vel': 1, 'acc': 2}[inter]
+    out = ctx.fk(t, g[f'{mode}_x'], g[f'{mode}_dx'], g[f'{mode}_ddx'], g[f'{mode}_tau'], intermode=im,
+                 directions=bool(dirs))
+    np.testing.assert_allclose(out, g[f'{mode}_{inter}_{dirs}'], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize('mode', ['default', 'default_nolure', 'head', 'upper_body', 'head_stabilize'])
+def test_fk_jacobian_matches_complex_step(ctx, mode):
+    t = pkin.build_table(mode)
+    rng = np.random.default_rng(3)
+    x = rng.normal(0, 0.5, (32, t.P))
+    x[:, :3] += [1.9, 6.4, 0.6]
+    pos, J = ctx.fk(t, x, jac=True)
+    np.testing.assert_allclose(pos, okin.marker_positions(mode, x), atol=1e-12)
+    np.testing.assert_allclose(J, okin.marker_jacobian(mode, x), atol=1e-10)
+
+
+@pytest.mark.parametrize('name', ['sba_cfg1', 'sba_cfg2'])
+def test_sba_points_matches_reference_and_oracle(ctx, name):
+    g = golden(name)
+    pts, rb, ra, rep = ctx.sba_points(_cams(g), g['points_2d'], g['point_indices'], g['camera_indices'],
+                                      g['points_3d'])
+    np.testing.assert_allclose(rb, g['resid_before'], rtol=0, atol=1e-9)
+    d_ref = np.linalg.norm(pts - g['pts_out'], axis=1)
+    assert np.sqrt(np.mean(d_ref ** 2)) < 1e-6 and d_ref.max() < 1e-5
+    x_or, info = osba.sba_points(g['points_2d'], g['points_3d'], g['point_indices'], g['camera_indices'],
+                                 g['K'], g['D'], g['R'], g['t'], return_info=True)
+    assert np.abs(pts - x_or).max() < 1e-9
+    np.testing.assert_allclose(ra, g['resid_after'], atol=1e-3)
+    assert rep['n_problems'] == len(pts)
+    assert rep['status_counts']['maxiter'] == 0 and rep['status_counts']['stalled'] == 0
+    np.testing.assert_allclose(rep['cost_before'], info['cost_before'].sum(), rtol=1e-12)
+    np.testing.assert_allclose(rep['cost_after'], info['cost_after'].sum(), rtol=1e-12)
+
+
+def test_sba_dense_matches_oracle_12cam(ctx):
+    scene = synth.ring_scene(12)
+    seq = synth.make_sequence(120, scene, seed=5)
+    uv, mask, pts0, truth, _ = synth.dense_sba_problem(seq)
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    pts, rep = ctx.sba_points_dense(cams, uv, mask, pts0)
+    pi, ci = np.nonzero(mask)
+    x_or = osba.sba_points(uv[pi, ci], pts0, pi, ci, scene.K, scene.D, scene.R, scene.t)
+    assert np.abs(pts - x_or).max() < 1e-9
+    assert np.sqrt(np.mean(np.sum((pts - truth) ** 2, 1))) < 0.01  # 1 px noise at ~6 m
+    # the list API on the same problem (compacted slots, different lane order)
+    pts2, _, _, _ = ctx.sba_points(cams, uv[pi, ci], pi, ci, pts0, residuals=False)
+    assert np.abs(pts - pts2).max() < 1e-9
+
+
+def test_sba_deterministic(ctx):
+    g = golden('sba_cfg2')
+    a = ctx.sba_points(_cams(g), g['points_2d'], g['point_indices'], g['camera_indices'], g['points_3d'])
+    b = ctx.sba_points(_cams(g), g['points_2d'], g['point_indices'], g['camera_indices'], g['points_3d'])
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2])
+
+
+def test_sba_edge_cases(ctx):
+    g = golden('sba_cfg1')
+    cams = _cams(g)
+    # empty observation list
+    pts, rb, ra, rep = ctx.sba_points(cams, np.zeros((0, 2)), np.zeros(0, np.int32), np.zeros(0, np.int32),
+                                      g['points_3d'])
+    assert np.array_equal(pts, g['points_3d'])
+    # a point with no observations keeps its value; a duplicated observation is allowed
+    p2 = np.concatenate([g['points_2d'], g['points_2d'][:1]])
+    pi = np.concatenate([g['point_indices'], g['point_indices'][:1]])
+    ci = np.concatenate([g['camera_indices'], g['camera_indices'][:1]])
+    p3 = np.concatenate([g['points_3d'], [[1.0, 2.0, 3.0]]])
+    pts, rb, ra, rep = ctx.sba_points(cams, p2, pi, ci, p3)
+    assert np.array_equal(pts[-1], [1.0, 2.0, 3.0])
+    assert rep['status_counts']['noobs'] == 1
+    x_or = osba.sba_points(p2, p3, pi, ci, g['K'], g['D'], g['R'], g['t'])
+    assert np.abs(pts - x_or).max() < 1e-9
+    # out-of-range point index -> error, not a crash
+    with pytest.raises(RuntimeError):
+        ctx.sba_points(cams, g['points_2d'], g['point_indices'] + 10 ** 6, g['camera_indices'], g['points_3d'])

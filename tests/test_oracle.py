@@ -1,0 +1,124 @@
+"""CPU: pin the oracle (and the product's skeleton tables) to the reference's own
+outputs captured in tests/golden/ (see tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import fisheye, kinematics as okin, sba as osba
+from acinoset_amd import kinematics as pkin
+
+
+def _shift(g, mode, inter):
+    dx, ddx, tau = g[f'{mode}_dx'], g[f'{mode}_ddx'], g[f'{mode}_tau']
+    if inter == 'pos':
+        return None
+    s = dx[:, :3] * tau[:, None]
+    if inter == 'acc':
+        s = s + ddx[:, :3] * (tau ** 2)[:, None]
+    return s
+
+
+@pytest.mark.parametrize('mode', ['default', 'head', 'upper_body', 'head_stabilize'])
+@pytest.mark.parametrize('inter', ['pos', 'vel', 'acc'])
+@pytest.mark.parametrize('dirs', [0, 1])
+def test_oracle_fk_matches_reference(mode, inter, dirs):
+    g = golden('fk')
+    ref = g[f'{mode}_{inter}_{dirs}']
+    out = okin.marker_positions(mode, g[f'{mode}_x'], _shift(g, mode, inter), directions=bool(dirs))
+    if mode == 'default':
+        # the reference never shifts the lure (src/lib/misc.py:222)
+        out[:, 20] = g['default_x'][:, 26:29]
+    np.testing.assert_allclose(out, ref, rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize('mode', ['default', 'head', 'upper_body', 'head_stabilize'])
+@pytest.mark.parametrize('inter', ['pos', 'vel', 'acc'])
+def test_table_fk_matches_reference(mode, inter):
+    """The product's skeleton *table* (what the HIP kernel evaluates) reproduces the
+    reference FK (host evaluation of the table)."""
+    g = golden('fk')
+    ref = g[f'{mode}_{inter}_1']
+    out = pkin.fk_numpy(mode, g[f'{mode}_x'], _shift(g, mode, inter), directions=True)
+    np.testing.assert_allclose(out, ref, rtol=0, atol=1e-12)
+
+
+def test_table_jacobian_structure_matches_complex_step():
+    """Host check of the analytic-Jacobian tables (deriv mask) against complex step."""
+    rng = np.random.default_rng(0)
+    for mode in ('default', 'default_nolure', 'head', 'upper_body', 'head_stabilize'):
+        t = pkin.build_table(mode)
+        x = rng.normal(0, 0.4, (3, t.P))
+        J = okin.marker_jacobian(mode, x)                 # (n, L, 3, P)
+        nz = (np.abs(J) > 1e-14).any(axis=(0, 2))           # (L, P)
+        K = t.n_nodes
+        deriv = t.ints[-K * t.P:].reshape(K, t.P)
+        J_ = t.n_joints
+        off = pkin.INT_HDR + 9 * J_ + 4 * K
+        outn = t.ints[off:off + t.L]
+        assert np.all(deriv[outn].astype(bool) >= nz), mode  # mask covers every true dependency
+
+
+def test_loss_matches_reference():
+    g = golden('loss')
+    np.testing.assert_allclose(okin.redescending_loss(g['err']), g['loss'], rtol=1e-14, atol=1e-14)
+
+
+def test_loss_derivatives_fd():
+    e = np.concatenate([np.linspace(-25, -0.01, 400), np.linspace(0.01, 25, 400)])
+    h = 1e-6
+    d1, d2 = okin.loss_derivs(e)
+    fd1 = (okin.redescending_loss(e + h) - okin.redescending_loss(e - h)) / (2 * h)
+    fd2 = (okin.loss_derivs(e + h)[0] - okin.loss_derivs(e - h)[0]) / (2 * h)
+    np.testing.assert_allclose(d1, fd1, atol=1e-7)
+    np.testing.assert_allclose(d2, fd2, atol=1e-6)
+
+
+def test_projection_jacobian_fd():
+    g = golden('sba_cfg2')
+    rng = np.random.default_rng(1)
+    X = g['points_3d'][:50] + rng.normal(0, 0.1, (50, 3))
+    ci = rng.integers(0, 6, 50)
+    uv, J = fisheye.project_jac(X, g['K'][ci], g['D'][ci], g['R'][ci], g['t'][ci])
+    np.testing.assert_allclose(uv, fisheye.project(X, g['K'][ci], g['D'][ci], g['R'][ci], g['t'][ci]), atol=1e-9)
+    h = 1e-6
+    for k in range(3):
+        e = np.zeros(3)
+        e[k] = h
+        fd = (fisheye.project(X + e, g['K'][ci], g['D'][ci], g['R'][ci], g['t'][ci])
+              - fisheye.project(X - e, g['K'][ci], g['D'][ci], g['R'][ci], g['t'][ci])) / (2 * h)
+        np.testing.assert_allclose(J[..., k], fd, rtol=1e-6, atol=1e-4)
+
+
+@pytest.mark.parametrize('name', ['sba_cfg1', 'sba_cfg2'])
+def test_oracle_sba_matches_reference(name):
+    g = golden(name)
+    n = len(g['points_3d'])
+    # residuals['before'] (reference cost function at the reference init)
+    f0 = osba.cost_func_points_only(g['points_3d'].ravel(), n, g['point_indices'], g['camera_indices'],
+                                    g['K'], g['D'], g['R'], g['t'], g['points_2d'])
+    np.testing.assert_allclose(f0, g['resid_before'], rtol=0, atol=1e-9)
+    x, info = osba.sba_points(g['points_2d'], g['points_3d'], g['point_indices'], g['camera_indices'],
+                              g['K'], g['D'], g['R'], g['t'], return_info=True)
+    d = np.linalg.norm(x - g['pts_out'], axis=1)
+    # scipy stops on xtol=1e-8 (relative); the oracle converges tighter. Contract: 1e-4 m RMS.
+    assert np.sqrt(np.mean(d ** 2)) < 1e-6 and d.max() < 1e-5
+    assert np.all(info['cost_after'] <= info['cost_before'] + 1e-9)
+    f1 = osba.cost_func_points_only(x.ravel(), n, g['point_indices'], g['camera_indices'],
+                                    g['K'], g['D'], g['R'], g['t'], g['points_2d'])
+    np.testing.assert_allclose(f1, g['resid_after'], atol=1e-3)
+    # robust cost no larger than the reference's
+    c_ref = 0.5 * 2500 * np.log1p(g['resid_after'] ** 2 / 2500).sum()
+    assert 0.5 * 2500 * np.log1p(f1 ** 2 / 2500).sum() <= c_ref + 1e-9
+
+
+def test_oracle_triangulation_matches_reference():
+    g = golden('triangulation')
+    X = fisheye.triangulate_pair(g['pair_a'], g['pair_b'], g['K'][0], g['D'][0], g['R'][0], g['t'][0],
+                                 g['K'][1], g['D'][1], g['R'][1], g['t'][1])
+    np.testing.assert_allclose(X, g['pair_xyz'], atol=1e-9)
+    fr, mk, xyz = fisheye.pairwise_points(g['df_frame'], g['df_camera'], g['df_marker'], g['df_x'], g['df_y'],
+                                          g['K'], g['D'], g['R'], g['t'])
+    ref = {(f, m): p for f, m, p in zip(g['out_frame'], g['out_marker'], g['out_xyz'])}
+    assert len(ref) == len(fr)
+    for f, m, p in zip(fr, mk, xyz):
+        np.testing.assert_allclose(p, ref[(f, m)], atol=1e-9)
