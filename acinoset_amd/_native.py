@@ -33,7 +33,7 @@ SYMBOLS = (
     'acs_ctx_create', 'acs_ctx_destroy', 'acs_last_error', 'acs_ctx_set_stream', 'acs_ctx_sync',
     'acs_abi_version', 'acs_device_count', 'acs_sba_default_opts', 'acs_project_fisheye',
     'acs_sba_residuals', 'acs_sba_points', 'acs_sba_points_dense', 'acs_redescending_loss', 'acs_fk',
-    'acs_fte_default_opts', 'acs_fte_solve', 'acs_fte_eval', 'acs_triangulate_pairs',
+    'acs_fte_default_opts', 'acs_fte_solve', 'acs_fte_eval',
 )
 
 
@@ -65,12 +65,14 @@ class FteOpts(C.Structure):
 
 
 class FteReport(C.Structure):
-    _fields_ = [('status', C.c_int32), ('iters', C.c_int32), ('n_accepted', C.c_int32), ('reserved', C.c_int32),
+    _fields_ = [('status', C.c_int32), ('iters', C.c_int32), ('n_accepted', C.c_int32), ('n_bad_pivots', C.c_int32),
                 ('cost_before', C.c_double), ('cost_after', C.c_double), ('cost_meas', C.c_double),
                 ('cost_model', C.c_double), ('grad_max', C.c_double), ('lambda_final', C.c_double)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != 'reserved'}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d['status_name'] = STATUS_NAMES[self.status] if 0 <= self.status < 7 else str(self.status)
+        return d
 
 
 _lib = None
@@ -287,6 +289,54 @@ class Context:
                                    _ptr(ddx), _ptr(tau), n, int(intermode), int(bool(directions)), _ptr(out),
                                    _ptr(J), 0), 'acs_fk')
         return (out, J) if jac else out
+
+    # ---- a10-a13: FTE ------------------------------------------------------------------
+    def fte_default_opts(self, **kw):
+        o = FteOpts()
+        self.lib.acs_fte_default_opts(C.byref(o))
+        for k, v in kw.items():
+            setattr(o, k, v)
+        return o
+
+    def _fte_args(self, table, cams, meas, w, Ts, qinv, shutter_delay, intermode):
+        cams = _c64(cams)
+        N, Cn, L, _ = np.shape(meas)
+        assert L == table.L and Cn == len(cams), (np.shape(meas), table.L, len(cams))
+        meas = _c64(np.nan_to_num(meas))
+        w = _c64(w).reshape(N, Cn, L)
+        qinv = _c64(qinv).reshape(table.P)
+        ints = np.ascontiguousarray(table.ints, np.int32)
+        reals = np.ascontiguousarray(table.reals, np.float64)
+        return ints, reals, cams, meas, w, qinv, N, Cn
+
+    def fte_solve(self, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutter_delay=True, intermode=1,
+                  opts=None):
+        ints, reals, cams, meas, w, qinv, N, Cn = self._fte_args(table, cams, meas, w, Ts, qinv, shutter_delay,
+                                                                 intermode)
+        X = _c64(X0).reshape(N + 2, table.P).copy()
+        tau = np.zeros(Cn) if tau0 is None else _c64(tau0).copy()
+        rep = FteReport()
+        opts = opts or self.fte_default_opts()
+        self.check(self.lib.acs_fte_solve(self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), _ptr(cams), Cn,
+                                          _ptr(meas), _ptr(w), N, int(bool(shutter_delay)), float(Ts), _ptr(qinv), 0,
+                                          int(intermode), _ptr(X), _ptr(tau), C.byref(opts), C.byref(rep), 0),
+                   'acs_fte_solve')
+        return X, tau, rep.as_dict()
+
+    def fte_eval(self, table, cams, meas, w, Ts, qinv, X, tau=None, shutter_delay=True, intermode=1, hessian=True):
+        ints, reals, cams, meas, w, qinv, N, Cn = self._fte_args(table, cams, meas, w, Ts, qinv, shutter_delay,
+                                                                 intermode)
+        X = _c64(X).reshape(N + 2, table.P)
+        tau = np.zeros(Cn) if tau is None else _c64(tau)
+        nv = (N + 2) * table.P + (Cn if shutter_delay else 0)
+        cost = np.empty(3)
+        grad = np.empty(nv)
+        H = np.empty((nv, nv)) if hessian else None
+        self.check(self.lib.acs_fte_eval(self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), _ptr(cams), Cn,
+                                         _ptr(meas), _ptr(w), N, int(bool(shutter_delay)), float(Ts), _ptr(qinv), 0,
+                                         int(intermode), _ptr(X), _ptr(tau), _ptr(cost), _ptr(grad), _ptr(H), 0),
+                   'acs_fte_eval')
+        return cost, grad, H
 
 
 _default_ctx = None

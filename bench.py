@@ -54,7 +54,9 @@ def main():
         dist.init_process_group('gloo')
     torch.cuda.set_device(local)
     ctx = _native.Context(local)
-    stream = torch.cuda.current_stream()
+    # one explicit (non-null) stream carries the copies, the kernels and the timing events
+    stream = torch.cuda.Stream(device=local)
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
     # ---- workload: rank-local frame shard of a synthetic sequence --------------------

@@ -129,6 +129,48 @@ int acs_fk(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double*
            int64_t n, int32_t intermode, int32_t directions, double* out, double* jac,
            uint32_t flags);
 
+/* ---- a10-a13: FTE trajectory solve (src/core/fte.py:176-555) ------------------------
+ * Unknowns: X ((n_frames + 2) x P, row f = frame f - 2; rows 0, 1 are the virtual frames
+ * carrying the reference's free dx[1], ddx[1]) and tau (n_cams; tau[0] pinned to 0,
+ * |tau| <= Ts, only when shutter_delay). meas (n_frames, n_cams, L, 2) pixels,
+ * w (n_frames, n_cams, L) = 1/R where likelihood > thresh else 0 (fte.py:210-215),
+ * qinv (P) = 1/Q_p = 1/_Q[p]^2 (fte.py:113-144, 217-218). intermode 0 pos / 1 vel / 2 acc
+ * (shutter_delay requires vel/acc, fte.py:44-48); sd_mode 0 = 'const' (1 'variable' is
+ * not implemented yet and returns ACS_E_INVALID). X and tau are in/out.                */
+typedef struct {
+  int32_t max_iters;  /* LM iterations; default 200 */
+  int32_t window;     /* frames per window interior of the banded solve (>= 3); default 24 */
+  double ftol;        /* relative cost decrease (|F|); default 1e-12 */
+  double xtol;        /* relative step; default 1e-12 */
+  double gtol;        /* max |gradient|; default 1e-8 */
+  double lambda0;     /* initial LM damping; default 1e-3 */
+  double redesc_a, redesc_b, redesc_c;  /* redescending loss knots; 3, 10, 20 (fte.py:53-55) */
+} acs_fte_opts;
+
+typedef struct {
+  int32_t status;      /* ACS_STATUS_* */
+  int32_t iters;       /* LM iterations (accepted + rejected) */
+  int32_t n_accepted;
+  int32_t n_bad_pivots;
+  double cost_before, cost_after, cost_meas, cost_model;
+  double grad_max, lambda_final;
+} acs_fte_report;
+
+void acs_fte_default_opts(acs_fte_opts* o);
+int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
+                  int64_t n_reals, const double* cams, int32_t n_cams, const double* meas,
+                  const double* w, int32_t n_frames, int32_t shutter_delay, double Ts,
+                  const double* qinv, int32_t sd_mode, int32_t intermode, double* X, double* tau,
+                  const acs_fte_opts* opts, acs_fte_report* report, uint32_t flags);
+/* objective (cost3 = [total, measurement, model]), gradient (nv = (n_frames+2)*P + C if
+ * shutter_delay) and the dense undamped GN normal matrix (nv x nv, may be NULL) at
+ * (X, tau): the linearisation acs_fte_solve uses, exported for parity tests. Host ptrs. */
+int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
+                 int64_t n_reals, const double* cams, int32_t n_cams, const double* meas,
+                 const double* w, int32_t n_frames, int32_t shutter_delay, double Ts,
+                 const double* qinv, int32_t sd_mode, int32_t intermode, const double* X,
+                 const double* tau, double* cost3, double* grad, double* H, uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,107 @@
+"""GPU parity of the FTE trajectory solve (acs_fte_eval / acs_fte_solve) against the
+oracle restatement of src/core/fte.py (parity unpinned vs IPOPT: see oracle/fte.py).
+
+Tolerances (float64):
+  * objective: 1e-10 relative; gradient / GN normal matrix: 1e-8 relative to their max
+  * solution vs oracle (same LM spec): 1e-6 m RMS keypoint position (contract 1e-4 m),
+    reprojection RMS within 1e-3 px (north_star), tau within 1e-6 s
+  * window partition: any window size gives the same step (exact substructuring), 1e-8
+"""
+import numpy as np
+import pytest
+
+from oracle import fte as ofte, kinematics as okin
+from acinoset_amd import _native, kinematics as pkin, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(N, mode='default_nolure', sd=True, inter='vel', seed=2, tau_max=0.004):
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(N, scene, mode=mode, seed=seed, tau_max=tau_max if sd else 0.0)
+    w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
+    prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter)
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    return seq, prob, cams
+
+
+def _reproj_rms(prob, X, tau):
+    e = prob.residuals(X, tau) * 3.0            # back to pixels (w = 1/3)
+    m = prob.w > 0
+    return float(np.sqrt(np.mean(np.sum(e[m] ** 2, -1))))
+
+
+@pytest.mark.parametrize('sd,inter', [(False, 'pos'), (True, 'vel'), (True, 'acc')])
+def test_fte_eval_matches_oracle(ctx, sd, inter):
+    seq, prob, cams = _problem(12, sd=sd, inter=inter)
+    rng = np.random.default_rng(4)
+    X = np.concatenate([seq.x[:1], seq.x[:1], seq.x], 0) + rng.normal(0, 0.01, (prob.M, prob.P))
+    tau = np.array([0.0, 0.002, -0.001, 0.003, 0.0, -0.002]) if sd else np.zeros(6)
+    table = pkin.build_table(prob.mode)
+    cost, g, H = ctx.fte_eval(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X, tau, shutter_delay=sd,
+                              intermode=prob.im)
+    F = prob.cost(X, tau)
+    np.testing.assert_allclose(cost, F, rtol=1e-10)
+    Fo, Ho, go = prob.linearize(X, tau)
+    go = go.copy()
+    if sd:
+        go[prob.M * prob.P] = 0.0
+    np.testing.assert_allclose(g, go, rtol=0, atol=1e-8 * np.abs(go).max())
+    Hd = Ho.toarray()
+    np.testing.assert_allclose(H, Hd, rtol=0, atol=1e-8 * np.abs(Hd).max())
+
+
+@pytest.mark.parametrize('mode,sd,inter,N', [('default_nolure', True, 'vel', 40), ('head', True, 'vel', 60),
+                                             ('default_nolure', False, 'pos', 30),
+                                             ('default_nolure', True, 'acc', 30)])
+def test_fte_solve_matches_oracle(ctx, mode, sd, inter, N):
+    seq, prob, cams = _problem(N, mode=mode, sd=sd, inter=inter)
+    nose = seq.pos3d[:, 0, 0]
+    X0 = ofte.initial_state(prob, np.arange(N), nose)
+    Xo, to, info = ofte.solve(prob, X0)
+    table = pkin.build_table(mode)
+    X, tau, rep = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, shutter_delay=sd,
+                                intermode=prob.im)
+    assert rep['status_name'] in ('ftol', 'xtol', 'gtol'), rep
+    assert info['status'] in ('ftol', 'xtol', 'gtol'), info
+    pg = okin.marker_positions(mode, X[2:])
+    po = okin.marker_positions(mode, Xo[2:])
+    rms = float(np.sqrt(np.mean(np.sum((pg - po) ** 2, -1))))
+    assert rms < 1e-6, (rms, rep, info)
+    assert abs(_reproj_rms(prob, X, tau) - _reproj_rms(prob, Xo, to)) < 1e-3
+    np.testing.assert_allclose(tau, to, atol=1e-6)
+    np.testing.assert_allclose(rep['cost_after'], info['cost_after'], rtol=1e-9, atol=1e-9)
+    # and the solve actually fits the data: keypoints within a few mm of the truth
+    truth = seq.pos3d[:, 0]
+    assert float(np.sqrt(np.mean(np.sum((pg - truth) ** 2, -1)))) < 0.02
+
+
+def test_fte_window_partition_is_exact(ctx):
+    seq, prob, cams = _problem(50)
+    X0 = ofte.initial_state(prob, np.arange(50), seq.pos3d[:, 0, 0])
+    table = pkin.build_table(prob.mode)
+    outs = []
+    for wl in (3, 7, 1000):
+        opts = ctx.fte_default_opts(window=wl, max_iters=6)
+        outs.append(ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, opts=opts))
+    for X, tau, rep in outs[:-1]:
+        assert rep['n_bad_pivots'] == 0
+        np.testing.assert_allclose(X, outs[-1][0], rtol=0, atol=1e-8)
+        np.testing.assert_allclose(tau, outs[-1][1], rtol=0, atol=1e-10)
+
+
+def test_fte_deterministic(ctx):
+    seq, prob, cams = _problem(30)
+    X0 = ofte.initial_state(prob, np.arange(30), seq.pos3d[:, 0, 0])
+    table = pkin.build_table(prob.mode)
+    a = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0)
+    b = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_fte_rejects_bad_modes(ctx):
+    seq, prob, cams = _problem(8)
+    table = pkin.build_table(prob.mode)
+    X0 = np.zeros((prob.M, prob.P))
+    with pytest.raises(RuntimeError):   # shutter delay with intermode 'pos' (fte.py:44-46)
+        ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, shutter_delay=True, intermode=0)

@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, bench, rocprofv3 kernel-trace summary.
+# Every GPU step has its own time limit; a fault/abort/timeout ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+REPO=$(pwd)
+OUT=$REPO/gpurun_out
+mkdir -p "$OUT"
+TAG=${TAG:-r01}
+run() {
+  local name=$1 lim=$2; shift 2
+  local t0=$(date +%s)
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc $(( $(date +%s) - t0 ))s"
+  tail -n 5 "$OUT/$name.log"
+  case $rc in 124|137|134|139|143) echo "[$name] fatal rc=$rc, stopping session"; exit $rc;; esac
+  return 0
+}
+STEPS=${STEPS:-all}
+if [[ $STEPS == *all* || $STEPS == *test* ]]; then
+  run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
+fi
+if [[ $STEPS == *all* || $STEPS == *smoke* ]]; then
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [[ $STEPS == *all* || $STEPS == *bench* ]]; then
+  run bench 600 python bench.py ${BENCH_ARGS:-}
+  grep '^{' "$OUT/bench.log" > "$OUT/bench_${TAG}.json" || true
+fi
+if [[ $STEPS == *all* || $STEPS == *prof* ]]; then
+  export TMPDIR=/tmp
+  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_${TAG}" -o run -- python3 "$REPO/bench.py" --no-cpu-baseline --steps 200 --warmup 20 ${BENCH_ARGS:-}
+fi
+echo done
