@@ -33,7 +33,7 @@ SYMBOLS = (
     'acs_ctx_create', 'acs_ctx_destroy', 'acs_last_error', 'acs_ctx_set_stream', 'acs_ctx_sync',
     'acs_abi_version', 'acs_device_count', 'acs_sba_default_opts', 'acs_project_fisheye',
     'acs_sba_residuals', 'acs_sba_points', 'acs_sba_points_dense', 'acs_redescending_loss', 'acs_fk',
-    'acs_fte_default_opts', 'acs_fte_solve', 'acs_fte_eval',
+    'acs_fte_default_opts', 'acs_fte_solve', 'acs_fte_eval', 'acs_triangulate_pairs', 'acs_triangulate_dense',
 )
 
 
@@ -106,6 +106,7 @@ def _declare(lib):
         'acs_fte_eval': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, dbl, _P, i32, i32, _P, _P,
                                    _P, _P, _P, u32]),
         'acs_triangulate_pairs': (C.c_int, [_P, _P, i32, _P, _P, _P, _P, i64, _P, u32]),
+        'acs_triangulate_dense': (C.c_int, [_P, _P, i32, _P, _P, i64, _P, _P, u32]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name):
@@ -323,6 +324,18 @@ class Context:
                    'acs_fte_solve')
         return X, tau, rep.as_dict()
 
+    def fte_solve_dev(self, table_ints_p, n_ints, table_reals_p, n_reals, cams_p, n_cams, meas_p, w_p, N,
+                      shutter_delay, Ts, qinv_p, intermode, X_p, tau_p, opts=None):
+        """Device-pointer variant (all arrays resident in HBM); returns the report."""
+        rep = FteReport()
+        opts = opts or self.fte_default_opts()
+        self.check(self.lib.acs_fte_solve(self.h, C.c_void_p(table_ints_p), n_ints, C.c_void_p(table_reals_p), n_reals,
+                                          C.c_void_p(cams_p), n_cams, C.c_void_p(meas_p), C.c_void_p(w_p), N,
+                                          int(bool(shutter_delay)), float(Ts), C.c_void_p(qinv_p), 0, int(intermode),
+                                          C.c_void_p(X_p), C.c_void_p(tau_p), C.byref(opts), C.byref(rep),
+                                          ACS_DEVICE_PTRS), 'acs_fte_solve')
+        return rep.as_dict()
+
     def fte_eval(self, table, cams, meas, w, Ts, qinv, X, tau=None, shutter_delay=True, intermode=1, hessian=True):
         ints, reals, cams, meas, w, qinv, N, Cn = self._fte_args(table, cams, meas, w, Ts, qinv, shutter_delay,
                                                                  intermode)
@@ -337,6 +350,31 @@ class Context:
                                          int(intermode), _ptr(X), _ptr(tau), _ptr(cost), _ptr(grad), _ptr(H), 0),
                    'acs_fte_eval')
         return cost, grad, H
+
+    # ---- triangulation -------------------------------------------------
+    def triangulate_pairs(self, cams, uv_a, uv_b, cam_a, cam_b):
+        cams = _c64(cams)
+        uv_a = _c64(uv_a).reshape(-1, 2)
+        uv_b = _c64(uv_b).reshape(-1, 2)
+        n = len(uv_a)
+        ca = np.ascontiguousarray(np.broadcast_to(cam_a, (n,)), np.int32)
+        cb = np.ascontiguousarray(np.broadcast_to(cam_b, (n,)), np.int32)
+        out = np.empty((n, 3))
+        self.check(self.lib.acs_triangulate_pairs(self.h, _ptr(cams), len(cams), _ptr(uv_a), _ptr(uv_b), _ptr(ca),
+                                                  _ptr(cb), n, _ptr(out), 0), 'acs_triangulate_pairs')
+        return out
+
+    def triangulate_dense(self, cams, uv, mask):
+        cams = _c64(cams)
+        C_ = len(cams)
+        uv = _c64(np.nan_to_num(uv)).reshape(-1, C_, 2)
+        mask = np.ascontiguousarray(mask, np.uint8).reshape(-1, C_)
+        n = len(uv)
+        out = np.empty((n, 3))
+        cnt = np.empty(n, np.int32)
+        self.check(self.lib.acs_triangulate_dense(self.h, _ptr(cams), C_, _ptr(uv), _ptr(mask), n, _ptr(out),
+                                                  _ptr(cnt), 0), 'acs_triangulate_dense')
+        return out, cnt
 
 
 _default_ctx = None

@@ -1,0 +1,64 @@
+"""Mirror of the SBA / FTE seams of src/lib/app.py: `sba_points_fisheye` (:135-138),
+`save_sba` (:271-295), `save_fte` (:317-332), `start_logging` / `stop_logging` (:337-345).
+Video rendering and plotting (pyqtgraph / OpenCV) are out of scope: the save functions
+write the pickle/.mat outputs and skip the labelled videos."""
+import os
+import sys
+
+import numpy as np
+
+from . import misc, utils
+from .calib import project_points_fisheye, triangulate_points_fisheye
+from .sba import _sba_points
+
+
+def sba_points_fisheye(scene_fpath, points_2d_df):
+    return _sba_points(scene_fpath, points_2d_df, triangulate_points_fisheye, project_points_fisheye)
+
+
+def _gaze_targets(head_pos, nose_pos, r_eye_pos, r=3.0):
+    """`get_gaze_target_from_positions` (src/lib/misc.py:107-119), vectorised."""
+    from scipy.spatial.transform import Rotation
+    out = []
+    for h, n, e in zip(head_pos, nose_pos, r_eye_pos):
+        vn = (n - h) / np.linalg.norm(n - h)
+        ve = (e - h) / np.linalg.norm(e - h)
+        out.append(h + r * Rotation.from_mrp(np.tan(np.pi / 4 / 4) * ve).apply(vn))
+    return np.array(out)
+
+
+def save_sba(positions, out_dir, scene_fpath, markers, start_frame, save_videos=True) -> str:
+    nose, r_eye, l_eye = positions[:, 0, :], positions[:, 1, :], positions[:, 2, :]
+    head = np.mean([r_eye, l_eye], axis=0)
+    with np.errstate(invalid='ignore'):
+        gaze = _gaze_targets(head, nose, r_eye)
+    positions = np.concatenate((positions, head[:, None], gaze[:, None]), axis=1)
+    markers += ['coe', 'gaze_target']
+    out_fpath = os.path.join(out_dir, 'sba.pickle')
+    utils.save_optimised_cheetah(positions, out_fpath, extra_data=dict(start_frame=start_frame))
+    return out_fpath
+
+
+def save_fte(states, mode, out_dir, scene_fpath, start_frame, intermode='pos', directions=True, save_videos=True,
+             n_cam=None) -> str:
+    """fte.pickle = {positions: per-camera (N, L+2, 3) list, x, dx, ddx, [shutter_delay], reprj_errors,
+    start_frame} (+ fte.mat). The reference sizes `positions` by the number of cam*.mp4
+    videos next to out_dir (an empty list without videos); `n_cam` overrides that count."""
+    from glob import glob
+    if n_cam is None:
+        n_cam = len(sorted(glob(os.path.join(os.path.dirname(out_dir), 'cam[1-9].mp4'))))
+    pos = misc.get_all_marker_coords_from_states(states, n_cam, mode=mode, intermode=intermode,
+                                                 directions=directions)
+    out_fpath = os.path.join(out_dir, 'fte.pickle')
+    utils.save_optimised_cheetah(pos, out_fpath, extra_data=dict(**states, start_frame=start_frame))
+    return out_fpath
+
+
+def start_logging(out_fpath):
+    sys.stdout = misc.Logger(out_fpath)
+
+
+def stop_logging():
+    if isinstance(sys.stdout, misc.Logger):
+        sys.stdout.logfile.close()
+        sys.stdout = sys.stdout.terminal

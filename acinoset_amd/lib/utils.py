@@ -1,0 +1,153 @@
+"""Mirror of src/lib/utils.py I/O used on the SBA / FTE path (formats kept: scene JSON,
+DLC long DataFrame, pickle + .mat outputs).
+
+`get_pairwise_3d_points_from_df` (:319-349) triangulates on the GPU. DLC `.h5` input
+needs PyTables (pandas.read_hdf); where it is absent, `load_dlc_points_as_df` raises a
+clear ImportError and `.csv` DLC exports are accepted instead.
+"""
+import json
+import os
+import pickle
+from datetime import datetime
+from errno import ENOENT
+from glob import glob
+
+import numpy as np
+import pandas as pd
+
+from .. import _native
+
+
+def load_scene(fpath, verbose=True):
+    """`src/lib/utils.py:55-74` -> (k_arr (C,3,3), d_arr (C,4,1), r_arr, t_arr (C,3,1), cam_res)."""
+    with open(fpath) as f:
+        data = json.load(f)
+    cam_res = tuple(data['camera_resolution'])
+    k = np.array([c['k'] for c in data['cameras']], dtype=np.float64)
+    d = np.array([c['d'] for c in data['cameras']], dtype=np.float64)
+    r = np.array([c['r'] for c in data['cameras']], dtype=np.float64)
+    t = np.array([c['t'] for c in data['cameras']], dtype=np.float64)
+    if verbose:
+        print(f'Loaded extrinsics from {fpath}\n')
+    return k, d, r, t, cam_res
+
+
+def save_scene(out_fpath, k_arr, d_arr, r_arr, t_arr, cam_res):
+    """`src/lib/utils.py:186-203`."""
+    cams = [{'k': np.asarray(k).tolist(), 'd': np.asarray(d).tolist(), 'r': np.asarray(r).tolist(),
+             't': np.asarray(t).tolist()} for k, d, r, t in zip(k_arr, d_arr, r_arr, t_arr)]
+    with open(out_fpath, 'w') as f:
+        json.dump({'timestamp': str(datetime.now()), 'camera_resolution': cam_res, 'cameras': cams}, f)
+    print(f'Saved extrinsics to {out_fpath}\n')
+
+
+def find_scene_file(dir_path, scene_fname=None, verbose=True):
+    """`src/lib/utils.py:290-310`."""
+    if scene_fname is None:
+        n_cams = len(glob(os.path.join(dir_path, 'cam[1-9].mp4')))
+        scene_fname = f'{n_cams}_cam_scene_sba.json' if n_cams else '[1-9]_cam_scene*.json'
+    if dir_path and dir_path != os.path.join('..', 'data'):
+        scene_fpath = os.path.join(dir_path, 'extrinsic_calib', scene_fname)
+        files = sorted([f for f in glob(scene_fpath) if ('before_corrections' not in f) or (f == scene_fpath)])
+        if files:
+            k, d, r, t, res = load_scene(files[-1], verbose)
+            n_cams = int(os.path.basename(files[-1])[0])
+            return k, d, r, t, res, n_cams, files[-1]
+        return find_scene_file(os.path.dirname(dir_path), scene_fname, verbose)
+    raise FileNotFoundError(ENOENT, os.strerror(ENOENT), os.path.join('extrinsic_calib', scene_fname))
+
+
+def _read_dlc(path):
+    if path.endswith('.csv'):
+        return pd.read_csv(path, header=[0, 1, 2], index_col=0)
+    try:
+        return pd.read_hdf(path)
+    except ImportError as e:  # PyTables missing
+        raise ImportError(f'reading {path} needs PyTables (pandas.read_hdf); export the DLC file as .csv '
+                          'or install tables') from e
+
+
+def load_dlc_points_as_df(dlc_df_fpaths, frame_shifts=None, verbose=False):
+    """`src/lib/utils.py:77-151` for standard DLC outputs (scorer/bodyparts/coords columns):
+    long DataFrame [frame, camera, marker, x, y, likelihood]."""
+    assert frame_shifts is None or len(dlc_df_fpaths) == len(frame_shifts)
+    out = []
+    for i, path in enumerate(dlc_df_fpaths):
+        df = _read_dlc(path)
+        df = df.droplevel(0, axis=1)                        # scorer
+        parts = list(dict.fromkeys(df.columns.get_level_values(0)))
+        coords = set(df.columns.get_level_values(1))
+        rows = []
+        idx = df.index
+        frames = np.array([int(str(s)[-7:-4]) if not np.issubdtype(type(s), np.integer) else int(s) for s in idx])
+        shift = 0 if frame_shifts is None else int(frame_shifts[i])
+        for bp in parts:
+            x = df[(bp, 'x')].to_numpy(np.float64)
+            y = df[(bp, 'y')].to_numpy(np.float64)
+            lk = df[(bp, 'likelihood')].to_numpy(np.float64) if 'likelihood' in coords else np.isfinite(x) * 1.0
+            if shift:
+                x, y, lk = (np.roll(v, shift) for v in (x, y, lk))
+            rows.append(pd.DataFrame({'frame': frames, 'camera': i, 'marker': bp, 'x': x, 'y': y,
+                                      'likelihood': np.nan_to_num(lk)}))
+        out.append(pd.concat(rows, ignore_index=True).sort_values(['frame'], kind='stable'))
+    dlc = pd.concat(out, ignore_index=True)[['frame', 'camera', 'marker', 'x', 'y', 'likelihood']]
+    if verbose:
+        print(f'DLC points dataframe:\n{dlc}\n')
+    return dlc
+
+
+def save_optimised_cheetah(positions, out_fpath, extra_data=None, for_matlab=True, save_as_csv=False):
+    """`src/lib/utils.py:206-234`: pickle {positions, **extra} (+ .mat)."""
+    file_data = dict(positions=positions)
+    if extra_data is not None:
+        assert type(extra_data) is dict
+        file_data.update(extra_data)
+    with open(out_fpath, 'wb') as f:
+        pickle.dump(file_data, f)
+    print('Saved', out_fpath)
+    if for_matlab:
+        from scipy.io import savemat
+        mat = {k: v for k, v in file_data.items() if not isinstance(v, dict)}
+        savemat(os.path.splitext(out_fpath)[0] + '.mat', mat)
+        print('Saved', os.path.splitext(out_fpath)[0] + '.mat')
+
+
+def create_board_object_pts(board_shape, square_edge_length):
+    obj = np.zeros((board_shape[0] * board_shape[1], 3), np.float32)
+    obj[:, :2] = np.mgrid[0:board_shape[0], 0:board_shape[1]].T.reshape(-1, 2) * square_edge_length
+    return obj
+
+
+def get_pairwise_3d_points_from_df(points_2d_df, k_arr, d_arr, r_arr, t_arr, triangulate_func=None, verbose=True):
+    """`src/lib/utils.py:319-349` with the GPU triangulation: for adjacent camera pairs
+    (i, i+1 mod C), inner join on (frame, marker), triangulate, then mean per
+    (frame, marker) in pair order. Returns [frame, marker, x, y, z] sorted by
+    (frame, marker) like the reference's groupby. `triangulate_func` is accepted for
+    signature compatibility (the fisheye model is always used)."""
+    n_cams = len(k_arr)
+    cams = _native.pack_cameras(k_arr, np.asarray(d_arr).reshape(-1, 4), r_arr, t_arr)
+    parts = []
+    for ca in range(n_cams):
+        cb = (ca + 1) % n_cams
+        d0 = points_2d_df[points_2d_df['camera'] == ca]
+        d1 = points_2d_df[points_2d_df['camera'] == cb]
+        j = d0.merge(d1, how='inner', on=['frame', 'marker'], suffixes=('_a', '_b'))
+        if j.shape[0] > 0:
+            if verbose:
+                print(f'Found {j.shape[0]} pairwise points between camera {ca} and {cb}')
+            parts.append((j, ca, cb))
+        elif verbose:
+            print(f'No pairwise points between camera {ca} and {cb}')
+    if verbose:
+        print()
+    if not parts:
+        return pd.DataFrame(columns=['frame', 'marker', 'x', 'y', 'z'])
+    uva = np.concatenate([p[0][['x_a', 'y_a']].to_numpy(np.float64) for p in parts])
+    uvb = np.concatenate([p[0][['x_b', 'y_b']].to_numpy(np.float64) for p in parts])
+    cia = np.concatenate([np.full(len(p[0]), p[1], np.int32) for p in parts])
+    cib = np.concatenate([np.full(len(p[0]), p[2], np.int32) for p in parts])
+    xyz = _native.default_context().triangulate_pairs(cams, uva, uvb, cia, cib)
+    frames = np.concatenate([p[0]['frame'].to_numpy() for p in parts])
+    markers = np.concatenate([p[0]['marker'].to_numpy() for p in parts])
+    df = pd.DataFrame({'frame': frames, 'marker': markers, 'x': xyz[:, 0], 'y': xyz[:, 1], 'z': xyz[:, 2]})
+    return df.groupby(['frame', 'marker']).mean().reset_index()

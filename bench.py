@@ -36,6 +36,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--fte', action='store_true', help='also time the FTE trajectory solve (configs[2])')
+    ap.add_argument('--fte-frames', type=int, default=1000)
     return ap.parse_args()
 
 
@@ -145,8 +146,8 @@ def main():
                         'cost_after': rep['cost_after'], 'pos_rms_vs_truth_m': pos_rms},
     }
 
-    if args.fte:
-        out['fte'] = bench_fte(ctx, torch, stream)
+    if args.fte and world == 1:
+        out['fte'] = bench_fte(ctx, torch, stream, n_frames=args.fte_frames)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(seq, scene, uv, mask, pts0, args.cpu_seconds)
@@ -176,8 +177,68 @@ def cpu_baseline(seq, scene, uv, mask, pts0, seconds):
                       f'(oracle/sba.py, numpy float64), {dt:.1f} s'}
 
 
-def bench_fte(ctx, torch, stream):  # filled in by the FTE milestone
-    return None
+def bench_fte(ctx, torch, stream, n_frames=1000, steps=3, window=24):
+    """configs[2]: 6-cam x 1000-frame FTE (20 keypoints, P = 26, shutter delay 'const',
+    interpolation 'vel' = the all_optimizations defaults, src/all_optimizations.py:127-136),
+    from the reference initialisation (pairwise triangulation on the GPU + nose line fit)."""
+    import numpy as np
+    from acinoset_amd import _native, synth
+    import importlib
+    cfte = importlib.import_module("acinoset_amd.core.fte")
+    from acinoset_amd.kinematics import build_table
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(n_frames, scene, mode='default_nolure', seed=77, tau_max=0.004)
+    w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
+    meas = np.nan_to_num(seq.uv)
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    # init exactly as core.fte: GPU pairwise triangulation of the nose, line fit
+    N, C, L, _ = seq.uv.shape
+    valid = (seq.likelihood > 0.5) & np.isfinite(seq.uv).all(-1)
+    nose_uv = seq.uv[:, :, 0]                                      # (N, C, 2)
+    xyz, cnt = ctx.triangulate_dense(cams, nose_uv, valid[:, :, 0])
+    import pandas as pd
+    ok = cnt > 0
+    nose_df = pd.DataFrame({'frame': np.arange(N)[ok], 'marker': 'nose', 'x': xyz[ok, 0], 'y': xyz[ok, 1],
+                            'z': xyz[ok, 2]})
+    X0 = cfte.initial_state(nose_df, 'default_nolure', 0, N - 1)
+    table = build_table('default_nolure')
+    qinv = cfte.model_weights('default_nolure')
+    dev = torch.device('cuda', torch.cuda.current_device())
+    T = lambda a, dt=torch.float64: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
+    d_ints, d_reals, d_cams, d_meas, d_w, d_q = (T(table.ints, torch.int32), T(table.reals), T(cams), T(meas), T(w),
+                                                 T(qinv))
+    d_X0, d_X, d_tau = T(X0), T(X0), torch.zeros(C, dtype=torch.float64, device=dev)
+    opts = ctx.fte_default_opts(window=window)
+
+    def run():
+        d_X.copy_(d_X0)
+        d_tau.zero_()
+        return ctx.fte_solve_dev(d_ints.data_ptr(), len(table.ints), d_reals.data_ptr(), len(table.reals),
+                                 d_cams.data_ptr(), C, d_meas.data_ptr(), d_w.data_ptr(), N, True, seq.Ts,
+                                 d_q.data_ptr(), 1, d_X.data_ptr(), d_tau.data_ptr(), opts)
+    rep = run()                                                    # warm-up + correctness
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        rep = run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    X = d_X.cpu().numpy()
+    tau = d_tau.cpu().numpy()
+    pos = ctx.fk(table, X[2:])
+    pos_rms = float(np.sqrt(np.mean(np.sum((pos - seq.pos3d[:, 0]) ** 2, -1))))
+    # reprojection RMS (px) over weighted observations at the solution
+    shift = ((X[2:, :3] - X[1:-1, :3]) / seq.Ts)[:, None, :] * tau[None, :, None]          # (N, C, 3)
+    pts = pos[:, None] + shift[:, :, None]
+    uv = np.stack([ctx.project(cams, pts[:, c].reshape(-1, 3), np.full(N * L, c), fte_form=True).reshape(N, L, 2)
+                   for c in range(C)], 1)
+    m = w > 0
+    rms = float(np.sqrt(np.mean(np.sum((uv - meas)[m] ** 2, -1))))
+    return {'workload': f'fte C={C} frames={N} L={L} P={table.P} sd=const intermode=vel (configs[2])',
+            'frames_per_s': N / dt, 'ms_per_solve': dt * 1e3, 'status': rep['status_name'], 'iters': rep['iters'],
+            'accepted': rep['n_accepted'], 'cost_before': rep['cost_before'], 'cost_after': rep['cost_after'],
+            'reproj_rms_px': rms, 'pos_rms_vs_truth_m': pos_rms, 'tau_err_max_s': float(np.abs(tau - seq.tau).max()),
+            'window': window}
 
 
 if __name__ == '__main__':

@@ -171,6 +171,19 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
                  const double* qinv, int32_t sd_mode, int32_t intermode, const double* X,
                  const double* tau, double* cost3, double* grad, double* H, uint32_t flags);
 
+/* ---- next: fisheye triangulation -------------------------------------
+ * acs_triangulate_pairs: triangulate_points_fisheye (src/lib/calib.py:120-129) for n
+ * (view a, view b) pairs; uv_a/uv_b (n, 2) pixels, cam_a/cam_b (n) camera ids, out (n, 3).
+ * acs_triangulate_dense: get_pairwise_3d_points_from_df (src/lib/utils.py:319-349) on the
+ * dense (n_pts, n_cams) observation tensor: mean over adjacent pairs (c, c+1 mod C) seen
+ * by both cameras; n_pairs_out (may be NULL) = number of pairs (0 -> NaN point).      */
+int acs_triangulate_pairs(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv_a,
+                          const double* uv_b, const int32_t* cam_a, const int32_t* cam_b, int64_t n,
+                          double* xyz_out, uint32_t flags);
+int acs_triangulate_dense(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
+                          const uint8_t* mask, int64_t n_pts, double* xyz_out, int32_t* n_pairs_out,
+                          uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,140 @@
+"""GPU: the drop-in Python entry points (reference signatures) against the reference's
+golden outputs and the oracle. These go through the same C ABI as every other GPU test."""
+import os
+import pickle
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import golden
+from oracle import fte as ofte, fisheye
+from acinoset_amd import kinematics as pkin, synth
+from acinoset_amd.lib import calib, metric, misc, sba as lsba, utils
+from acinoset_amd import core
+
+pytestmark = pytest.mark.gpu
+
+MARKERS20 = pkin.get_markers('default_nolure')
+
+
+def _df(g):
+    return pd.DataFrame({'frame': g['df_frame'], 'camera': g['df_camera'],
+                         'marker': np.array(MARKERS20, dtype=object)[g['df_marker']],
+                         'x': g['df_x'], 'y': g['df_y'], 'likelihood': g['df_likelihood']})
+
+
+def _scene_file(g, tmp_path):
+    p = os.path.join(tmp_path, 'scene.json')
+    utils.save_scene(p, g['K'], g['D'], g['R'], g['t'], [2704, 1520])
+    return p
+
+
+@pytest.mark.parametrize('name', ['sba_cfg1', 'sba_cfg2'])
+def test_sba_points_dropin_matches_reference(name, tmp_path):
+    g = golden(name)
+    pts_df, res = lsba._sba_points(_scene_file(g, tmp_path), _df(g))
+    ref = {(f, MARKERS20[m]): p for f, m, p in zip(g['pts_frame'], g['pts_marker'], g['pts_out'])}
+    assert len(ref) == len(pts_df)
+    # same point ordering as the reference (groupby (frame, marker) order)
+    assert list(zip(pts_df['frame'], pts_df['marker'])) == [(f, MARKERS20[m]) for f, m in
+                                                            zip(g['pts_frame'], g['pts_marker'])]
+    d = np.linalg.norm(pts_df[['x', 'y', 'z']].to_numpy() - g['pts_out'], axis=1)
+    assert np.sqrt(np.mean(d ** 2)) < 1e-6 and d.max() < 1e-5
+    np.testing.assert_allclose(res['before'], g['resid_before'], atol=1e-8)
+    np.testing.assert_allclose(res['after'], g['resid_after'], atol=1e-3)
+
+
+def test_pairwise_triangulation_matches_reference():
+    g = golden('triangulation')
+    out = utils.get_pairwise_3d_points_from_df(_df(g), g['K'], g['D'].reshape(-1, 4), g['R'], g['t'], verbose=False)
+    ref = {(f, MARKERS20[m]): p for f, m, p in zip(g['out_frame'], g['out_marker'], g['out_xyz'])}
+    assert len(out) == len(ref)
+    for f, m, x, y, z in out[['frame', 'marker', 'x', 'y', 'z']].itertuples(index=False):
+        np.testing.assert_allclose([x, y, z], ref[(f, m)], atol=1e-9)
+    X = calib.triangulate_points_fisheye(g['pair_a'], g['pair_b'], g['K'][0], g['D'][0], g['R'][0], g['t'][0],
+                                         g['K'][1], g['D'][1], g['R'][1], g['t'][1])
+    np.testing.assert_allclose(X, g['pair_xyz'], atol=1e-9)
+
+
+def test_triangulate_dense_matches_oracle(ctx):
+    from acinoset_amd import _native
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(12, scene, seed=9)
+    N, C, L, _ = seq.uv.shape
+    valid = (seq.likelihood > 0.5)
+    uv = seq.uv.transpose(0, 2, 1, 3).reshape(N * L, C, 2)
+    mk = valid.transpose(0, 2, 1).reshape(N * L, C)
+    xyz, cnt = ctx.triangulate_dense(_native.pack_cameras(scene.K, scene.D, scene.R, scene.t), uv, mk)
+    for p in range(0, N * L, 7):
+        Xs = [fisheye.triangulate_pair(uv[p, c][None], uv[p, (c + 1) % C][None], scene.K[c], scene.D[c], scene.R[c],
+                                       scene.t[c], scene.K[(c + 1) % C], scene.D[(c + 1) % C], scene.R[(c + 1) % C],
+                                       scene.t[(c + 1) % C])[0] for c in range(C) if mk[p, c] and mk[p, (c + 1) % C]]
+        assert cnt[p] == len(Xs)
+        if Xs:
+            np.testing.assert_allclose(xyz[p], np.mean(Xs, 0), atol=1e-9)
+
+
+def test_residual_error_matches_reference(tmp_path):
+    g = golden('sba_cfg2')
+    df = _df(g)
+    pts = pd.DataFrame({'frame': g['pts_frame'], 'marker': np.array(MARKERS20, dtype=object)[g['pts_marker']],
+                        'x': g['pts_out'][:, 0], 'y': g['pts_out'][:, 1], 'z': g['pts_out'][:, 2]})
+    cp = (g['K'], g['D'], g['R'], g['t'], (2704, 1520), 6)
+    err = metric.residual_error(df, pts, MARKERS20, cp)
+    mine = np.concatenate([err[str(c)]['pixel_residual'].to_numpy() for c in range(6)])
+    np.testing.assert_allclose(mine, g['metric_pixel_residual'], atol=1e-9)
+    assert err['0']['pixel_residual'].dtype == np.float64
+
+
+def test_get_3d_marker_coords_dropin():
+    g = golden('fk')
+    for mode in ('default', 'head'):
+        i = 3
+        out = misc.get_3d_marker_coords({'x': g[f'{mode}_x'][i], 'dx': g[f'{mode}_dx'][i],
+                                         'ddx': g[f'{mode}_ddx'][i]}, g[f'{mode}_tau'][i], directions=True,
+                                        mode=mode, intermode='acc')
+        np.testing.assert_allclose(out, g[f'{mode}_acc_1'][i], atol=1e-12)
+    np.testing.assert_allclose(misc.redescending_loss(golden('loss')['err'], 3, 10, 20), golden('loss')['loss'],
+                               rtol=1e-13, atol=1e-13)
+
+
+def test_core_sba_end_to_end(tmp_path):
+    g = golden('sba_cfg2')
+    scene = _scene_file(g, tmp_path)
+    cp = (g['K'], g['D'], g['R'], g['t'], (2704, 1520), 6)
+    out = core.sba(str(tmp_path), _df(g), 0, 99, 0.5, cp, scene)
+    with open(out, 'rb') as f:
+        data = pickle.load(f)
+    assert data['positions'].shape == (100, 23, 3) and data['start_frame'] == 0
+    assert os.path.exists(os.path.join(tmp_path, 'sba', 'sba.mat'))
+
+
+@pytest.mark.parametrize('mode', ['head', 'default_nolure'])
+def test_core_fte_end_to_end_matches_oracle(mode, tmp_path):
+    scene = synth.load_scene_file()
+    N = 40
+    seq = synth.make_sequence(N, scene, mode=mode, seed=13, tau_max=0.003)
+    df = seq.to_df()
+    cp = scene.camera_params()
+    out = core.fte(str(tmp_path / 'fte'), df, mode, cp, 0, N - 1, 0.5, 'scene.json', params={'vid_fps': 90.0},
+                   shutter_delay=True, shutter_delay_mode='const', interpolation_mode='vel', video=False)
+    with open(out, 'rb') as f:
+        st = pickle.load(f)
+    assert set(['x', 'dx', 'ddx', 'shutter_delay', 'reprj_errors', 'start_frame', 'positions']) <= set(st)
+    X = np.asarray(st['x'])
+    # oracle from the same (reference) initialisation
+    w = np.where(seq.likelihood > 0.5, 1 / 3, 0.0)
+    prob = ofte.Problem(mode, np.nan_to_num(seq.uv), w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=True,
+                        intermode='vel')
+    tri = utils.get_pairwise_3d_points_from_df(df.query('likelihood > 0.5'), scene.K, scene.D.reshape(-1, 4),
+                                               scene.R, scene.t, verbose=False)
+    nose = tri[tri['marker'] == 'nose']
+    X0 = ofte.initial_state(prob, nose['frame'].to_numpy(), nose[['x', 'y', 'z']].to_numpy())
+    Xo, to, info = ofte.solve(prob, X0)
+    from oracle import kinematics as okin
+    d = okin.marker_positions(mode, X) - okin.marker_positions(mode, Xo[2:])
+    assert float(np.sqrt(np.mean(np.sum(d ** 2, -1)))) < 1e-6
+    np.testing.assert_allclose([s[0] for s in st['shutter_delay']], to, atol=1e-6)
+    rms = metric.reprojection_rms(st['reprj_errors'])
+    assert rms < 10.0  # includes the 1 % +-30 px outliers and dropouts, as the reference metric does

@@ -1,0 +1,53 @@
+"""CPU: host-side glue of the drop-in layer (no GPU calls)."""
+import numpy as np
+import pandas as pd
+
+from oracle import fte as ofte
+from acinoset_amd import synth
+import importlib
+cfte = importlib.import_module("acinoset_amd.core.fte")
+from acinoset_amd.kinematics import get_markers
+
+
+def test_build_measurements_matches_reference_lookup():
+    seq = synth.make_sequence(6, synth.load_scene_file(), mode='head', seed=1)
+    df = seq.to_df(start_frame=10)
+    markers = get_markers('head')
+    meas, w = cfte.build_measurements(df, markers, 6, 11, 14, 0.5)
+    # reference semantics (src/core/fte.py:195-221): boolean-mask lookup, first row
+    for n in range(4):
+        for c in range(6):
+            for l, m in enumerate(markers):
+                row = df[(df['frame'] == n + 11) & (df['marker'] == m) & (df['camera'] == c)]
+                lk = row['likelihood'].values[0]
+                assert w[n, c, l] == (1 / 3 if lk > 0.5 else 0.0)
+                if np.isfinite(row['x'].values[0]):
+                    assert meas[n, c, l, 0] == row['x'].values[0] and meas[n, c, l, 1] == row['y'].values[0]
+
+
+def test_initial_state_matches_reference_linregress():
+    rng = np.random.default_rng(0)
+    fr = np.arange(5, 45)
+    xyz = np.stack([1 + 0.05 * fr, 6 - 0.01 * fr, 0.6 + 0 * fr], 1) + rng.normal(0, 0.01, (40, 3))
+    df = pd.DataFrame({'frame': fr, 'marker': 'nose', 'x': xyz[:, 0], 'y': xyz[:, 1], 'z': xyz[:, 2]})
+    X = cfte.initial_state(df, 'default_nolure', 5, 44)
+    prob = type('P', (), {'mode': 'default_nolure', 'N': 40, 'P': 26})()
+    Xo = ofte.initial_state(prob, fr, xyz, start_frame=5)
+    np.testing.assert_allclose(X, Xo, atol=1e-12)
+
+
+def test_states_satisfy_reference_integration_constraints():
+    """x_n = x_{n-1} + Ts dx_n, dx_n = dx_{n-1} + Ts ddx_n for n >= 2 (src/core/fte.py:467-477)."""
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(12, 6))
+    Ts = 1 / 90
+    st = cfte.states_from_solution(X, np.array([0.0, 1e-3]), Ts, True, 10)
+    x, dx, ddx = (np.asarray(st[k]) for k in ('x', 'dx', 'ddx'))
+    np.testing.assert_allclose(x[1:], x[:-1] + Ts * dx[1:], atol=1e-12)
+    np.testing.assert_allclose(dx[1:], dx[:-1] + Ts * ddx[1:], atol=1e-9)
+    assert len(st['shutter_delay']) == 2 and len(st['shutter_delay'][1]) == 10
+
+
+def test_model_weights_are_reference_Q():
+    q = cfte.model_weights('head')
+    np.testing.assert_allclose(q, 1 / np.array([4, 7, 5, 13, 9, 26], float) ** 2)
