@@ -8,33 +8,31 @@
 // (:492-510) is  sum rho(w * (proj(FK(x_n) + shift) - meas)) + sum (Delta^3 x / Ts^2)^2 / Q.
 // It is minimised by Levenberg-Marquardt with the spec in oracle/fte.py.
 //
-// One LM iteration = 7 launches, all device-resident (state in FteState):
+// One LM iteration (captured into a hipGraph, 4 iterations per graph, no host round trip):
 //   k_fte_linearize  [N blocks]  FK + analytic FK Jacobian (fk.hpp), fisheye projection
 //                                and its Jacobian, loss derivatives, per-frame local
 //                                Jacobian rows (2CL x NZ) in LDS and the per-frame normal
-//                                block J^T W J via v_mfma_f64_16x16x4f64 (the dense small
-//                                GEMM of the path), gradient, cost
+//                                block J^T W J via v_mfma_f64_16x16x4f64, gradient, cost
 //   k_fte_assemble   [M blocks]  block-banded (bandwidth 3) normal matrix + tau border
 //                                + exact model term (third differences)
-//   k_fte_window     [W blocks]  per-window band Cholesky of the interior, fill columns
-//                                Y = L^-1 [A_IS | A_Itau | b_I], window Schur block Y^T Y
-//   k_fte_reduced    [1 block ]  block-tridiagonal separator system + tau border, solved
-//   k_fte_backsolve  [W blocks]  interior back substitution, trial state
+//   k_cr_build       [n blocks]  3-frame super-blocks (block tridiagonal) + LM damping
+//   k_cr_elim/update [log2 n levels]  block cyclic reduction: SPD block inverse by blocked
+//                                Gauss-Jordan and Schur updates, all on f64 MFMA tiles
+//   k_cr_top         [1 block ]  last block + tau border
+//   k_cr_back        [log2 n levels]  back substitution
+//   k_cr_trial       [n blocks]  trial state X + delta, tau clipped to [-Ts, Ts]
 //   k_fte_cost       [N blocks]  exact objective at the trial state (per-frame partials)
 //   k_fte_lm         [1 block ]  fixed-order reduction, accept/reject, lambda, stop tests
-// Windows are a partition of frames into interiors separated by 3-frame separators; with
-// bandwidth 3 the interiors decouple exactly (a SPIKE/substructuring direct solve).
 #include "fk.hpp"
-#include "wgla.hpp"
+#include "mfma64.hpp"
 
 #define FTE_NZP 64
 #define FTE_MAXC 16
 #define FTE_CH 32  // observations per LDS chunk (64 Jacobian rows)
 
-typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 struct FteDims {
-  int N, M, P, L, C, Cg, NZ, im, W, NCOL, B;
+  int N, M, P, L, C, Cg, NZ, im, nblk, BP, GR, nlev;
   double Ts, la, lb, lc;
 };
 
@@ -338,118 +336,142 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
 }
 
 // ---------------------------------------------------------------------------------------
-// 3. window factorisation
+// 3-6. block cyclic reduction on 3-frame super-blocks
+//
+// Frames are grouped into n = ceil(M/3) super-blocks of B = 3P unknowns (padded to BP, a
+// multiple of 16; padding rows are identity). With bandwidth 3 the normal matrix is block
+// tridiagonal in super-blocks: D_i (diagonal) and E_i = T(i, i-1), plus the tau border
+// G_i and rhs b_i = -g_i packed as GB_i = [G_i | b_i] (BP x GR). Level s (= 1, 2, 4, ..)
+// eliminates the active blocks i = s(2m+1) in parallel:
+//   W_i = D_i^-1 [E_i | E_{i+s}^T | GB_i]      (blocked Gauss-Jordan + MFMA GEMMs)
+// and every survivor j = 2sm gathers the Schur updates of its eliminated neighbours
+// a = j - s and c = j + s:
+//   D_j -= E_j W_r(a) + E_c^T W_l(c),  GB_j -= E_j W_gb(a) + E_c^T W_gb(c),
+//   E_j <- -E_j W_l(a)   (new coupling to the next active block on the left)
+// until only block 0 is left; k_cr_top solves block 0 with the tau border (tau Schur sum
+// over every eliminated block, fixed order), and k_cr_back substitutes the levels back:
+//   delta_i = W_b(i) - W_l(i) delta_{i-s} - W_r(i) delta_{i+s} - W_g(i) delta_tau.
+// All sums are in a fixed order, so the solve is deterministic run to run.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_fte_window(FteDims d, const int* __restrict__ wstart,
-                                                    const int* __restrict__ wlen, const FteState* __restrict__ st,
-                                                    int force, double lam_force, const double* __restrict__ Ab,
-                                                    const double* __restrict__ gb, const double* __restrict__ Bt,
-                                                    double* __restrict__ Lb, double* __restrict__ Y,
-                                                    double* __restrict__ Sw, int* __restrict__ bad) {
-  if (!force && st->status != 0) return;
-  const int w = blockIdx.x;
+#define CR_MAXBP 96
+
+__global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __restrict__ st,
+                                                  const double* __restrict__ Ab, const double* __restrict__ gb,
+                                                  const double* __restrict__ Bt, double* __restrict__ Dc,
+                                                  double* __restrict__ Ec, double* __restrict__ GBc) {
+  if (st->status != 0) return;
+  const int i = blockIdx.x;
   const int tid = threadIdx.x, nth = blockDim.x;
-  const int P = d.P, PP = P * P, NCOL = d.NCOL, Cg = d.Cg;
-  const int s0 = wstart[w], n = wlen[w];
-  const bool hasL = w > 0, hasR = w < d.W - 1;
-  const int cL = 0, cR = 3 * P, cT = 6 * P, cb = 6 * P + Cg;
-  const double lam = force ? lam_force : st->lam;
-  for (int j = 0; j < n; ++j) {
-    const int f = s0 + j;
-    double* Lrow = Lb + (size_t)f * 4 * PP;
-    const double* Arow = Ab + (size_t)f * 4 * PP;
-    for (int i = tid; i < 4 * PP; i += nth) {
-      const int blk = i / PP;
-      double v = (blk == 0 || f - blk >= s0) ? Arow[i] : 0.0;
-      if (blk == 0) {
-        const int r = (i % PP) / P, c = i % P;
-        if (r == c) v += lam * fmax(v, 1e-12);
-      }
-      Lrow[i] = v;
+  const int P = d.P, PP = P * P, BP = d.BP, GR = d.GR, Cg = d.Cg;
+  const double lam = st->lam;
+  double* D = Dc + (size_t)i * BP * BP;
+  double* E = Ec + (size_t)i * BP * BP;
+  double* G = GBc + (size_t)i * BP * GR;
+  for (int e = tid; e < BP * BP; e += nth) {
+    const int r = e / BP, c = e % BP;
+    const int ar = r / P, pr = r % P, ac = c / P, pc = c % P;
+    const int fr = 3 * i + ar, fc = 3 * i + ac;
+    double v = 0.0, w = 0.0;
+    const bool rin = r < 3 * P && fr < d.M, cin = c < 3 * P && fc < d.M;
+    if (rin && cin) {
+      v = (ar >= ac) ? Ab[(size_t)fr * 4 * PP + (ar - ac) * PP + pr * P + pc]
+                     : Ab[(size_t)fc * 4 * PP + (ac - ar) * PP + pc * P + pr];
+      if (r == c) v += lam * fmax(v, 1e-12);
+    } else if (r == c) {
+      v = 1.0;  // padding: identity
     }
-    __syncthreads();
-    for (int dd = 3; dd >= 1; --dd) {
-      if (f - dd < s0) continue;
-      for (int e = dd + 1; e <= 3; ++e) {
-        if (f - e < s0) continue;
-        wg_gemm<false, true>(Lrow + dd * PP, P, Lrow + e * PP, P, Lb + (size_t)(f - dd) * 4 * PP + (e - dd) * PP, P,
-                             P, P, P, -1.0);
-      }
-      wg_trsm_rlt(Lrow + dd * PP, P, Lb + (size_t)(f - dd) * 4 * PP, P, P, P);
+    D[e] = v;
+    // E_i = T(block i, block i-1): frames 3i+ar vs 3(i-1)+ac, distance 3 + ar - ac <= 3
+    const int fe = 3 * (i - 1) + ac;
+    if (i > 0 && rin && c < 3 * P && fe < d.M) {
+      const int dist = 3 + ar - ac;
+      if (dist <= 3) w = Ab[(size_t)fr * 4 * PP + dist * PP + pr * P + pc];
     }
-    for (int dd = 1; dd <= 3; ++dd) {
-      if (f - dd < s0) continue;
-      wg_gemm<false, true>(Lrow, P, Lrow + dd * PP, P, Lrow + dd * PP, P, P, P, P, -1.0);
-    }
-    wg_chol(Lrow, P, P, bad);
-    // E row
-    double* Yrow = Y + (size_t)f * P * NCOL;
-    for (int i = tid; i < P * NCOL; i += nth) {
-      const int r = i / NCOL, c = i % NCOL;
-      double v = 0.0;
-      if (c < cR) {
-        if (hasL) {
-          const int sfi = c / P, sc = c % P;  // separator frame s0-3+sfi
-          const int sf = s0 - 3 + sfi, dd = f - sf;
-          if (dd >= 1 && dd <= 3) v = Arow[dd * PP + r * P + sc];
-        }
-      } else if (c < cT) {
-        if (hasR) {
-          const int sfi = (c - cR) / P, sc = (c - cR) % P;
-          const int sf = s0 + n + sfi, dd = sf - f;
-          if (dd >= 1 && dd <= 3) v = Ab[(size_t)sf * 4 * PP + dd * PP + sc * P + r];
-        }
-      } else if (c < cb) {
-        v = Bt[(size_t)f * P * Cg + r * Cg + (c - cT)];
-      } else {
-        v = -gb[(size_t)f * P + r];
-      }
-      Yrow[i] = v;
-    }
-    __syncthreads();
-    for (int dd = 1; dd <= 3; ++dd) {
-      if (f - dd < s0) continue;
-      wg_gemm<false, false>(Yrow, NCOL, Lrow + dd * PP, P, Y + (size_t)(f - dd) * P * NCOL, NCOL, P, NCOL, P, -1.0);
-    }
-    wg_trsm_lln(Yrow, NCOL, Lrow, P, P, NCOL);
+    E[e] = w;
   }
-  // Schur block of this window: Sw = Y^T Y over its interior rows
-  double* S = Sw + (size_t)w * NCOL * NCOL;
-  const double* Yw = Y + (size_t)s0 * P * NCOL;
-  const int rows = n * P;
-  for (int idx = tid; idx < NCOL * NCOL; idx += nth) {
-    const int i = idx / NCOL, j = idx % NCOL;
-    if (j < i) continue;
-    double sacc = 0.0;
-    // right-separator columns are zero above the last 3 interior frames
-    int r0 = 0;
-    if ((i >= cR && i < cT) || (j >= cR && j < cT)) r0 = max(0, (n - 3) * P);
-    for (int r = r0; r < rows; ++r) sacc = fma(Yw[(size_t)r * NCOL + i], Yw[(size_t)r * NCOL + j], sacc);
-    S[i * NCOL + j] = sacc;
-    S[j * NCOL + i] = sacc;
+  for (int e = tid; e < BP * GR; e += nth) {
+    const int r = e / GR, c = e % GR;
+    const int ar = r / P, pr = r % P, fr = 3 * i + ar;
+    double v = 0.0;
+    if (r < 3 * P && fr < d.M) {
+      if (c < Cg)
+        v = Bt[(size_t)fr * P * Cg + pr * Cg + c];
+      else if (c == Cg)
+        v = -gb[(size_t)fr * P + pr];
+    }
+    G[e] = v;
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// 4. reduced (separator + tau) system
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_fte_reduced(FteDims d, const int* __restrict__ wstart,
-                                                     const int* __restrict__ wlen, FteState* __restrict__ st,
-                                                     int force, double lam_force, const double* __restrict__ Ab,
-                                                     const double* __restrict__ gb, const double* __restrict__ Bt,
-                                                     const double* __restrict__ Hloc,
-                                                     const double* __restrict__ gloc,
-                                                     const double* __restrict__ Sw,
-                                                     const double* __restrict__ gmaxp, double* __restrict__ RA,
-                                                     double* __restrict__ RL, double* __restrict__ LT,
-                                                     double* __restrict__ ry, double* __restrict__ Rt,
-                                                     double* __restrict__ rt, double* __restrict__ dS,
-                                                     double* __restrict__ dtau, int* __restrict__ bad) {
-  if (!force && st->status != 0) return;
+__global__ __launch_bounds__(256) void k_cr_elim(FteDims d, int s, const FteState* __restrict__ st,
+                                                 const double* __restrict__ Dc, const double* __restrict__ Ec,
+                                                 const double* __restrict__ GBc, double* __restrict__ Wc,
+                                                 double* __restrict__ Tau, int* __restrict__ bad) {
+  if (st->status != 0) return;
+  const int i = s * (2 * blockIdx.x + 1);
+  const int r = (i + s < d.nblk) ? i + s : -1;
+  const int BP = d.BP, GR = d.GR, WL = 2 * BP + GR;
+  __shared__ double sD[CR_MAXBP * CR_MAXBP];
+  __shared__ double tmp[512];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < BP * BP; e += blockDim.x) sD[e] = Dc[(size_t)i * BP * BP + e];
+  __syncthreads();
+  wg_spd_inverse(sD, BP, BP >> 4, tmp, bad);
+  double* W = Wc + (size_t)i * BP * WL;
+  wg_mgemm<false, false>(W, WL, sD, BP, Ec + (size_t)i * BP * BP, BP, BP, BP, BP, 1.0, 0.0);
+  if (r >= 0)
+    wg_mgemm<false, true>(W + BP, WL, sD, BP, Ec + (size_t)r * BP * BP, BP, BP, BP, BP, 1.0, 0.0);
+  else
+    for (int e = tid; e < BP * BP; e += blockDim.x) W[(e / BP) * WL + BP + e % BP] = 0.0;
+  const double* G = GBc + (size_t)i * BP * GR;
+  wg_mgemm<false, false>(W + 2 * BP, WL, sD, BP, G, GR, BP, GR, BP, 1.0, 0.0);
+  // tau Schur contribution GB_i^T W_gb(i)
+  wg_mgemm<true, false>(Tau + (size_t)i * GR * GR, GR, G, GR, W + 2 * BP, WL, GR, GR, BP, 1.0, 0.0);
+}
+
+__global__ __launch_bounds__(256) void k_cr_update(FteDims d, int s, const FteState* __restrict__ st,
+                                                   double* __restrict__ Dc, double* __restrict__ Ec,
+                                                   double* __restrict__ GBc, const double* __restrict__ Wc) {
+  if (st->status != 0) return;
+  const int j = 2 * s * blockIdx.x;
+  const int a = j - s >= 0 ? j - s : -1;
+  const int c = j + s < d.nblk ? j + s : -1;
+  const int BP = d.BP, GR = d.GR, WL = 2 * BP + GR;
+  __shared__ double sE[CR_MAXBP * CR_MAXBP];
+  double* D = Dc + (size_t)j * BP * BP;
+  double* E = Ec + (size_t)j * BP * BP;
+  double* G = GBc + (size_t)j * BP * GR;
+  if (a >= 0) {
+    const double* Wa = Wc + (size_t)a * BP * WL;
+    wg_mgemm<false, false>(D, BP, E, BP, Wa + BP, WL, BP, BP, BP, -1.0, 1.0);
+    wg_mgemm<false, false>(G, GR, E, BP, Wa + 2 * BP, WL, BP, GR, BP, -1.0, 1.0);
+    wg_mgemm<false, false>(sE, BP, E, BP, Wa, WL, BP, BP, BP, -1.0, 0.0);
+  }
+  if (c >= 0) {
+    const double* Wcc = Wc + (size_t)c * BP * WL;
+    const double* Ecc = Ec + (size_t)c * BP * BP;
+    wg_mgemm<true, false>(D, BP, Ecc, BP, Wcc, WL, BP, BP, BP, -1.0, 1.0);
+    wg_mgemm<true, false>(G, GR, Ecc, BP, Wcc + 2 * BP, WL, BP, GR, BP, -1.0, 1.0);
+  }
+  if (a >= 0) {
+    for (int e = threadIdx.x; e < BP * BP; e += blockDim.x) E[e] = sE[e];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ Dc,
+                                                const double* __restrict__ GBc, const double* __restrict__ Tau,
+                                                const double* __restrict__ Hloc, const double* __restrict__ gloc,
+                                                const double* __restrict__ gmaxp, double* __restrict__ dcv,
+                                                double* __restrict__ dtau, int* __restrict__ bad) {
+  if (st->status != 0) return;
   const int tid = threadIdx.x, nth = blockDim.x;
-  const int P = d.P, PP = P * P, NCOL = d.NCOL, Cg = d.Cg, B = d.B, J = d.W - 1;
-  const int cL = 0, cR = 3 * P, cT = 6 * P, cb = 6 * P + Cg;
-  const double lam = force ? lam_force : st->lam;
+  const int P = d.P, BP = d.BP, GR = d.GR, Cg = d.Cg;
+  const double lam = st->lam;
+  __shared__ double sD[CR_MAXBP * CR_MAXBP];
+  __shared__ double sW[CR_MAXBP * 32];
+  __shared__ double sS[32 * 32];
+  __shared__ double sr[32];
+  __shared__ double tmp[512];
   __shared__ double s_red[256];
   // gradient max (frames + tau border)
   {
@@ -461,196 +483,117 @@ __global__ __launch_bounds__(256) void k_fte_reduced(FteDims d, const int* __res
       mx = fmax(mx, fabs(gt));
     }
     mx = block_max(mx, s_red);
-    if (tid == 0 && !force) st->gmax = mx;
+    if (tid == 0) st->gmax = mx;
   }
-  // tau block: Rt = sum_k Hloc_tt - sum_w Sw_tt (+ damping, tau_0 pinned); rt = -g_t - sum_w Sw_t,rhs
-  for (int i = tid; i < Cg * Cg; i += nth) {
-    const int r = i / Cg, c = i % Cg;
-    double v = 0.0;
-    for (int k = 0; k < d.N; ++k) v += Hloc[(size_t)k * FTE_NZP * FTE_NZP + (P + 6 + r) * FTE_NZP + P + 6 + c];
-    if (r == c) v += lam * fmax(v, 1e-12);
-    for (int w = 0; w < d.W; ++w) v -= Sw[(size_t)w * NCOL * NCOL + (cT + r) * NCOL + cT + c];
-    if (r == 0 || c == 0) v = (r == c) ? 1.0 : 0.0;
-    Rt[i] = v;
-  }
-  for (int r = tid; r < Cg; r += nth) {
-    double v = 0.0;
-    for (int k = 0; k < d.N; ++k) v += gloc[(size_t)k * FTE_NZP + P + 6 + r];
-    v = -v;
-    for (int w = 0; w < d.W; ++w) v -= Sw[(size_t)w * NCOL * NCOL + (cT + r) * NCOL + cb];
-    rt[r] = (r == 0) ? 0.0 : v;
-  }
+  for (int e = tid; e < BP * BP; e += nth) sD[e] = Dc[e];
   __syncthreads();
-  // assemble separator blocks
-  for (int j = 0; j < J; ++j) {
-    const int e = wstart[j] + wlen[j];
-    double* A = RA + (size_t)j * B * B;
-    const double* SL = Sw + (size_t)j * NCOL * NCOL;        // window j: S_j is its right separator
-    const double* SR = Sw + (size_t)(j + 1) * NCOL * NCOL;  // window j+1: S_j is its left separator
-    for (int i = tid; i < B * B; i += nth) {
-      const int r = i / B, c = i % B;
-      const int fa = r / P, pa = r % P, fb = c / P, pb = c % P;
-      double v;
-      if (fa >= fb)
-        v = Ab[(size_t)(e + fa) * 4 * PP + (fa - fb) * PP + pa * P + pb];
-      else
-        v = Ab[(size_t)(e + fb) * 4 * PP + (fb - fa) * PP + pb * P + pa];
-      if (r == c) v += lam * fmax(v, 1e-12);
-      v -= SL[(cR + r) * NCOL + cR + c];
-      v -= SR[(cL + r) * NCOL + cL + c];
-      A[i] = v;
-    }
-    if (j >= 1) {
-      double* Lo = RL + (size_t)j * B * B;  // block (S_j, S_{j-1}) = -(window j) right x left
-      for (int i = tid; i < B * B; i += nth) {
-        const int r = i / B, c = i % B;
-        Lo[i] = -SL[(cR + r) * NCOL + cL + c];
-      }
-    }
-    double* T = LT + (size_t)j * Cg * B;  // border, stored transposed (Cg x B)
-    for (int i = tid; i < Cg * B; i += nth) {
-      const int c = i / B, r = i % B;
-      const int fa = r / P, pa = r % P;
-      double v = Bt[(size_t)(e + fa) * P * Cg + pa * Cg + c];
-      v -= SL[(cR + r) * NCOL + cT + c];
-      v -= SR[(cL + r) * NCOL + cT + c];
-      T[i] = (c == 0) ? 0.0 : v;
-    }
-    for (int r = tid; r < B; r += nth) {
-      const int fa = r / P, pa = r % P;
-      double v = -gb[(size_t)(e + fa) * P + pa];
-      v -= SL[(cR + r) * NCOL + cb];
-      v -= SR[(cL + r) * NCOL + cb];
-      ry[(size_t)j * B + r] = v;
-    }
-    __syncthreads();
-  }
-  // block Cholesky of the arrow matrix, forward substitution
-  for (int j = 0; j < J; ++j) {
-    double* A = RA + (size_t)j * B * B;
-    double* T = LT + (size_t)j * Cg * B;
-    double* y = ry + (size_t)j * B;
-    if (j >= 1) {
-      const double* Lo = RL + (size_t)j * B * B;
-      wg_gemm<false, true>(A, B, Lo, B, Lo, B, B, B, B, -1.0);
-      if (Cg) wg_gemm<false, true>(T, B, LT + (size_t)(j - 1) * Cg * B, B, Lo, B, Cg, B, B, -1.0);
-      wg_gemm<false, false>(y, 1, Lo, B, ry + (size_t)(j - 1) * B, 1, B, 1, B, -1.0);
-    }
-    wg_chol(A, B, B, bad);
-    wg_trsm_lln(y, 1, A, B, B, 1);
-    if (Cg) {
-      wg_trsm_rlt(T, B, A, B, Cg, B);
-      wg_gemm<false, true>(Rt, Cg, T, B, T, B, Cg, Cg, B, -1.0);
-      wg_gemm<false, false>(rt, 1, T, B, y, 1, Cg, 1, B, -1.0);
-    }
-    if (j + 1 < J) {
-      // next sub-diagonal block must exist: assembled above; transform to L_{j+1,j}
-      wg_trsm_rlt(RL + (size_t)(j + 1) * B * B, B, A, B, B, B);
-    }
-  }
+  wg_spd_inverse(sD, BP, BP >> 4, tmp, bad);
+  // W0 = D0^-1 GB0 (BP x GR)
+  wg_mgemm<false, false>(sW, GR, sD, BP, GBc, GR, BP, GR, BP, 1.0, 0.0);
   if (Cg) {
-    // keep the pinned tau_0 row exact
-    for (int i = tid; i < Cg; i += nth) {
-      if (i != 0) {
-        Rt[i] = 0.0;
-        Rt[i * Cg] = 0.0;
+    // S = D_tau - sum_i Tau_i - G0^T W0g ;  rhs = b_tau - sum_i Tau_i[:, Cg] - G0^T W0b   (GR x GR, padded)
+    wg_mgemm<true, false>(sS, GR, GBc, GR, sW, GR, GR, GR, BP, -1.0, 0.0);
+    for (int e = tid; e < GR * GR; e += nth) {
+      const int r = e / GR, c = e % GR;
+      if (r < Cg && c <= Cg) {
+        double h = 0.0;
+        if (c < Cg) {
+          for (int k = 0; k < d.N; ++k) h += Hloc[(size_t)k * FTE_NZP * FTE_NZP + (P + 6 + r) * FTE_NZP + P + 6 + c];
+          if (r == c) h += lam * fmax(h, 1e-12);
+        } else {
+          for (int k = 0; k < d.N; ++k) h -= gloc[(size_t)k * FTE_NZP + P + 6 + r];
+        }
+        for (int b = 1; b < d.nblk; ++b) h -= Tau[(size_t)b * GR * GR + r * GR + c];
+        sS[e] += h;
       }
     }
-    if (tid == 0) {
-      Rt[0] = 1.0;
-      rt[0] = 0.0;
+    __syncthreads();
+    if (tid < GR) sr[tid] = (tid > 0 && tid < Cg) ? sS[tid * GR + Cg] : 0.0;
+    __syncthreads();
+    // pin tau_0 and the padding (identity rows / columns)
+    for (int e = tid; e < GR * GR; e += nth) {
+      const int r = e / GR, c = e % GR;
+      if (r >= Cg || c >= Cg || r == 0 || c == 0) sS[e] = (r == c) ? 1.0 : 0.0;
     }
     __syncthreads();
-    wg_chol(Rt, Cg, Cg, bad);
-    wg_trsm_lln(rt, 1, Rt, Cg, Cg, 1);
-    wg_trsm_llt(rt, 1, Rt, Cg, Cg, 1);
-    for (int i = tid; i < Cg; i += nth) dtau[i] = rt[i];
+    wg_spd_inverse(sS, GR, GR >> 4, tmp, bad);
+    if (tid < GR) {
+      double v = 0.0;
+      for (int c = 0; c < GR; ++c) v += sS[tid * GR + c] * sr[c];
+      dtau[tid] = (tid < Cg && tid > 0) ? v : 0.0;
+    }
     __syncthreads();
   }
-  for (int j = J - 1; j >= 0; --j) {
-    double* y = ry + (size_t)j * B;
-    if (j + 1 < J) wg_gemm<true, false>(y, 1, RL + (size_t)(j + 1) * B * B, B, ry + (size_t)(j + 1) * B, 1, B, 1, B, -1.0);
-    if (Cg) wg_gemm<true, false>(y, 1, LT + (size_t)j * Cg * B, B, rt, 1, B, 1, Cg, -1.0);
-    wg_trsm_llt(y, 1, RA + (size_t)j * B * B, B, B, 1);
-    for (int i = tid; i < B; i += nth) dS[(size_t)j * B + i] = y[i];
-    __syncthreads();
+  for (int r = tid; r < BP; r += nth) {
+    double v = sW[r * GR + Cg];
+    for (int c = 0; c < Cg; ++c) v -= sW[r * GR + c] * dtau[c];
+    dcv[r] = v;
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// 5. back substitution + trial state
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_fte_backsolve(FteDims d, const int* __restrict__ wstart,
-                                                       const int* __restrict__ wlen, const FteState* __restrict__ st,
-                                                       int force, const double* __restrict__ Lb,
-                                                       const double* __restrict__ Y, const double* __restrict__ dS,
-                                                       const double* __restrict__ dtau, double* __restrict__ delta,
-                                                       double* __restrict__ Xbuf, double* __restrict__ taubuf,
-                                                       double* __restrict__ normp) {
-  if (!force && st->status != 0) return;
-  const int w = blockIdx.x;
-  const int tid = threadIdx.x, nth = blockDim.x;
-  const int P = d.P, PP = P * P, NCOL = d.NCOL, Cg = d.Cg, B = d.B;
-  const int s0 = wstart[w], n = wlen[w];
-  const bool hasL = w > 0, hasR = w < d.W - 1;
-  const int cL = 0, cR = 3 * P, cT = 6 * P, cb = 6 * P + Cg;
+__global__ __launch_bounds__(256) void k_cr_back(FteDims d, int s, const FteState* __restrict__ st,
+                                                 const double* __restrict__ Wc, const double* __restrict__ dtau,
+                                                 double* __restrict__ dcv) {
+  if (st->status != 0) return;
+  const int i = s * (2 * blockIdx.x + 1);
+  const int l = i - s, r = (i + s < d.nblk) ? i + s : -1;
+  const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
+  const double* W = Wc + (size_t)i * BP * WL;
+  __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32];
+  for (int e = threadIdx.x; e < BP; e += blockDim.x) {
+    sl[e] = dcv[(size_t)l * BP + e];
+    sr_[e] = r >= 0 ? dcv[(size_t)r * BP + e] : 0.0;
+  }
+  if (threadIdx.x < 32) st_[threadIdx.x] = threadIdx.x < Cg ? dtau[threadIdx.x] : 0.0;
+  __syncthreads();
+  for (int row = threadIdx.x; row < BP; row += blockDim.x) {
+    const double* w = W + (size_t)row * WL;
+    double v = w[2 * BP + Cg];
+    for (int c = 0; c < BP; ++c) v -= w[c] * sl[c];
+    if (r >= 0)
+      for (int c = 0; c < BP; ++c) v -= w[BP + c] * sr_[c];
+    for (int c = 0; c < Cg; ++c) v -= w[2 * BP + c] * st_[c];
+    dcv[(size_t)i * BP + row] = v;
+  }
+}
+
+// trial state X + delta, tau + dtau (clipped), norm partials per super-block
+__global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __restrict__ st,
+                                                  const double* __restrict__ dcv, const double* __restrict__ dtau,
+                                                  double* __restrict__ Xbuf, double* __restrict__ taubuf,
+                                                  double* __restrict__ normp) {
+  if (st->status != 0) return;
+  const int i = blockIdx.x;
+  const int P = d.P, BP = d.BP;
   __shared__ double s_red[256];
-  // r = y_b - Y_L dS_{w-1} - Y_R dS_w - Y_T dtau
-  for (int i = tid; i < n * P; i += nth) {
-    const double* Yr = Y + ((size_t)s0 * P + i) * NCOL;
-    double v = Yr[cb];
-    if (hasL)
-      for (int c = 0; c < B; ++c) v -= Yr[cL + c] * dS[(size_t)(w - 1) * B + c];
-    if (hasR)
-      for (int c = 0; c < B; ++c) v -= Yr[cR + c] * dS[(size_t)w * B + c];
-    for (int c = 0; c < Cg; ++c) v -= Yr[cT + c] * dtau[c];
-    delta[(size_t)s0 * P + i] = v;
-  }
-  __syncthreads();
-  for (int j = n - 1; j >= 0; --j) {
-    const int f = s0 + j;
-    double* df = delta + (size_t)f * P;
-    for (int dd = 1; dd <= 3; ++dd) {
-      if (j + dd >= n) continue;
-      // df -= L_{f+dd, f}^T delta_{f+dd}
-      wg_gemm<true, false>(df, 1, Lb + (size_t)(f + dd) * 4 * PP + dd * PP, P, delta + (size_t)(f + dd) * P, 1, P, 1,
-                           P, -1.0);
-    }
-    wg_trsm_llt(df, 1, Lb + (size_t)f * 4 * PP, P, P, 1);
-  }
-  if (hasR) {
-    for (int i = tid; i < B; i += nth) delta[(size_t)(s0 + n) * P + i] = dS[(size_t)w * B + i];
-  }
-  __syncthreads();
-  const int cur = force ? 0 : st->cur;
+  const int cur = st->cur;
   const double* X = Xbuf + (size_t)cur * d.M * P;
   double* Xn = Xbuf + (size_t)(cur ^ 1) * d.M * P;
-  const int span = (n + (hasR ? 3 : 0)) * P;
   double dn = 0.0, xn = 0.0;
-  for (int i = tid; i < span; i += nth) {
-    const size_t o = (size_t)s0 * P + i;
-    const double x = X[o], dv = delta[o];
+  for (int e = threadIdx.x; e < 3 * P; e += blockDim.x) {
+    const int f = 3 * i + e / P, p = e % P;
+    if (f >= d.M) continue;
+    const size_t o = (size_t)f * P + p;
+    const double dv = dcv[(size_t)i * BP + e], x = X[o];
     Xn[o] = x + dv;
     dn += dv * dv;
     xn += x * x;
   }
-  if (w == 0 && Cg) {
+  if (i == 0 && d.Cg) {
     const double* tau = taubuf + cur * d.C;
     double* taun = taubuf + (cur ^ 1) * d.C;
-    for (int c = tid; c < d.C; c += nth) {
+    for (int c = threadIdx.x; c < d.C; c += blockDim.x) {
       const double dv = (c == 0) ? 0.0 : dtau[c];
-      double v = (c == 0) ? 0.0 : tau[c] + dv;
-      v = fmin(fmax(v, -d.Ts), d.Ts);
-      taun[c] = v;
+      taun[c] = (c == 0) ? 0.0 : fmin(fmax(tau[c] + dv, -d.Ts), d.Ts);
       dn += dv * dv;
       xn += tau[c] * tau[c];
     }
   }
   dn = block_sum(dn, s_red);
   xn = block_sum(xn, s_red);
-  if (tid == 0) {
-    normp[2 * w] = dn;
-    normp[2 * w + 1] = xn;
+  if (threadIdx.x == 0) {
+    normp[2 * i] = dn;
+    normp[2 * i + 1] = xn;
   }
 }
 
@@ -740,7 +683,7 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
   }
   if (st->status != 0) return;
   double dn = 0.0, xn = 0.0;
-  for (int w = tid; w < d.W; w += blockDim.x) {
+  for (int w = tid; w < d.nblk; w += blockDim.x) {
     dn += normp[2 * w];
     xn += normp[2 * w + 1];
   }
@@ -783,39 +726,20 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
 struct FteBuffers {
   int* I;
   double *Rl, *cams, *meas, *w, *qinv, *X, *tau;
-  double *Hloc, *gloc, *Floc, *Ab, *gb, *Bt, *gmaxp, *Lb, *Y, *Sw, *RA, *RL, *LT, *ry, *Rt, *rt, *dS, *dtau, *delta,
-      *normp, *Fm, *Fq;
-  int *wstart, *wlen, *bad;
+  double *Hloc, *gloc, *Floc, *Ab, *gb, *Bt, *gmaxp, *Dc, *Ec, *GBc, *Wc, *Tau, *dcv, *dtau, *normp, *Fm, *Fq;
+  int* bad;
   FteState* st;
 };
-
-static void fte_windows(int M, int wl, std::vector<int>& ws, std::vector<int>& wn) {
-  if (wl < 3) wl = 3;
-  int W = (M + 3) / (wl + 3);
-  if (W < 1) W = 1;
-  while (W > 1 && M - 3 * (W - 1) < 3 * W) --W;
-  const int interior = M - 3 * (W - 1);
-  ws.resize(W);
-  wn.resize(W);
-  int pos = 0;
-  for (int w = 0; w < W; ++w) {
-    const int n = interior / W + (w < interior % W ? 1 : 0);
-    ws[w] = pos;
-    wn[w] = n;
-    pos += n + 3;
-  }
-}
 
 struct FteSetup {
   FteDims d;
   FteBuffers b;
-  std::vector<int> ws, wn;
 };
 
 static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
                      int64_t n_reals, const double* cams, int32_t n_cams, const double* meas, const double* w,
                      int32_t N, int32_t sd, double Ts, const double* qinv, int32_t intermode, const double* X,
-                     const double* tau, int window, double la, double lb, double lc, uint32_t flags) {
+                     const double* tau, double la, double lb, double lc, uint32_t flags) {
   int hdr[FK_HDR];
   if (flags & ACS_DEVICE_PTRS)
     ACS_HIP(ctx, hipMemcpy(hdr, skel_ints, sizeof(hdr), hipMemcpyDeviceToHost));
@@ -843,11 +767,13 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   d.la = la;
   d.lb = lb;
   d.lc = lc;
-  d.B = 3 * P;
-  d.NCOL = 6 * P + d.Cg + 1;
-  fte_windows(d.M, window, S.ws, S.wn);
-  d.W = (int)S.ws.size();
-  const int M = d.M, W = d.W, NCOL = d.NCOL, B = d.B, Cg = d.Cg, C = d.C;
+  d.nblk = (d.M + 2) / 3;
+  d.BP = ((3 * P + 15) / 16) * 16;
+  ACS_CHECK(ctx, d.BP <= CR_MAXBP, "fte: 3P = %d exceeds %d", 3 * P, CR_MAXBP);
+  d.GR = ((d.Cg + 1 + 15) / 16) * 16;
+  d.nlev = 0;
+  for (int s = 1; s < d.nblk; s <<= 1) d.nlev++;
+  const int M = d.M, C = d.C, BP = d.BP, GR = d.GR, n = d.nblk;
   FteBuffers& b = S.b;
   int rc;
   void* p;
@@ -863,23 +789,20 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.w = (double*)p;
   if ((rc = acs_stage_in(ctx, WS_FTE4, qinv, sizeof(double) * P, flags, &p))) return rc;
   b.qinv = (double*)p;
-  // one arena for everything else
   size_t off = 0;
-  auto take = [&](size_t n) {
+  auto take = [&](size_t cnt) {
     size_t o = off;
-    off += ((n * sizeof(double) + 255) / 256) * 256 / sizeof(double);
+    off += ((cnt * sizeof(double) + 255) / 256) * 256 / sizeof(double);
     return o;
   };
+  const size_t Cg1 = d.Cg ? d.Cg : 1;
   const size_t oX = take((size_t)2 * M * P), oT = take(2 * C), oH = take((size_t)N * FTE_NZP * FTE_NZP),
                og = take((size_t)N * FTE_NZP), oF = take(N), oAb = take((size_t)M * 4 * P * P),
-               ogb = take((size_t)M * P), oBt = take((size_t)M * P * (Cg ? Cg : 1)), ogm = take(M),
-               oLb = take((size_t)M * 4 * P * P), oY = take((size_t)M * P * NCOL),
-               oSw = take((size_t)W * NCOL * NCOL), oRA = take((size_t)(W > 1 ? W - 1 : 1) * B * B),
-               oRL = take((size_t)(W > 1 ? W - 1 : 1) * B * B), oLT = take((size_t)(W > 1 ? W - 1 : 1) * (Cg ? Cg : 1) * B),
-               ory = take((size_t)(W > 1 ? W - 1 : 1) * B), oRt = take((Cg ? Cg : 1) * (Cg ? Cg : 1)),
-               ort = take(Cg ? Cg : 1), odS = take((size_t)(W > 1 ? W - 1 : 1) * B), odt = take(Cg ? Cg : 1),
-               odl = take((size_t)M * P), onp = take(2 * W), oFm = take(N), oFq = take(N), ost = take(16),
-               oint = take(2 * W + 8);
+               ogb = take((size_t)M * P), oBt = take((size_t)M * P * Cg1), ogm = take(M),
+               oD = take((size_t)n * BP * BP), oE = take((size_t)n * BP * BP), oG = take((size_t)n * BP * GR),
+               oW = take((size_t)n * BP * (2 * BP + GR)), oTau = take((size_t)n * GR * GR),
+               odc = take((size_t)n * BP), odt = take(GR), onp = take(2 * (size_t)n), oFm = take(N), oFq = take(N),
+               ost = take(16), oint = take(8);
   double* arena = (double*)acs_ws(ctx, WS_FTE5, off * sizeof(double));
   if (!arena) return ACS_E_NOMEM;
   b.X = arena + oX;
@@ -891,26 +814,18 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.gb = arena + ogb;
   b.Bt = arena + oBt;
   b.gmaxp = arena + ogm;
-  b.Lb = arena + oLb;
-  b.Y = arena + oY;
-  b.Sw = arena + oSw;
-  b.RA = arena + oRA;
-  b.RL = arena + oRL;
-  b.LT = arena + oLT;
-  b.ry = arena + ory;
-  b.Rt = arena + oRt;
-  b.rt = arena + ort;
-  b.dS = arena + odS;
+  b.Dc = arena + oD;
+  b.Ec = arena + oE;
+  b.GBc = arena + oG;
+  b.Wc = arena + oW;
+  b.Tau = arena + oTau;
+  b.dcv = arena + odc;
   b.dtau = arena + odt;
-  b.delta = arena + odl;
   b.normp = arena + onp;
   b.Fm = arena + oFm;
   b.Fq = arena + oFq;
   b.st = (FteState*)(arena + ost);
-  int* ints = (int*)(arena + oint);
-  b.wstart = ints;
-  b.wlen = ints + W;
-  b.bad = ints + 2 * W;
+  b.bad = (int*)(arena + oint);
   hipStream_t s = ctx->stream;
   const hipMemcpyKind kin = (flags & ACS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   ACS_HIP(ctx, hipMemcpyAsync(b.X, X, sizeof(double) * M * P, kin, s));
@@ -920,49 +835,51 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
     ACS_HIP(ctx, hipMemsetAsync(b.tau, 0, sizeof(double) * C, s));
   ACS_HIP(ctx, hipMemsetAsync(b.tau + C, 0, sizeof(double) * C, s));
   ACS_HIP(ctx, hipMemcpyAsync(b.X + (size_t)M * P, b.X, sizeof(double) * M * P, hipMemcpyDeviceToDevice, s));
-  ACS_HIP(ctx, hipMemcpyAsync(b.wstart, S.ws.data(), sizeof(int) * W, hipMemcpyHostToDevice, s));
-  ACS_HIP(ctx, hipMemcpyAsync(b.wlen, S.wn.data(), sizeof(int) * W, hipMemcpyHostToDevice, s));
   ACS_HIP(ctx, hipMemsetAsync(b.bad, 0, sizeof(int), s));
-  ACS_HIP(ctx, hipStreamSynchronize(s));  // host vectors ws/wn must outlive the copies
+  ACS_HIP(ctx, hipMemsetAsync(b.dtau, 0, sizeof(double) * GR, s));
   return ACS_OK;
 }
 
-static int fte_linearize_launch(acs_ctx* ctx, FteSetup& S, int force) {
+static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
-  hipStream_t s = ctx->stream;
   hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
                      b.st, force, b.Hloc, b.gloc, b.Floc);
   hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.qinv, b.st, force, b.Hloc, b.gloc, b.Ab,
                      b.gb, b.Bt, b.gmaxp);
-  ACS_HIP(ctx, hipGetLastError());
-  return ACS_OK;
 }
 
-static int fte_iteration(acs_ctx* ctx, FteSetup& S, const FteOptsDev& o) {
+// one LM iteration: linearise (if the last step was accepted), cyclic-reduction solve,
+// trial state, exact cost, accept/reject — all device-resident, no host round trip
+static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& o) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
-  hipStream_t s = ctx->stream;
-  int rc;
-  if ((rc = fte_linearize_launch(ctx, S, 0))) return rc;
-  hipLaunchKernelGGL(k_fte_window, dim3(d.W), dim3(256), 0, s, d, b.wstart, b.wlen, b.st, 0, 0.0, b.Ab, b.gb, b.Bt,
-                     b.Lb, b.Y, b.Sw, b.bad);
-  hipLaunchKernelGGL(k_fte_reduced, dim3(1), dim3(256), 0, s, d, b.wstart, b.wlen, b.st, 0, 0.0, b.Ab, b.gb, b.Bt,
-                     b.Hloc, b.gloc, b.Sw, b.gmaxp, b.RA, b.RL, b.LT, b.ry, b.Rt, b.rt, b.dS, b.dtau, b.bad);
-  hipLaunchKernelGGL(k_fte_backsolve, dim3(d.W), dim3(256), 0, s, d, b.wstart, b.wlen, b.st, 0, b.Lb, b.Y, b.dS,
-                     b.dtau, b.delta, b.X, b.tau, b.normp);
+  fte_enqueue_linearize(S, s, 0);
+  hipLaunchKernelGGL(k_cr_build, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc);
+  for (int lv = 0, st = 1; lv < d.nlev; ++lv, st <<= 1) {
+    const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
+    const int ns = (d.nblk + 2 * st - 1) / (2 * st);
+    hipLaunchKernelGGL(k_cr_elim, dim3(ne), dim3(256), 0, s, d, st, b.st, b.Dc, b.Ec, b.GBc, b.Wc, b.Tau, b.bad);
+    hipLaunchKernelGGL(k_cr_update, dim3(ns), dim3(256), 0, s, d, st, b.st, b.Dc, b.Ec, b.GBc, b.Wc);
+  }
+  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, d, b.st, b.Dc, b.GBc, b.Tau, b.Hloc, b.gloc, b.gmaxp, b.dcv,
+                     b.dtau, b.bad);
+  for (int lv = d.nlev - 1; lv >= 0; --lv) {
+    const int st = 1 << lv;
+    const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
+    hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(256), 0, s, d, st, b.st, b.Wc, b.dtau, b.dcv);
+  }
+  hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.X, b.tau, b.normp);
   hipLaunchKernelGGL(k_fte_cost, dim3(d.N), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau, b.qinv,
                      b.st, 1, b.Fm, b.Fq);
   hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 0, b.Fm, b.Fq, b.normp);
-  ACS_HIP(ctx, hipGetLastError());
-  return ACS_OK;
 }
 
 extern "C" {
 
 void acs_fte_default_opts(acs_fte_opts* o) {
   o->max_iters = 200;
-  o->window = 24;
+  o->window = 0;
   o->ftol = 1e-12;
   o->xtol = 1e-12;
   o->gtol = 1e-8;
@@ -980,10 +897,11 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   acs_fte_default_opts(&op);
   if (opts) op = *opts;
   ACS_CHECK(ctx, sd_mode == 0, "fte: only shutter_delay_mode='const' (0) is implemented");
+  ACS_CHECK(ctx, op.max_iters >= 0, "fte: max_iters < 0");
   FteSetup S;
   int rc;
   if ((rc = fte_setup(ctx, S, skel_ints, n_ints, skel_reals, n_reals, cams, n_cams, meas, w, n_frames, shutter_delay,
-                      Ts, qinv, intermode, X, tau, op.window, op.redesc_a, op.redesc_b, op.redesc_c, flags)))
+                      Ts, qinv, intermode, X, tau, op.redesc_a, op.redesc_b, op.redesc_c, flags)))
     return rc;
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
@@ -998,16 +916,45 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
                      b.st, 0, b.Fm, b.Fq);
   hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 1, b.Fm, b.Fq, b.normp);
   ACS_HIP(ctx, hipGetLastError());
+  // capture `chunk` iterations into one hipGraph (kernels read the LM state from device
+  // memory, so the graph is static); replay until the device reports a stop status
+  const int chunk = 4;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  bool use_graph = op.max_iters > 0;
+  if (use_graph) {
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) != hipSuccess) use_graph = false;
+  }
+  if (use_graph) {
+    for (int c = 0; c < chunk; ++c) fte_enqueue_iteration(S, s, o);
+    if (hipStreamEndCapture(s, &graph) != hipSuccess || hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) !=
+                                                            hipSuccess) {
+      if (graph) (void)hipGraphDestroy(graph);
+      (void)hipGetLastError();
+      graph = nullptr;
+      exec = nullptr;
+      use_graph = false;
+    }
+  }
   FteState hs;
-  const int chunk = 4;  // iterations enqueued between host polls of the device status
-  for (int it = 0; it < op.max_iters + 1; it += chunk) {
-    for (int c = 0; c < chunk; ++c)
-      if ((rc = fte_iteration(ctx, S, o))) return rc;
+  std::memset(&hs, 0, sizeof(hs));
+  for (int it = 0; it < op.max_iters + chunk; it += chunk) {
+    if (use_graph) {
+      ACS_HIP(ctx, hipGraphLaunch(exec, s));
+    } else {
+      for (int c = 0; c < chunk; ++c) fte_enqueue_iteration(S, s, o);
+    }
+    ACS_HIP(ctx, hipGetLastError());
     ACS_HIP(ctx, hipMemcpyAsync(&hs, b.st, sizeof(hs), hipMemcpyDeviceToHost, s));
     ACS_HIP(ctx, hipStreamSynchronize(s));
     if (hs.status != 0) break;
   }
-  // outputs: current state
+  if (exec) (void)hipGraphExecDestroy(exec);
+  if (graph) (void)hipGraphDestroy(graph);
+  if (op.max_iters == 0) {
+    ACS_HIP(ctx, hipMemcpyAsync(&hs, b.st, sizeof(hs), hipMemcpyDeviceToHost, s));
+    ACS_HIP(ctx, hipStreamSynchronize(s));
+  }
   const hipMemcpyKind kout = (flags & ACS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
   ACS_HIP(ctx, hipMemcpyAsync(X, b.X + (size_t)hs.cur * d.M * d.P, sizeof(double) * d.M * d.P, kout, s));
   if (tau) ACS_HIP(ctx, hipMemcpyAsync(tau, b.tau + hs.cur * d.C, sizeof(double) * d.C, kout, s));
@@ -1015,7 +962,7 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   ACS_HIP(ctx, hipMemcpyAsync(&nbad, b.bad, sizeof(int), hipMemcpyDeviceToHost, s));
   ACS_HIP(ctx, hipStreamSynchronize(s));
   if (report) {
-    report->status = hs.status;
+    report->status = hs.status == 0 ? ACS_STATUS_MAXITER : hs.status;
     report->iters = hs.iters;
     report->n_accepted = hs.nacc;
     report->n_bad_pivots = nbad;
@@ -1040,7 +987,7 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
   FteSetup S;
   int rc;
   if ((rc = fte_setup(ctx, S, skel_ints, n_ints, skel_reals, n_reals, cams, n_cams, meas, w, n_frames, shutter_delay,
-                      Ts, qinv, intermode, X, tau, 1 << 20, 3.0, 10.0, 20.0, 0)))
+                      Ts, qinv, intermode, X, tau, 3.0, 10.0, 20.0, 0)))
     return rc;
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
@@ -1049,7 +996,7 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
   std::memset(&st0, 0, sizeof(st0));
   st0.relin = 1;
   ACS_HIP(ctx, hipMemcpyAsync(b.st, &st0, sizeof(st0), hipMemcpyHostToDevice, s));
-  if ((rc = fte_linearize_launch(ctx, S, 1))) return rc;
+  fte_enqueue_linearize(S, s, 1);
   hipLaunchKernelGGL(k_fte_cost, dim3(d.N), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau, b.qinv,
                      b.st, 0, b.Fm, b.Fq);
   ACS_HIP(ctx, hipGetLastError());

@@ -1,0 +1,121 @@
+// mfma64.hpp — workgroup-level f64 dense kernels on v_mfma_f64_16x16x4f64 (gfx950).
+//
+// Fragment maps (cdna_hip_programming.md §3): for D(16x16) = A(16x4) B(4x16) + C, lane l
+// supplies A[l & 15][l >> 4] and B[l >> 4][l & 15] (one f64 each); the accumulator holds
+// 4 f64 per lane, element r at row (l >> 4) + 4 r, column l & 15.
+// All matrices are row-major with explicit leading dimensions; M, N are multiples of 16 and
+// K of 4. Every routine is called by all threads of the workgroup (blockDim = 256, 4 waves)
+// and ends with a __syncthreads().
+#pragma once
+#include "common.hpp"
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ dbl4 mfma64(double a, double b, dbl4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// C = beta*C + alpha * op(A) op(B)    (op = transpose when TA / TB)
+template <bool TA, bool TB>
+__device__ void wg_mgemm(double* C, int ldc, const double* A, int lda, const double* B, int ldb, int M, int N, int K,
+                         double alpha, double beta) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int tn = N >> 4, nt = (M >> 4) * tn;
+  const int li = lane & 15, lk = lane >> 4;
+  for (int t = wave; t < nt; t += nw) {
+    const int i0 = (t / tn) << 4, j0 = (t % tn) << 4;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int k0 = 0; k0 < K; k0 += 4) {
+      const int k = k0 + lk;
+      const double a = TA ? A[k * lda + i0 + li] : A[(i0 + li) * lda + k];
+      const double b = TB ? B[(j0 + li) * ldb + k] : B[k * ldb + j0 + li];
+      acc = mfma64(a, b, acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double* c = C + (size_t)(i0 + lk + 4 * r) * ldc + j0 + li;
+      *c = (beta == 0.0 ? 0.0 : beta * *c) + alpha * acc[r];
+    }
+  }
+  __syncthreads();
+}
+
+// In-place inverse of an SPD matrix (n = 16*nb, LDS or global, ld) by blocked
+// Gauss-Jordan without pivoting (SPD + LM damping: every pivot block is SPD).
+// tmp: 512 doubles of LDS. Non-positive pivots are counted in *bad.
+__device__ void wg_spd_inverse(double* A, int lda, int nb, double* tmp, int* bad) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  for (int k = 0; k < nb; ++k) {
+    double* Akk = A + (size_t)(k << 4) * lda + (k << 4);
+    // 1. 16x16 diagonal block: unblocked Gauss-Jordan, one entry per thread, double buffer
+    const int i = tid >> 4, j = tid & 15;
+    if (tid < 256) tmp[tid] = Akk[i * lda + j];
+    __syncthreads();
+    for (int s = 0; s < 16; ++s) {
+      const double* cur = tmp + ((s & 1) << 8);
+      double* nxt = tmp + (((s + 1) & 1) << 8);
+      if (tid < 256) {
+        double p = cur[s * 16 + s];
+        if (!(p > 0.0)) {
+          if (bad && i == 0 && j == 0) atomicAdd(bad, 1);
+          p = 1e-300;
+        }
+        const double ip = 1.0 / p;
+        double v;
+        if (i == s && j == s)
+          v = ip;
+        else if (i == s)
+          v = cur[s * 16 + j] * ip;
+        else if (j == s)
+          v = -cur[i * 16 + s] * ip;
+        else
+          v = cur[i * 16 + j] - cur[i * 16 + s] * cur[s * 16 + j] * ip;
+        nxt[tid] = v;
+      }
+      __syncthreads();
+    }
+    if (tid < 256) Akk[i * lda + j] = tmp[tid];  // 16 steps: result in buffer 0
+    __syncthreads();
+    // 2. row panel A_kJ <- Akk^-1 A_kJ (J != k); each tile read and written by one wave
+    for (int J = wave; J < nb; J += nw) {
+      if (J == k) continue;
+      double* AkJ = A + (size_t)(k << 4) * lda + (J << 4);
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k0 = 0; k0 < 16; k0 += 4) acc = mfma64(Akk[li * lda + k0 + lk], AkJ[(k0 + lk) * lda + li], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) AkJ[(lk + 4 * r) * lda + li] = acc[r];
+    }
+    __syncthreads();
+    // 3. trailing A_IJ -= A_Ik A_kJ (I, J != k)
+    const int nt = nb * nb;
+    for (int t = wave; t < nt; t += nw) {
+      const int I = t / nb, J = t % nb;
+      if (I == k || J == k) continue;
+      double* AIJ = A + (size_t)(I << 4) * lda + (J << 4);
+      const double* AIk = A + (size_t)(I << 4) * lda + (k << 4);
+      const double* AkJ = A + (size_t)(k << 4) * lda + (J << 4);
+      dbl4 acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = AIJ[(lk + 4 * r) * lda + li];
+#pragma unroll
+      for (int k0 = 0; k0 < 16; k0 += 4) acc = mfma64(-AIk[li * lda + k0 + lk], AkJ[(k0 + lk) * lda + li], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) AIJ[(lk + 4 * r) * lda + li] = acc[r];
+    }
+    __syncthreads();
+    // 4. column panel A_Ik <- -A_Ik Akk^-1 (I != k)
+    for (int I = wave; I < nb; I += nw) {
+      if (I == k) continue;
+      double* AIk = A + (size_t)(I << 4) * lda + (k << 4);
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k0 = 0; k0 < 16; k0 += 4) acc = mfma64(-AIk[li * lda + k0 + lk], Akk[(k0 + lk) * lda + li], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) AIk[(lk + 4 * r) * lda + li] = acc[r];
+    }
+    __syncthreads();
+  }
+}

@@ -139,7 +139,7 @@ int acs_fk(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double*
  * not implemented yet and returns ACS_E_INVALID). X and tau are in/out.                */
 typedef struct {
   int32_t max_iters;  /* LM iterations; default 200 */
-  int32_t window;     /* frames per window interior of the banded solve (>= 3); default 24 */
+  int32_t window;     /* reserved (0) */
   double ftol;        /* relative cost decrease (|F|); default 1e-12 */
   double xtol;        /* relative step; default 1e-12 */
   double gtol;        /* max |gradient|; default 1e-8 */

@@ -5,7 +5,7 @@ Tolerances (float64):
   * objective: 1e-10 relative; gradient / GN normal matrix: 1e-8 relative to their max
   * solution vs oracle (same LM spec): 1e-6 m RMS keypoint position (contract 1e-4 m),
     reprojection RMS within 1e-3 px (north_star), tau within 1e-6 s
-  * window partition: any window size gives the same step (exact substructuring), 1e-8
+  * one LM step (the cyclic-reduction solve of the damped normal equations): 1e-9
 """
 import numpy as np
 import pytest
@@ -76,18 +76,20 @@ def test_fte_solve_matches_oracle(ctx, mode, sd, inter, N):
     assert float(np.sqrt(np.mean(np.sum((pg - truth) ** 2, -1)))) < 0.02
 
 
-def test_fte_window_partition_is_exact(ctx):
-    seq, prob, cams = _problem(50)
-    X0 = ofte.initial_state(prob, np.arange(50), seq.pos3d[:, 0, 0])
+@pytest.mark.parametrize('N', [7, 31, 64])
+def test_fte_single_lm_step_matches_oracle(ctx, N):
+    """One LM step (lambda0) = one solve of the damped normal equations: checks the
+    block-cyclic-reduction linear solve (odd/even/power-of-two super-block counts)."""
+    seq, prob, cams = _problem(N)
+    X0 = ofte.initial_state(prob, np.arange(N), seq.pos3d[:, 0, 0])
     table = pkin.build_table(prob.mode)
-    outs = []
-    for wl in (3, 7, 1000):
-        opts = ctx.fte_default_opts(window=wl, max_iters=6)
-        outs.append(ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, opts=opts))
-    for X, tau, rep in outs[:-1]:
-        assert rep['n_bad_pivots'] == 0
-        np.testing.assert_allclose(X, outs[-1][0], rtol=0, atol=1e-8)
-        np.testing.assert_allclose(tau, outs[-1][1], rtol=0, atol=1e-10)
+    X, tau, rep = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
+                                opts=ctx.fte_default_opts(max_iters=1))
+    Xo, to, info = ofte.solve(prob, X0, max_iters=1)
+    assert rep['n_bad_pivots'] == 0 and rep['iters'] == 1 and info['iters'] == 1
+    assert rep['n_accepted'] == info['n_accepted']
+    np.testing.assert_allclose(X, Xo, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(tau, to, rtol=0, atol=1e-12)
 
 
 def test_fte_deterministic(ctx):
