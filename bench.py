@@ -177,7 +177,7 @@ def cpu_baseline(seq, scene, uv, mask, pts0, seconds):
                       f'(oracle/sba.py, numpy float64), {dt:.1f} s'}
 
 
-def bench_fte(ctx, torch, stream, n_frames=1000, steps=3, window=24):
+def bench_fte(ctx, torch, stream, n_frames=1000, steps=5):
     """configs[2]: 6-cam x 1000-frame FTE (20 keypoints, P = 26, shutter delay 'const',
     interpolation 'vel' = the all_optimizations defaults, src/all_optimizations.py:127-136),
     from the reference initialisation (pairwise triangulation on the GPU + nose line fit)."""
@@ -208,7 +208,7 @@ def bench_fte(ctx, torch, stream, n_frames=1000, steps=3, window=24):
     d_ints, d_reals, d_cams, d_meas, d_w, d_q = (T(table.ints, torch.int32), T(table.reals), T(cams), T(meas), T(w),
                                                  T(qinv))
     d_X0, d_X, d_tau = T(X0), T(X0), torch.zeros(C, dtype=torch.float64, device=dev)
-    opts = ctx.fte_default_opts(window=window)
+    opts = ctx.fte_default_opts()
 
     def run():
         d_X.copy_(d_X0)
@@ -238,7 +238,7 @@ def bench_fte(ctx, torch, stream, n_frames=1000, steps=3, window=24):
             'frames_per_s': N / dt, 'ms_per_solve': dt * 1e3, 'status': rep['status_name'], 'iters': rep['iters'],
             'accepted': rep['n_accepted'], 'cost_before': rep['cost_before'], 'cost_after': rep['cost_after'],
             'reproj_rms_px': rms, 'pos_rms_vs_truth_m': pos_rms, 'tau_err_max_s': float(np.abs(tau - seq.tau).max()),
-            'window': window}
+            }
 
 
 if __name__ == '__main__':
