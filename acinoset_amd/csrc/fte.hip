@@ -403,64 +403,152 @@ __global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __r
   }
 }
 
-__global__ __launch_bounds__(256) void k_cr_elim(FteDims d, int s, const FteState* __restrict__ st,
-                                                 const double* __restrict__ Dc, const double* __restrict__ Ec,
-                                                 const double* __restrict__ GBc, double* __restrict__ Wc,
-                                                 double* __restrict__ Tau, int* __restrict__ bad) {
+// LDS budget (BP <= 96): sD + one staged panel, both (BP x BP+1) doubles
+__global__ __launch_bounds__(1024) void k_cr_elim(FteDims d, int s, const FteState* __restrict__ st,
+                                                  const double* __restrict__ Dc, const double* __restrict__ Ec,
+                                                  const double* __restrict__ GBc, double* __restrict__ Wc,
+                                                  double* __restrict__ Tau, int* __restrict__ bad) {
   if (st->status != 0) return;
   const int i = s * (2 * blockIdx.x + 1);
   const int r = (i + s < d.nblk) ? i + s : -1;
-  const int BP = d.BP, GR = d.GR, WL = 2 * BP + GR;
-  __shared__ double sD[CR_MAXBP * CR_MAXBP];
-  __shared__ double tmp[512];
-  const int tid = threadIdx.x;
-  for (int e = tid; e < BP * BP; e += blockDim.x) sD[e] = Dc[(size_t)i * BP * BP + e];
+  const int BP = d.BP, GR = d.GR, WL = 2 * BP + GR, LD = BP + 1;
+  extern __shared__ double lds[];
+  double* sD = lds;                 // BP x LD
+  double* sB = lds + BP * LD;       // BP x LD (panel)
+  double* tmp = sB + BP * LD;       // 512
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  lds_stage<false>(sD, Dc + (size_t)i * BP * BP, BP, BP, BP);
   __syncthreads();
-  wg_spd_inverse(sD, BP, BP >> 4, tmp, bad);
+  wg_spd_inverse(sD, LD, BP >> 4, tmp, bad);
   double* W = Wc + (size_t)i * BP * WL;
-  wg_mgemm<false, false>(W, WL, sD, BP, Ec + (size_t)i * BP * BP, BP, BP, BP, BP, 1.0, 0.0);
-  if (r >= 0)
-    wg_mgemm<false, true>(W + BP, WL, sD, BP, Ec + (size_t)r * BP * BP, BP, BP, BP, BP, 1.0, 0.0);
-  else
-    for (int e = tid; e < BP * BP; e += blockDim.x) W[(e / BP) * WL + BP + e % BP] = 0.0;
-  const double* G = GBc + (size_t)i * BP * GR;
-  wg_mgemm<false, false>(W + 2 * BP, WL, sD, BP, G, GR, BP, GR, BP, 1.0, 0.0);
-  // tau Schur contribution GB_i^T W_gb(i)
-  wg_mgemm<true, false>(Tau + (size_t)i * GR * GR, GR, G, GR, W + 2 * BP, WL, GR, GR, BP, 1.0, 0.0);
+  // W_l = D^-1 E_i ; W_r = D^-1 E_r^T ; W_gb = D^-1 GB_i
+  for (int part = 0; part < 3; ++part) {
+    const int cols = part < 2 ? BP : GR;
+    const int ldb = lds_ld(cols);
+    if (part == 0) lds_stage<false>(sB, Ec + (size_t)i * BP * BP, BP, BP, BP);
+    if (part == 1) {
+      if (r >= 0)
+        lds_stage<true>(sB, Ec + (size_t)r * BP * BP, BP, BP, BP);
+      else
+        for (int e = threadIdx.x; e < BP * ldb; e += blockDim.x) sB[e] = 0.0;
+    }
+    if (part == 2) lds_stage<false>(sB, GBc + (size_t)i * BP * GR, GR, BP, GR);
+    __syncthreads();
+    double* Wp = W + part * BP;
+    lds_gemm(sD, LD, sB, ldb, BP, cols, BP, [&](int i0, int j0, dbl4 acc) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Wp[(size_t)(i0 + lk + 4 * q) * WL + j0 + li] = acc[q];
+    });
+    __syncthreads();
+  }
+  // tau Schur contribution Tau_i = GB_i^T (D^-1 GB_i): A = GB_i^T (staged transposed into sD)
+  lds_stage<true>(sD, GBc + (size_t)i * BP * GR, GR, GR, BP);          // GR x BP
+  lds_stage<false>(sB, W + 2 * BP, WL, BP, GR);                        // BP x GR
+  __syncthreads();
+  double* T = Tau + (size_t)i * GR * GR;
+  lds_gemm(sD, BP + 1, sB, GR + 1, GR, GR, BP, [&](int i0, int j0, dbl4 acc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) T[(i0 + lk + 4 * q) * GR + j0 + li] = acc[q];
+  });
 }
 
-__global__ __launch_bounds__(256) void k_cr_update(FteDims d, int s, const FteState* __restrict__ st,
-                                                   double* __restrict__ Dc, double* __restrict__ Ec,
-                                                   double* __restrict__ GBc, const double* __restrict__ Wc) {
+__global__ __launch_bounds__(1024) void k_cr_update(FteDims d, int s, const FteState* __restrict__ st,
+                                                    double* __restrict__ Dc, double* __restrict__ Ec,
+                                                    double* __restrict__ GBc, const double* __restrict__ Wc) {
   if (st->status != 0) return;
   const int j = 2 * s * blockIdx.x;
   const int a = j - s >= 0 ? j - s : -1;
   const int c = j + s < d.nblk ? j + s : -1;
-  const int BP = d.BP, GR = d.GR, WL = 2 * BP + GR;
-  __shared__ double sE[CR_MAXBP * CR_MAXBP];
+  const int BP = d.BP, GR = d.GR, WL = 2 * BP + GR, LD = BP + 1;
+  extern __shared__ double lds[];
+  double* sA = lds;             // BP x LD
+  double* sB = lds + BP * LD;   // BP x LD
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
   double* D = Dc + (size_t)j * BP * BP;
   double* E = Ec + (size_t)j * BP * BP;
   double* G = GBc + (size_t)j * BP * GR;
+  dbl4 keep[3];
+  int nkeep = 0;
+  auto sub_D = [&](int i0, int j0, dbl4 acc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) D[(size_t)(i0 + lk + 4 * q) * BP + j0 + li] -= acc[q];
+  };
+  auto sub_G = [&](int i0, int j0, dbl4 acc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) G[(size_t)(i0 + lk + 4 * q) * GR + j0 + li] -= acc[q];
+  };
   if (a >= 0) {
     const double* Wa = Wc + (size_t)a * BP * WL;
-    wg_mgemm<false, false>(D, BP, E, BP, Wa + BP, WL, BP, BP, BP, -1.0, 1.0);
-    wg_mgemm<false, false>(G, GR, E, BP, Wa + 2 * BP, WL, BP, GR, BP, -1.0, 1.0);
-    wg_mgemm<false, false>(sE, BP, E, BP, Wa, WL, BP, BP, BP, -1.0, 0.0);
+    lds_stage<false>(sA, E, BP, BP, BP);
+    lds_stage<false>(sB, Wa + BP, WL, BP, BP);          // W_r(a)
+    __syncthreads();
+    lds_gemm(sA, LD, sB, LD, BP, BP, BP, sub_D);
+    __syncthreads();
+    lds_stage<false>(sB, Wa + 2 * BP, WL, BP, GR);      // W_gb(a)
+    __syncthreads();
+    lds_gemm(sA, LD, sB, GR + 1, BP, GR, BP, sub_G);
+    __syncthreads();
+    lds_stage<false>(sB, Wa, WL, BP, BP);               // W_l(a)
+    __syncthreads();
+    lds_gemm(sA, LD, sB, LD, BP, BP, BP, [&](int i0, int j0, dbl4 acc) { keep[nkeep++] = acc; });
+    __syncthreads();
   }
   if (c >= 0) {
     const double* Wcc = Wc + (size_t)c * BP * WL;
-    const double* Ecc = Ec + (size_t)c * BP * BP;
-    wg_mgemm<true, false>(D, BP, Ecc, BP, Wcc, WL, BP, BP, BP, -1.0, 1.0);
-    wg_mgemm<true, false>(G, GR, Ecc, BP, Wcc + 2 * BP, WL, BP, GR, BP, -1.0, 1.0);
+    lds_stage<true>(sA, Ec + (size_t)c * BP * BP, BP, BP, BP);  // E_c^T
+    lds_stage<false>(sB, Wcc, WL, BP, BP);                      // W_l(c)
+    __syncthreads();
+    lds_gemm(sA, LD, sB, LD, BP, BP, BP, sub_D);
+    __syncthreads();
+    lds_stage<false>(sB, Wcc + 2 * BP, WL, BP, GR);             // W_gb(c)
+    __syncthreads();
+    lds_gemm(sA, LD, sB, GR + 1, BP, GR, BP, sub_G);
   }
   if (a >= 0) {
-    for (int e = threadIdx.x; e < BP * BP; e += blockDim.x) E[e] = sE[e];
+    // E_j <- -E_j W_l(a): tiles were assigned to waves in lds_gemm order
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6, tn = BP >> 4, nt = tn * tn;
+    int q = 0;
+    for (int t = wave; t < nt; t += nw, ++q) {
+      const int i0 = (t / tn) << 4, j0 = (t % tn) << 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) E[(size_t)(i0 + lk + 4 * r) * BP + j0 + li] = -keep[q][r];
+    }
+  }
+}
+
+// Fixed-order partial sums feeding the tau border (parallel over chunks, summed in chunk
+// order by k_cr_top): per-frame tau blocks of the normal matrix / gradient, and the tau
+// Schur contributions of every eliminated super-block.
+#define CR_NCHUNK 64
+__global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteState* __restrict__ st,
+                                                        const double* __restrict__ Hloc,
+                                                        const double* __restrict__ gloc,
+                                                        const double* __restrict__ Tau, double* __restrict__ part) {
+  if (st->status != 0) return;
+  const int ch = blockIdx.x;
+  const int P = d.P, Cg = d.Cg, GR = d.GR;
+  const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
+  const int fc = (d.N + CR_NCHUNK - 1) / CR_NCHUNK, bc = (d.nblk + CR_NCHUNK - 1) / CR_NCHUNK;
+  const int k0 = ch * fc, k1 = min(d.N, k0 + fc);
+  const int b0 = max(1, ch * bc), b1 = min(d.nblk, ch * bc + bc);
+  for (int e = threadIdx.x; e < nE; e += blockDim.x) {
+    double v = 0.0;
+    if (e < nH) {
+      const int r = e / Cg, c = e % Cg;
+      for (int k = k0; k < k1; ++k) v += Hloc[(size_t)k * FTE_NZP * FTE_NZP + (P + 6 + r) * FTE_NZP + P + 6 + c];
+    } else if (e < nH + Cg) {
+      const int r = e - nH;
+      for (int k = k0; k < k1; ++k) v += gloc[(size_t)k * FTE_NZP + P + 6 + r];
+    } else {
+      const int t = e - nH - Cg;
+      for (int b = b0; b < b1; ++b) v += Tau[(size_t)b * GR * GR + t];
+    }
+    part[(size_t)ch * nE + e] = v;
   }
 }
 
 __global__ __launch_bounds__(256) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ Dc,
-                                                const double* __restrict__ GBc, const double* __restrict__ Tau,
-                                                const double* __restrict__ Hloc, const double* __restrict__ gloc,
+                                                const double* __restrict__ GBc, const double* __restrict__ part,
                                                 const double* __restrict__ gmaxp, double* __restrict__ dcv,
                                                 double* __restrict__ dtau, int* __restrict__ bad) {
   if (st->status != 0) return;
@@ -473,15 +561,20 @@ __global__ __launch_bounds__(256) void k_cr_top(FteDims d, FteState* __restrict_
   __shared__ double sr[32];
   __shared__ double tmp[512];
   __shared__ double s_red[256];
+  // chunk partials -> sums (fixed order)
+  const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
+  __shared__ double s_sum[16 * 16 + 16 + 32 * 32];
+  for (int e = tid; e < nE; e += nth) {
+    double v = 0.0;
+    for (int ch = 0; ch < CR_NCHUNK; ++ch) v += part[(size_t)ch * nE + e];
+    s_sum[e] = v;
+  }
+  __syncthreads();
   // gradient max (frames + tau border)
   {
     double mx = 0.0;
     for (int f = tid; f < d.M; f += nth) mx = fmax(mx, gmaxp[f]);
-    for (int c = 1 + tid; c < Cg; c += nth) {
-      double gt = 0.0;
-      for (int k = 0; k < d.N; ++k) gt += gloc[(size_t)k * FTE_NZP + P + 6 + c];
-      mx = fmax(mx, fabs(gt));
-    }
+    for (int c = 1 + tid; c < Cg; c += nth) mx = fmax(mx, fabs(s_sum[nH + c]));
     mx = block_max(mx, s_red);
     if (tid == 0) st->gmax = mx;
   }
@@ -496,14 +589,14 @@ __global__ __launch_bounds__(256) void k_cr_top(FteDims d, FteState* __restrict_
     for (int e = tid; e < GR * GR; e += nth) {
       const int r = e / GR, c = e % GR;
       if (r < Cg && c <= Cg) {
-        double h = 0.0;
+        double h;
         if (c < Cg) {
-          for (int k = 0; k < d.N; ++k) h += Hloc[(size_t)k * FTE_NZP * FTE_NZP + (P + 6 + r) * FTE_NZP + P + 6 + c];
+          h = s_sum[r * Cg + c];
           if (r == c) h += lam * fmax(h, 1e-12);
         } else {
-          for (int k = 0; k < d.N; ++k) h -= gloc[(size_t)k * FTE_NZP + P + 6 + r];
+          h = -s_sum[nH + r];
         }
-        for (int b = 1; b < d.nblk; ++b) h -= Tau[(size_t)b * GR * GR + r * GR + c];
+        h -= s_sum[nH + Cg + r * GR + c];
         sS[e] += h;
       }
     }
@@ -726,7 +819,7 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
 struct FteBuffers {
   int* I;
   double *Rl, *cams, *meas, *w, *qinv, *X, *tau;
-  double *Hloc, *gloc, *Floc, *Ab, *gb, *Bt, *gmaxp, *Dc, *Ec, *GBc, *Wc, *Tau, *dcv, *dtau, *normp, *Fm, *Fq;
+  double *Hloc, *gloc, *Floc, *Ab, *gb, *Bt, *gmaxp, *Dc, *Ec, *GBc, *Wc, *Tau, *dcv, *dtau, *normp, *Fm, *Fq, *part;
   int* bad;
   FteState* st;
 };
@@ -801,7 +894,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
                ogb = take((size_t)M * P), oBt = take((size_t)M * P * Cg1), ogm = take(M),
                oD = take((size_t)n * BP * BP), oE = take((size_t)n * BP * BP), oG = take((size_t)n * BP * GR),
                oW = take((size_t)n * BP * (2 * BP + GR)), oTau = take((size_t)n * GR * GR),
-               odc = take((size_t)n * BP), odt = take(GR), onp = take(2 * (size_t)n), oFm = take(N), oFq = take(N),
+               odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)), onp = take(2 * (size_t)n), oFm = take(N), oFq = take(N),
                ost = take(16), oint = take(8);
   double* arena = (double*)acs_ws(ctx, WS_FTE5, off * sizeof(double));
   if (!arena) return ACS_E_NOMEM;
@@ -820,6 +913,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.Wc = arena + oW;
   b.Tau = arena + oTau;
   b.dcv = arena + odc;
+  b.part = arena + opart;
   b.dtau = arena + odt;
   b.normp = arena + onp;
   b.Fm = arena + oFm;
@@ -855,15 +949,18 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
   fte_enqueue_linearize(S, s, 0);
+  const size_t lds_elim = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1) + 512);
+  const size_t lds_upd = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1));
   hipLaunchKernelGGL(k_cr_build, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc);
   for (int lv = 0, st = 1; lv < d.nlev; ++lv, st <<= 1) {
     const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
     const int ns = (d.nblk + 2 * st - 1) / (2 * st);
-    hipLaunchKernelGGL(k_cr_elim, dim3(ne), dim3(256), 0, s, d, st, b.st, b.Dc, b.Ec, b.GBc, b.Wc, b.Tau, b.bad);
-    hipLaunchKernelGGL(k_cr_update, dim3(ns), dim3(256), 0, s, d, st, b.st, b.Dc, b.Ec, b.GBc, b.Wc);
+    hipLaunchKernelGGL(k_cr_elim, dim3(ne), dim3(1024), lds_elim, s, d, st, b.st, b.Dc, b.Ec, b.GBc, b.Wc, b.Tau, b.bad);
+    hipLaunchKernelGGL(k_cr_update, dim3(ns), dim3(1024), lds_upd, s, d, st, b.st, b.Dc, b.Ec, b.GBc, b.Wc);
   }
-  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, d, b.st, b.Dc, b.GBc, b.Tau, b.Hloc, b.gloc, b.gmaxp, b.dcv,
-                     b.dtau, b.bad);
+  hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part);
+  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, d, b.st, b.Dc, b.GBc, b.part, b.gmaxp, b.dcv, b.dtau,
+                     b.bad);
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);

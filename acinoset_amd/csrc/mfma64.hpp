@@ -119,3 +119,41 @@ __device__ void wg_spd_inverse(double* A, int lda, int nb, double* tmp, int* bad
     __syncthreads();
   }
 }
+
+// ---------------------------------------------------------------------------------------
+// LDS-staged variants. Operands are copied into LDS with an odd leading dimension
+// (ld = cols + 1 doubles) so that the 16 rows a fragment touches land on distinct banks;
+// the MFMA loop then reads only LDS. `consume(i0, j0, acc)` receives each finished
+// 16x16 tile (lane layout: element r at row i0 + (lane>>4) + 4r, column j0 + (lane&15)).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int lds_ld(int cols) { return cols + 1; }
+
+// dst (rows x cols, ld = cols+1) <- src (row-major, ld_src) or its transpose
+template <bool TRANS>
+__device__ void lds_stage(double* dst, const double* __restrict__ src, int ld_src, int rows, int cols) {
+  const int ld = lds_ld(cols);
+  for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
+    if (TRANS) {
+      const int c = e / rows, r = e % rows;  // coalesced along the source rows
+      dst[r * ld + c] = src[(size_t)c * ld_src + r];
+    } else {
+      const int r = e / cols, c = e % cols;
+      dst[r * ld + c] = src[(size_t)r * ld_src + c];
+    }
+  }
+}
+
+template <typename F>
+__device__ void lds_gemm(const double* A, int lda, const double* B, int ldb, int M, int N, int K, F&& consume) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int tn = N >> 4, nt = (M >> 4) * tn;
+  const int li = lane & 15, lk = lane >> 4;
+  for (int t = wave; t < nt; t += nw) {
+    const int i0 = (t / tn) << 4, j0 = (t % tn) << 4;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int k0 = 0; k0 < K; k0 += 4)
+      acc = mfma64(A[(i0 + li) * lda + k0 + lk], B[(k0 + lk) * ldb + j0 + li], acc);
+    consume(i0, j0, acc);
+  }
+}
