@@ -225,7 +225,7 @@ class Context:
 
     # ---- a4 -------------------------------------------------------------------------
     @staticmethod
-    def sba_opts(f_scale=50.0, max_iters=100, ftol=1e-15, xtol=1e-10, gtol=1e-10):
+    def sba_opts(f_scale=50.0, max_iters=100, ftol=1e-15, xtol=1e-9, gtol=1e-10):
         return SbaOpts(int(max_iters), 0, float(f_scale), float(ftol), float(xtol), float(gtol))
 
     def sba_points(self, cams, uv, pt_idx, cam_idx, pts0, opts=None, residuals=True):

@@ -73,7 +73,7 @@ void acs_sba_default_opts(acs_sba_opts* o) {
   o->reserved = 0;
   o->f_scale = 50.0;
   o->ftol = 1e-15;
-  o->xtol = 1e-10;
+  o->xtol = 1e-9;
   o->gtol = 1e-10;
 }
 

@@ -10,13 +10,16 @@
 // slots, <= 64) — lane l owns slot l (+ j*G). Observations are an (n_pts, K) slot tensor
 // (slot = camera for the dense core.sba layout) read once, coalesced, into registers;
 // the camera records are staged in LDS. Each LM iteration: every lane projects its
-// observation(s) and forms its IRLS contribution to H = sum w J^T J (6), g (3) and the
-// Cauchy cost (1); a butterfly __shfl_xor reduction inside the group gives every lane
+// observation(s) and forms its contribution to the gradient g = sum rho'(z) r J (3), the
+// Gauss-Newton matrix H = sum max(rho' + 2 z rho'', 0.1 rho') J^T J (6; Triggs-corrected,
+// which converges quadratically where IRLS weights only converge linearly) and the Cauchy
+// cost (1); a butterfly __shfl_xor reduction inside the group gives every lane
 // bit-identical sums, so all lanes take the same accept/reject decision with no LDS
 // round trip and no atomics. The whole LM loop runs inside one launch: HBM traffic is
 // the observation tensor once plus the points in and out.
 //
 // LM spec (shared with oracle/sba.py): lam0 = 1e-3, Marquardt damping H + lam*diag(H),
+// xtol default 1e-9 (scipy's default, used by the reference, is 1e-8),
 // accept on strict decrease (lam /= 10, floor 1e-15), reject (lam *= 10); stop on
 // gtol / ftol / xtol / lam > 1e16 / max_iters.
 #include <hipcub/hipcub.hpp>
@@ -111,19 +114,21 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
 #pragma unroll
       for (int d = 0; d < 2; ++d) {
         const double z = r[d] * r[d] * if2;
-        const double w = 1.0 / (1.0 + z);
+        const double w = 1.0 / (1.0 + z);                   // rho'(z): gradient weight
+        const double wh = fmax((1.0 - z) * w * w, 0.1 * w);  // rho' + 2 z rho'' (Triggs), floored
         Fl += log1p(z);
         const double j0 = o.J[3 * d], j1 = o.J[3 * d + 1], j2 = o.J[3 * d + 2];
-        const double wj0 = w * j0, wj1 = w * j1, wj2 = w * j2;
-        H[0] += wj0 * j0;
-        H[1] += wj0 * j1;
-        H[2] += wj0 * j2;
-        H[3] += wj1 * j1;
-        H[4] += wj1 * j2;
-        H[5] += wj2 * j2;
-        g[0] += wj0 * r[d];
-        g[1] += wj1 * r[d];
-        g[2] += wj2 * r[d];
+        const double hj0 = wh * j0, hj1 = wh * j1, hj2 = wh * j2;
+        H[0] += hj0 * j0;
+        H[1] += hj0 * j1;
+        H[2] += hj0 * j2;
+        H[3] += hj1 * j1;
+        H[4] += hj1 * j2;
+        H[5] += hj2 * j2;
+        const double wr = w * r[d];
+        g[0] += wr * j0;
+        g[1] += wr * j1;
+        g[2] += wr * j2;
       }
     }
 #pragma unroll

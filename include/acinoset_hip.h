@@ -61,7 +61,7 @@ typedef struct {
   int32_t reserved;
   double f_scale;     /* Cauchy soft-threshold in px; reference default 50 (src/lib/sba.py:181) */
   double ftol;        /* relative cost decrease; reference passes 1e-15 (src/lib/sba.py:189) */
-  double xtol;        /* relative step; default 1e-10 */
+  double xtol;        /* relative step; default 1e-9 (scipy default 1e-8) */
   double gtol;        /* max |gradient|; default 1e-10 */
 } acs_sba_opts;
 

@@ -12,11 +12,13 @@ least-squares problems (the reference output equals the
 per-point minimiser to <= 4e-8 m).
 
 This module minimises each point's cost  F = 0.5 f^2 sum log1p((r/f)^2)  with the same
-safeguarded Levenberg-Marquardt the HIP kernel runs (IRLS Gauss-Newton normal matrix
-H = sum w J^T J, w = 1/(1 + (r/f)^2); Marquardt damping H + lam*diag(H); accept only on
-strict cost decrease). Spec shared with `acinoset_amd/csrc/sba.hip`:
+safeguarded Levenberg-Marquardt the HIP kernel runs: gradient g = sum w r J with
+w = rho'(z) = 1/(1 + z), z = (r/f)^2; Gauss-Newton matrix H = sum wh J^T J with the
+Triggs-corrected weight wh = max(rho' + 2 z rho'', 0.1 rho') = max((1-z) w^2, 0.1 w);
+Marquardt damping H + lam*diag(H); accept only on strict cost decrease. Spec shared with
+`acinoset_amd/csrc/sba.hip`:
 
-    lam0 = 1e-3; accept: lam = max(lam/10, 1e-15); reject: lam *= 10
+    lam0 = 1e-3; accept: lam = max(lam/10, 1e-15); reject: lam *= 10; xtol default 1e-9
     stop: |g|_inf <= gtol | accepted and (dF <= ftol*F or |dx| <= xtol*(xtol+|x|))
           | rejected and |dx| <= xtol*(xtol+|x|) | lam > 1e16 | iters >= max_iters
 """
@@ -51,7 +53,7 @@ def _group(point_idx, n_pts):
 
 
 def sba_points(points_2d, points_3d, point_idx, cam_idx, K, D, R, t, f_scale=50.0, max_iters=100,
-               ftol=1e-15, xtol=1e-10, gtol=1e-10, return_info=False):
+               ftol=1e-15, xtol=1e-9, gtol=1e-10, return_info=False):
     """Batched per-point LM. Returns optimised points (n_pts, 3) [, info dict]."""
     uvobs = np.asarray(points_2d, np.float64)
     x = np.array(points_3d, np.float64).reshape(-1, 3)
@@ -80,7 +82,8 @@ def sba_points(points_2d, points_3d, point_idx, cam_idx, K, D, R, t, f_scale=50.
         r = np.where(valid[..., None], uv - meas, 0.0)
         z = r * r / f2
         w = np.where(valid[..., None], 1.0 / (1.0 + z), 0.0)
-        H = np.einsum('nkd,nkdi,nkdj->nij', w, J, J)
+        wh = np.where(valid[..., None], np.maximum((1.0 - z) * w * w, 0.1 * w), 0.0)
+        H = np.einsum('nkd,nkdi,nkdj->nij', wh, J, J)
         g = np.einsum('nkd,nkd,nkdi->ni', w, r, J)
         F = 0.5 * f2 * np.log1p(z).sum((1, 2))
         return F, H, g
