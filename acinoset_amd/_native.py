@@ -34,6 +34,7 @@ SYMBOLS = (
     'acs_abi_version', 'acs_device_count', 'acs_sba_default_opts', 'acs_project_fisheye',
     'acs_sba_residuals', 'acs_sba_points', 'acs_sba_points_dense', 'acs_redescending_loss', 'acs_fk',
     'acs_fte_default_opts', 'acs_fte_solve', 'acs_fte_eval', 'acs_triangulate_pairs', 'acs_triangulate_dense',
+    'acs_sba_ext_default_opts', 'acs_sba_extrinsics',
 )
 
 
@@ -75,6 +76,22 @@ class FteReport(C.Structure):
         return d
 
 
+class SbaExtOpts(C.Structure):
+    _fields_ = [('max_iters', C.c_int32), ('reserved', C.c_int32), ('f_scale', C.c_double), ('ftol', C.c_double),
+                ('xtol', C.c_double), ('gtol', C.c_double), ('lambda0', C.c_double)]
+
+
+class SbaExtReport(C.Structure):
+    _fields_ = [('status', C.c_int32), ('iters', C.c_int32), ('n_accepted', C.c_int32), ('n_bad_pivots', C.c_int32),
+                ('cost_before', C.c_double), ('cost_after', C.c_double), ('grad_max', C.c_double),
+                ('lambda_final', C.c_double)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d['status_name'] = STATUS_NAMES[self.status] if 0 <= self.status < 7 else str(self.status)
+        return d
+
+
 _lib = None
 _lock = threading.Lock()
 _P = C.c_void_p
@@ -107,6 +124,9 @@ def _declare(lib):
                                    _P, _P, _P, u32]),
         'acs_triangulate_pairs': (C.c_int, [_P, _P, i32, _P, _P, _P, _P, i64, _P, u32]),
         'acs_triangulate_dense': (C.c_int, [_P, _P, i32, _P, _P, i64, _P, _P, u32]),
+        'acs_sba_ext_default_opts': (None, [C.POINTER(SbaExtOpts)]),
+        'acs_sba_extrinsics': (C.c_int, [_P, _P, i32, _P, _P, _P, i64, _P, i64, C.POINTER(SbaExtOpts), _P, _P,
+                                         C.POINTER(SbaExtReport), u32]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name):
@@ -264,6 +284,30 @@ class Context:
                                                  C.byref(rep) if rep is not None else None, ACS_DEVICE_PTRS),
                    'acs_sba_points_dense')
         return rep.as_dict() if rep is not None else None
+
+    # ---- a6 -------------------------------------------------------------------------
+    def sba_ext_opts(self, **kw):
+        o = SbaExtOpts()
+        self.lib.acs_sba_ext_default_opts(C.byref(o))
+        for k, v in kw.items():
+            setattr(o, k, v)
+        return o
+
+    def sba_extrinsics(self, cams, uv, pt_idx, cam_idx, pts0, opts=None, residuals=True):
+        """Points + camera extrinsics LM. Returns (cams (C,20), pts (n,3), res_before, res_after, report)."""
+        cams = _c64(cams).copy()
+        uv = _c64(uv).reshape(-1, 2)
+        pi = np.ascontiguousarray(pt_idx, np.int32)
+        ci = np.ascontiguousarray(cam_idx, np.int32)
+        pts = _c64(pts0).reshape(-1, 3).copy()
+        rb = np.empty(2 * len(uv)) if residuals else None
+        ra = np.empty(2 * len(uv)) if residuals else None
+        rep = SbaExtReport()
+        opts = opts or self.sba_ext_opts()
+        self.check(self.lib.acs_sba_extrinsics(self.h, _ptr(cams), len(cams), _ptr(uv), _ptr(pi), _ptr(ci), len(uv),
+                                               _ptr(pts), len(pts), C.byref(opts), _ptr(rb), _ptr(ra),
+                                               C.byref(rep), 0), 'acs_sba_extrinsics')
+        return cams, pts, rb, ra, rep.as_dict()
 
     # ---- a9 -------------------------------------------------------------------------
     def redescending_loss(self, err, a=3.0, b=10.0, c=20.0, deriv=False):

@@ -62,6 +62,11 @@ void* acs_out_buf(acs_ctx* ctx, int slot, void* dst, size_t bytes, uint32_t flag
 
 static inline int acs_grid(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
+// Observation list (any order) -> per-point slot tensor (n_pts, K): uv_pad, mask, camid,
+// deterministic (stable radix sort by point id). Defined in sba.hip. *K_out = max obs/pt.
+int acs_obs_to_slots(acs_ctx* ctx, const double* duv, const int32_t* dpi, const int32_t* dci, int64_t n_obs,
+                     int64_t n_pts, int n_cams, double2** uv_pad, uint8_t** mask, uint8_t** camid, int* K_out);
+
 // ------------------------------------------------------------------------------------
 // Fisheye camera model (cv::fisheye::projectPoints with alpha = 0; src/lib/calib.py:132,
 // restated by the reference itself in src/core/fte.py:80-96). Camera record layout:
@@ -69,7 +74,9 @@ static inline int acs_grid(int64_t n, int block) { return (int)((n + block - 1) 
 // ------------------------------------------------------------------------------------
 struct ProjOut {
   double u, v;
-  double J[6];  // d(u,v)/dX, row-major 2x3
+  double J[6];   // d(u,v)/dX (world point), row-major 2x3
+  double JY[6];  // d(u,v)/dY (camera-frame point Y = R X + t)
+  double Y[3];
 };
 
 template <bool JAC, bool FTE_FORM = false>
@@ -109,6 +116,15 @@ __device__ __forceinline__ void fisheye_project(const double* __restrict__ c, do
     // d(u,v)/dY = J_uv_ab * [[iz, 0, -a iz], [0, iz, -b iz]]
     const double u0 = duda * iz, u1 = dudb * iz, u2 = -(duda * a + dudb * b) * iz;
     const double v0 = dvda * iz, v1 = dvdb * iz, v2 = -(dvda * a + dvdb * b) * iz;
+    o.JY[0] = u0;
+    o.JY[1] = u1;
+    o.JY[2] = u2;
+    o.JY[3] = v0;
+    o.JY[4] = v1;
+    o.JY[5] = v2;
+    o.Y[0] = Y0;
+    o.Y[1] = Y1;
+    o.Y[2] = Y2;
     // times R
     o.J[0] = u0 * c[8] + u1 * c[11] + u2 * c[14];
     o.J[1] = u0 * c[9] + u1 * c[12] + u2 * c[15];

@@ -405,6 +405,54 @@ static int run_report(acs_ctx* ctx, const double* c0, const double* c1, const in
   return ACS_OK;
 }
 
+int acs_obs_to_slots(acs_ctx* ctx, const double* duv, const int32_t* dpi, const int32_t* dci, int64_t n_obs,
+                     int64_t n_pts, int n_cams, double2** uv_pad, uint8_t** mask, uint8_t** camid, int* K_out) {
+  hipStream_t s = ctx->stream;
+  // stable sort of observation ids by point id
+  int32_t* skey = (int32_t*)acs_ws(ctx, WS_SORT0, sizeof(int32_t) * n_obs);
+  int32_t* vin = (int32_t*)acs_ws(ctx, WS_SORT1, sizeof(int32_t) * n_obs);
+  int32_t* sval = (int32_t*)acs_ws(ctx, WS_SORT2, sizeof(int32_t) * n_obs);
+  int32_t* cnt = (int32_t*)acs_ws(ctx, WS_TMP0, sizeof(int32_t) * (n_pts + 2));
+  int32_t* start = (int32_t*)acs_ws(ctx, WS_TMP1, sizeof(int32_t) * (n_pts + 1));
+  if (!skey || !vin || !sval || !cnt || !start) return ACS_E_NOMEM;
+  hipLaunchKernelGGL(k_iota, dim3(acs_grid(n_obs, 256)), dim3(256), 0, s, vin, n_obs);
+  size_t tb0 = 0, tb1 = 0, tb2 = 0;
+  ACS_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, tb0, dpi, skey, (const int32_t*)vin, sval,
+                                                   (int)n_obs, 0, 32, s));
+  ACS_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, cnt, start, (int)n_pts, s));
+  ACS_HIP(ctx, hipcub::DeviceReduce::Max(nullptr, tb2, cnt, cnt + n_pts, (int)n_pts, s));
+  size_t tb = std::max(tb0, std::max(tb1, tb2));
+  void* tmp = acs_ws(ctx, WS_SORT3, tb);
+  if (!tmp) return ACS_E_NOMEM;
+  ACS_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, tb, dpi, skey, (const int32_t*)vin, sval,
+                                                   (int)n_obs, 0, 32, s));
+  ACS_HIP(ctx, hipMemsetAsync(cnt, 0, sizeof(int32_t) * (n_pts + 2), s));
+  hipLaunchKernelGGL(k_count, dim3(acs_grid(n_obs, 256)), dim3(256), 0, s, dpi, n_obs, cnt, n_pts,
+                     cnt + n_pts + 1);
+  ACS_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, start, (int)n_pts, s));
+  ACS_HIP(ctx, hipcub::DeviceReduce::Max(tmp, tb, cnt, cnt + n_pts, (int)n_pts, s));
+  int32_t hk[2] = {0, 0};
+  ACS_HIP(ctx, hipMemcpyAsync(hk, cnt + n_pts, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, s));
+  ACS_HIP(ctx, hipStreamSynchronize(s));
+  ACS_CHECK(ctx, hk[1] == 0, "acs_sba_points: %d point indices out of [0, %lld)", hk[1], (long long)n_pts);
+  const int K = hk[0] < 1 ? 1 : hk[0];
+  ACS_CHECK(ctx, K <= 256, "acs_sba_points: a point has %d observations (max 256)", K);
+  double2* uvp = (double2*)acs_ws(ctx, WS_TMP2, sizeof(double2) * n_pts * K);
+  uint8_t* mk = (uint8_t*)acs_ws(ctx, WS_TMP3, (size_t)n_pts * K);
+  uint8_t* cid = (uint8_t*)acs_ws(ctx, WS_TMP4, (size_t)n_pts * K);
+  if (!uvp || !mk || !cid) return ACS_E_NOMEM;
+  ACS_HIP(ctx, hipMemsetAsync(mk, 0, (size_t)n_pts * K, s));
+  hipLaunchKernelGGL(k_scatter_slots, dim3(acs_grid(n_obs, 256)), dim3(256), 0, s, skey, sval, n_obs, start,
+                     (const double2*)duv, dci, K, n_cams, uvp, mk, cid);
+  ACS_HIP(ctx, hipGetLastError());
+
+  *uv_pad = uvp;
+  *mask = mk;
+  *camid = cid;
+  *K_out = K;
+  return ACS_OK;
+}
+
 extern "C" {
 
 int acs_sba_points_dense(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv, const uint8_t* mask,
@@ -464,43 +512,12 @@ int acs_sba_points(acs_ctx* ctx, const double* cams, int32_t n_cams, const doubl
     ACS_HIP(ctx, hipGetLastError());
   }
 
-  // stable sort of observation ids by point id
-  int32_t* skey = (int32_t*)acs_ws(ctx, WS_SORT0, sizeof(int32_t) * n_obs);
-  int32_t* vin = (int32_t*)acs_ws(ctx, WS_SORT1, sizeof(int32_t) * n_obs);
-  int32_t* sval = (int32_t*)acs_ws(ctx, WS_SORT2, sizeof(int32_t) * n_obs);
-  int32_t* cnt = (int32_t*)acs_ws(ctx, WS_TMP0, sizeof(int32_t) * (n_pts + 2));
-  int32_t* start = (int32_t*)acs_ws(ctx, WS_TMP1, sizeof(int32_t) * (n_pts + 1));
-  if (!skey || !vin || !sval || !cnt || !start) return ACS_E_NOMEM;
-  hipLaunchKernelGGL(k_iota, dim3(acs_grid(n_obs, 256)), dim3(256), 0, s, vin, n_obs);
-  size_t tb0 = 0, tb1 = 0, tb2 = 0;
-  ACS_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, tb0, (const int32_t*)dpi, skey, (const int32_t*)vin, sval,
-                                                   (int)n_obs, 0, 32, s));
-  ACS_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, cnt, start, (int)n_pts, s));
-  ACS_HIP(ctx, hipcub::DeviceReduce::Max(nullptr, tb2, cnt, cnt + n_pts, (int)n_pts, s));
-  size_t tb = std::max(tb0, std::max(tb1, tb2));
-  void* tmp = acs_ws(ctx, WS_SORT3, tb);
-  if (!tmp) return ACS_E_NOMEM;
-  ACS_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, tb, (const int32_t*)dpi, skey, (const int32_t*)vin, sval,
-                                                   (int)n_obs, 0, 32, s));
-  ACS_HIP(ctx, hipMemsetAsync(cnt, 0, sizeof(int32_t) * (n_pts + 2), s));
-  hipLaunchKernelGGL(k_count, dim3(acs_grid(n_obs, 256)), dim3(256), 0, s, (const int32_t*)dpi, n_obs, cnt, n_pts,
-                     cnt + n_pts + 1);
-  ACS_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, start, (int)n_pts, s));
-  ACS_HIP(ctx, hipcub::DeviceReduce::Max(tmp, tb, cnt, cnt + n_pts, (int)n_pts, s));
-  int32_t hk[2] = {0, 0};
-  ACS_HIP(ctx, hipMemcpyAsync(hk, cnt + n_pts, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, s));
-  ACS_HIP(ctx, hipStreamSynchronize(s));
-  ACS_CHECK(ctx, hk[1] == 0, "acs_sba_points: %d point indices out of [0, %lld)", hk[1], (long long)n_pts);
-  const int K = hk[0] < 1 ? 1 : hk[0];
-  ACS_CHECK(ctx, K <= 256, "acs_sba_points: a point has %d observations (max 256)", K);
-  double2* uvp = (double2*)acs_ws(ctx, WS_TMP2, sizeof(double2) * n_pts * K);
-  uint8_t* mk = (uint8_t*)acs_ws(ctx, WS_TMP3, (size_t)n_pts * K);
-  uint8_t* cid = (uint8_t*)acs_ws(ctx, WS_TMP4, (size_t)n_pts * K);
-  if (!uvp || !mk || !cid) return ACS_E_NOMEM;
-  ACS_HIP(ctx, hipMemsetAsync(mk, 0, (size_t)n_pts * K, s));
-  hipLaunchKernelGGL(k_scatter_slots, dim3(acs_grid(n_obs, 256)), dim3(256), 0, s, skey, sval, n_obs, start,
-                     (const double2*)duv, (const int32_t*)dci, K, n_cams, uvp, mk, cid);
-  ACS_HIP(ctx, hipGetLastError());
+  double2* uvp;
+  uint8_t *mk, *cid;
+  int K;
+  if ((rc = acs_obs_to_slots(ctx, (const double*)duv, (const int32_t*)dpi, (const int32_t*)dci, n_obs, n_pts, n_cams,
+                             &uvp, &mk, &cid, &K)))
+    return rc;
 
   double *c0, *c1;
   int* st;

@@ -137,3 +137,26 @@ def cost_func_points_extrinsics(params, n_cams, n_points, point_3d_indices, came
     obj, r_arr, t_arr = params_to_points_extrinsics(np.asarray(params, np.float64), n_cams, n_points)
     return cost_func_points_only(obj.ravel(), n_points, point_3d_indices, camera_indices, k_arr, d_arr, r_arr, t_arr,
                                  points_2d)
+
+
+def bundle_adjust_points_and_extrinsics(points_2d, points_3d, point_3d_indices, camera_indices, k_arr, d_arr, r_arr,
+                                        t_arr, project_func=None, f_scale=1.0, **opts):
+    """`src/lib/sba.py:158-178` -> acs_sba_extrinsics: points and every camera's rotation and
+    translation refined together (intrinsics fixed) on the same Cauchy objective (scipy's
+    default f_scale = 1). Returns (obj_pts (n,3), r_arr (C,3,3), t_arr (C,3,1),
+    {'before', 'after'}) like the reference; rotations stay orthonormal matrices (updated
+    on SO(3), which is what the reference's Rodrigues round trip represents)."""
+    ctx = _native.default_context()
+    n = len(k_arr)
+    o = ctx.sba_ext_opts(f_scale=float(f_scale), **opts)
+    t0 = time()
+    cams, pts, rb, ra, rep = ctx.sba_extrinsics(_cams(k_arr, d_arr, r_arr, t_arr), np.asarray(points_2d, np.float64),
+                                                np.asarray(point_3d_indices), np.asarray(camera_indices),
+                                                np.asarray(points_3d, np.float64), o)
+    t1 = time()
+    print(f'GPU SBA (points + extrinsics): {len(pts)} points, {n} cameras, {rep["iters"]} iterations, cost '
+          f'{rep["cost_before"]:.6e} -> {rep["cost_after"]:.6e} ({rep["status_name"]})')
+    print(f'\nOptimization took {t1 - t0:.2f} seconds')
+    r_out = cams[:, 8:17].reshape(n, 3, 3).copy()
+    t_out = cams[:, 17:20].reshape(n, 3, 1).copy()
+    return pts, r_out, t_out, dict(before=rb, after=ra)

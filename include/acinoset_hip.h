@@ -184,6 +184,31 @@ int acs_triangulate_dense(acs_ctx* ctx, const double* cams, int32_t n_cams, cons
                           const uint8_t* mask, int64_t n_pts, double* xyz_out, int32_t* n_pairs_out,
                           uint32_t flags);
 
+/* ---- §8(a) a6: bundle adjustment of points AND extrinsics ---------------------------
+ * bundle_adjust_points_and_extrinsics (src/lib/sba.py:158-178): least_squares(trf,
+ * loss='cauchy', f_scale=1) over cost_func_points_extrinsics (:142-146), x = [rvecs, tvecs,
+ * points]. Schur-complement LM on the GPU; cams (n_cams <= 16 records) and pts are in/out
+ * (rotation and translation of every camera refined, intrinsics kept). Observation list
+ * form as acs_sba_points; a point may have at most 64 observations.                   */
+typedef struct {
+  int32_t max_iters;  /* LM iterations; default 500 */
+  int32_t reserved;
+  double f_scale;     /* Cauchy scale; default 1 (scipy default used at sba.py:168) */
+  double ftol, xtol, gtol;  /* defaults 1e-12, 1e-12, 1e-8 */
+  double lambda0;     /* default 1e-3 */
+} acs_sba_ext_opts;
+
+typedef struct {
+  int32_t status, iters, n_accepted, n_bad_pivots;
+  double cost_before, cost_after, grad_max, lambda_final;
+} acs_sba_ext_report;
+
+void acs_sba_ext_default_opts(acs_sba_ext_opts* o);
+int acs_sba_extrinsics(acs_ctx* ctx, double* cams, int32_t n_cams, const double* uv,
+                       const int32_t* pt_idx, const int32_t* cam_idx, int64_t n_obs, double* pts,
+                       int64_t n_pts, const acs_sba_ext_opts* opts, double* resid_before,
+                       double* resid_after, acs_sba_ext_report* report, uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

@@ -122,3 +122,64 @@ def test_oracle_triangulation_matches_reference():
     assert len(ref) == len(fr)
     for f, m, p in zip(fr, mk, xyz):
         np.testing.assert_allclose(p, ref[(f, m)], atol=1e-9)
+
+
+def _ext_args(g):
+    return (g['K'], g['D'].reshape(-1, 4), g['points_2d'], g['point_indices'].astype(np.int64),
+            g['camera_indices'].astype(np.int64))
+
+
+def test_oracle_sba_extrinsics_cost_matches_reference():
+    """Golden `bundle_adjust_points_and_extrinsics` (src/lib/sba.py:158-178): the oracle's
+    residual function reproduces the reference's before/after residual vectors at the
+    reference's own initial and final states."""
+    from oracle import sba_ext
+    g = golden('sba_extrinsics')
+    K, D, uv, pi, ci = _ext_args(g)
+    r0 = sba_ext.residuals(g['points_3d'], g['R0'], g['t0'].reshape(-1, 3), K, D, uv, pi, ci)
+    np.testing.assert_allclose(r0.ravel(), g['resid_before'], atol=1e-9)
+    r1 = sba_ext.residuals(g['obj_out'], g['R_out'], g['t_out'].reshape(-1, 3), K, D, uv, pi, ci)
+    np.testing.assert_allclose(r1.ravel(), g['resid_after'], atol=1e-6)
+
+
+def test_oracle_sba_extrinsics_jacobian_fd():
+    """Left-perturbation camera Jacobian [-J_Y [R X]x | J_Y] and point Jacobian J_Y R vs
+    central differences of the residual function."""
+    from oracle import sba_ext
+    g = golden('sba_extrinsics')
+    K, D, uv, pi, ci = _ext_args(g)
+    X, R, t = g['points_3d'], g['R0'], g['t0'].reshape(-1, 3)
+    *_, Jc, Jp = sba_ext.linearize(X, R, t, K, D, uv, pi, ci, 1.0)
+    h = 1e-6
+    for k in range(6):
+        c = 2
+        dw = np.zeros(6)
+        dw[k] = h
+        def res(s):
+            Rn, tn = R.copy(), t.copy()
+            Rn[c] = sba_ext.rodrigues(s * dw[:3]) @ R[c]
+            tn[c] = t[c] + s * dw[3:]
+            return sba_ext.residuals(X, Rn, tn, K, D, uv, pi, ci)
+        fd = (res(1) - res(-1)) / (2 * h)
+        sel = ci == c
+        np.testing.assert_allclose(Jc[sel, :, k], fd[sel], rtol=1e-5, atol=1e-3)
+    for k in range(3):
+        e = np.zeros(3)
+        e[k] = h
+        fd = (sba_ext.residuals(X + e, R, t, K, D, uv, pi, ci) - sba_ext.residuals(X - e, R, t, K, D, uv, pi, ci)) / (
+            2 * h)
+        np.testing.assert_allclose(Jp[..., k], fd, rtol=1e-5, atol=1e-3)
+
+
+def test_oracle_sba_extrinsics_beats_reference_cost():
+    """Parity on the objective (scipy stopped unconverged): the oracle's
+    Schur LM reaches a robust cost no larger than the reference's final state."""
+    from oracle import sba_ext
+    g = golden('sba_extrinsics')
+    K, D, uv, pi, ci = _ext_args(g)
+    X, R, t, info = sba_ext.sba_extrinsics(uv, g['points_3d'], pi, ci, K, D, g['R0'], g['t0'], max_iters=200)
+    c_ref = 0.5 * np.log1p(g['resid_after'] ** 2).sum()
+    c0 = 0.5 * np.log1p(g['resid_before'] ** 2).sum()
+    assert abs(info['cost_before'] - c0) < 1e-9 * c0
+    assert info['cost_after'] <= c_ref
+    np.testing.assert_allclose(R @ np.swapaxes(R, 1, 2), np.broadcast_to(np.eye(3), R.shape), atol=1e-12)
