@@ -26,6 +26,10 @@
 #define EXT_MAXC 16
 #define EXT_CHUNK 64
 #define EXT_Q 45  // per slot: U (21 packed upper) + g_c (6) + W (18)
+// damping floor: the 7-DoF similarity gauge is left free (as in the reference), so the
+// reduced camera system is singular up to lambda; below ~1e-8 its gauge directions are
+// resolved by rounding alone. Spec shared with oracle/sba_ext.py (LAM_MIN).
+#define EXT_LAM_MIN 1e-7
 
 struct ExtDims {
   int n, K, C, G, chunk;  // chunk: points per k_ext_schur block (LDS-sized)
@@ -219,7 +223,8 @@ __global__ __launch_bounds__(256) void k_ext_schur(ExtDims d, const ExtState* __
 
 __global__ __launch_bounds__(256) void k_ext_solve(ExtDims d, ExtState* __restrict__ st, int nchunk,
                                                    const double* __restrict__ part, const double* __restrict__ Vg,
-                                                   double* __restrict__ dc, int* __restrict__ bad) {
+                                                   double* __restrict__ dc, double* __restrict__ Sg,
+                                                   int* __restrict__ bad) {
   if (st->status != 0) return;
   const int NC = 6 * d.C, NP = ((NC + 15) / 16) * 16, nE = NC * NC + 3 * NC, LD = NP + 1;
   const double lam = st->lam;
@@ -242,6 +247,7 @@ __global__ __launch_bounds__(256) void k_ext_solve(ExtDims d, ExtState* __restri
       v = 1.0;
     }
     sS[r * LD + c] = v;
+    if (r < NC && c < NC) Sg[r * NC + c] = v;  // kept for the refinement step
   }
   double gm = 0.0;
   for (int r = threadIdx.x; r < NP; r += blockDim.x) {
@@ -268,9 +274,25 @@ __global__ __launch_bounds__(256) void k_ext_solve(ExtDims d, ExtState* __restri
     __syncthreads();
   }
   wg_spd_inverse(sS, LD, NP >> 4, tmp, bad);
+  // dc = S^-1 b, then one step of iterative refinement dc += S^-1 (b - S dc): with the
+  // gauge left free (as in the reference) S is conditioned like 1/lambda at small damping
+  double* sx = tmp;  // NC <= 96 < 512
+  double* sr = tmp + 256;
   for (int r = threadIdx.x; r < NC; r += blockDim.x) {
     double v = 0.0;
     for (int c = 0; c < NC; ++c) v += sS[r * LD + c] * sb[c];
+    sx[r] = v;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < NC; r += blockDim.x) {
+    double v = sb[r];
+    for (int c = 0; c < NC; ++c) v -= Sg[r * NC + c] * sx[c];
+    sr[r] = v;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < NC; r += blockDim.x) {
+    double v = sx[r];
+    for (int c = 0; c < NC; ++c) v += sS[r * LD + c] * sr[c];
     dc[r] = v;
   }
 }
@@ -427,7 +449,7 @@ __global__ __launch_bounds__(256) void k_ext_lm(ExtDims d, ExtState* __restrict_
     st->nacc += 1;
     st->F = f;
     st->cur ^= 1;
-    st->lam = fmax(st->lam * 0.1, 1e-15);
+    st->lam = fmax(st->lam * 0.1, EXT_LAM_MIN);
     st->relin = 1;
     if (fconv)
       st->status = ACS_STATUS_FTOL;
@@ -449,14 +471,15 @@ static size_t ext_schur_lds(const ExtDims& d) {
 template <int G>
 static void ext_enqueue(hipStream_t s, const ExtDims& d, ExtState* st, const ExtOpts& o, double* cams, double* pts,
                         const double2* uv, const uint8_t* mk, const uint8_t* cid, double* Q, double* Vg, double* Fp,
-                        double* part, double* dc, double* normp, double* camnorm, int* bad, int nchunk) {
+                        double* part, double* dc, double* Sg, double* normp, double* camnorm, int* bad,
+                        int nchunk) {
   const int blocks = acs_grid((int64_t)d.n * G, 256);
   const size_t lds = ext_schur_lds(d);
   const int NP = ((6 * d.C + 15) / 16) * 16;
   const size_t lds_solve = sizeof(double) * ((size_t)NP * (NP + 1) + NP + 512 + 256);
   hipLaunchKernelGGL((k_ext_linearize<G>), dim3(blocks), dim3(256), 0, s, d, st, cams, pts, uv, mk, cid, Q, Vg, Fp);
   hipLaunchKernelGGL(k_ext_schur, dim3(nchunk), dim3(256), lds, s, d, st, Q, Vg, mk, cid, part);
-  hipLaunchKernelGGL(k_ext_solve, dim3(1), dim3(256), lds_solve, s, d, st, nchunk, part, Vg, dc, bad);
+  hipLaunchKernelGGL(k_ext_solve, dim3(1), dim3(256), lds_solve, s, d, st, nchunk, part, Vg, dc, Sg, bad);
   hipLaunchKernelGGL(k_ext_back, dim3(acs_grid(d.n, 256)), dim3(256), 0, s, d, st, Q, Vg, mk, cid, dc, pts, normp);
   hipLaunchKernelGGL(k_ext_cam, dim3(1), dim3(64), 0, s, d, st, dc, cams, camnorm);
   hipLaunchKernelGGL((k_ext_cost<G>), dim3(blocks), dim3(256), 0, s, d, st, 1, cams, pts, uv, mk, cid, Fp);
@@ -523,12 +546,12 @@ int acs_sba_extrinsics(acs_ctx* ctx, double* cams, int32_t n_cams, const double*
   };
   const size_t oC = take(2 * (size_t)n_cams * ACS_CAM_STRIDE), oP = take(6 * (size_t)n_pts),
                oQ = take((size_t)n_pts * K * EXT_Q), oV = take((size_t)n_pts * 10), oF = take(n_pts),
-               oPart = take((size_t)nchunk * nE), odc = take(96), onp = take(2 * (size_t)n_pts), ocn = take(64),
+               oPart = take((size_t)nchunk * nE), odc = take(96), oSg = take(96 * 96), onp = take(2 * (size_t)n_pts), ocn = take(64),
                ost = take(16), obad = take(2);
   double* arena = (double*)acs_ws(ctx, WS_FTE6, off * sizeof(double));
   if (!arena) return ACS_E_NOMEM;
   double *dcams = arena + oC, *dpts = arena + oP, *Q = arena + oQ, *Vg = arena + oV, *Fp = arena + oF,
-         *part = arena + oPart, *dc = arena + odc, *normp = arena + onp, *camnorm = arena + ocn;
+         *part = arena + oPart, *dc = arena + odc, *Sg = arena + oSg, *normp = arena + onp, *camnorm = arena + ocn;
   ExtState* st = (ExtState*)(arena + ost);
   int* bad = (int*)(arena + obad);
   ACS_HIP(ctx, hipMemcpyAsync(dcams, dcam0, sizeof(double) * ACS_CAM_STRIDE * n_cams, hipMemcpyDeviceToDevice, s));
@@ -557,7 +580,8 @@ int acs_sba_extrinsics(acs_ctx* ctx, double* cams, int32_t n_cams, const double*
   auto enqueue = [&]() {
     switch (G) {
 #define EXT_IT(g) \
-  case g: ext_enqueue<g>(s, d, st, o, dcams, dpts, uvp, mk, cid, Q, Vg, Fp, part, dc, normp, camnorm, bad, nchunk); break;
+  case g: ext_enqueue<g>(s, d, st, o, dcams, dpts, uvp, mk, cid, Q, Vg, Fp, part, dc, Sg, normp, camnorm, bad, nchunk); \
+    break;
       EXT_IT(2) EXT_IT(4) EXT_IT(8) EXT_IT(16) EXT_IT(32) EXT_IT(64)
 #undef EXT_IT
     }

@@ -16,12 +16,15 @@ Same safeguarded LM as the GPU (acinoset_amd/csrc/sba_ext.hip):
   g = sum w r J, H = sum wh J^T J with w = 1/(1+z), wh = max((1-z) w^2, 0.1 w)
   Marquardt damping on every diagonal; points eliminated by Schur complement:
     S = U + lam D_U - sum_i W_i (V_i + lam D_V)^-1 W_i^T ; b = -g_c + sum_i W_i M_i g_i
-  accept iff F_new < F: lam /= 10 (>= 1e-15); reject: lam *= 10
+  accept iff F_new < F: lam /= 10 (>= LAM_MIN = 1e-7: the gauge is
+  free, so lambda also keeps the reduced system non-singular); reject: lam *= 10
   stop: |g|_inf <= gtol | accept & (dF <= ftol F or |d| <= xtol (xtol + |x|)) | lam > 1e16
 """
 import numpy as np
 
-from .fisheye import project
+from .fisheye import project  # noqa: F401
+
+LAM_MIN = 1e-7
 
 
 def rodrigues(w):
@@ -166,7 +169,7 @@ def sba_extrinsics(points_2d, points_3d, point_idx, cam_idx, K, D, R0, t0, f_sca
             nacc += 1
             fconv = (F - Fn) <= ftol * abs(F)
             X, R, t = Xn, Rn, tn
-            lam = max(lam * 0.1, 1e-15)
+            lam = max(lam * 0.1, LAM_MIN)
             F, U, gc, V, gp, Wm = linearize(X, R, t, K, D, uv, pi, ci, f_scale)[:6]
             if fconv:
                 status = 'ftol'

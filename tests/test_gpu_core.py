@@ -103,7 +103,7 @@ def test_sba_dense_matches_oracle_12cam(ctx):
     assert np.sqrt(np.mean(np.sum((pts - truth) ** 2, 1))) < 0.01  # 1 px noise at ~6 m
     # the list API on the same problem (compacted slots, different lane order)
     pts2, _, _, _ = ctx.sba_points(cams, uv[pi, ci], pi, ci, pts0, residuals=False)
-    assert np.abs(pts - pts2).max() < 1e-9
+    assert np.abs(pts - pts2).max() < 1e-7  # xtol 1e-9 stops differ by summation order
 
 
 def test_sba_deterministic(ctx):
