@@ -86,24 +86,13 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
   const double f2 = prm.f_scale * prm.f_scale;
   const double if2 = 1.0 / f2;
 
-  auto cost_at = [&](double X0, double X1, double X2) -> double {
-    double F = 0.0;
+  // One pass over the observations at X: robust cost, Triggs-weighted GN matrix (packed
+  // upper 3x3) and IRLS gradient, group-reduced. The trial point of every LM iteration is
+  // linearised speculatively, so an accepted step (the common case) costs one projection.
+  auto linearize = [&](double X0, double X1, double X2, double* Ho, double* go, double& Fo) {
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      if (!ok[s]) continue;
-      ProjOut o;
-      fisheye_project<false>(oc[s], X0, X1, X2, o);
-      const double ru = o.u - ou[s], rv = o.v - ov[s];
-      F += log1p(ru * ru * if2) + log1p(rv * rv * if2);
-    }
-    return 0.5 * f2 * group_sum<G>(F);
-  };
-
-  double H[6], g[3], F;
-  auto linearize = [&](double X0, double X1, double X2) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) H[i] = 0.0;
-    g[0] = g[1] = g[2] = 0.0;
+    for (int i = 0; i < 6; ++i) Ho[i] = 0.0;
+    go[0] = go[1] = go[2] = 0.0;
     double Fl = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -119,26 +108,27 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
         Fl += log1p(z);
         const double j0 = o.J[3 * d], j1 = o.J[3 * d + 1], j2 = o.J[3 * d + 2];
         const double hj0 = wh * j0, hj1 = wh * j1, hj2 = wh * j2;
-        H[0] += hj0 * j0;
-        H[1] += hj0 * j1;
-        H[2] += hj0 * j2;
-        H[3] += hj1 * j1;
-        H[4] += hj1 * j2;
-        H[5] += hj2 * j2;
+        Ho[0] += hj0 * j0;
+        Ho[1] += hj0 * j1;
+        Ho[2] += hj0 * j2;
+        Ho[3] += hj1 * j1;
+        Ho[4] += hj1 * j2;
+        Ho[5] += hj2 * j2;
         const double wr = w * r[d];
-        g[0] += wr * j0;
-        g[1] += wr * j1;
-        g[2] += wr * j2;
+        go[0] += wr * j0;
+        go[1] += wr * j1;
+        go[2] += wr * j2;
       }
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) H[i] = group_sum<G>(H[i]);
+    for (int i = 0; i < 6; ++i) Ho[i] = group_sum<G>(Ho[i]);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) g[i] = group_sum<G>(g[i]);
-    F = 0.5 * f2 * group_sum<G>(Fl);
+    for (int i = 0; i < 3; ++i) go[i] = group_sum<G>(go[i]);
+    Fo = 0.5 * f2 * group_sum<G>(Fl);
   };
 
-  linearize(x0, x1, x2);
+  double H[6], g[3], F;
+  linearize(x0, x1, x2, H, g, F);
   const double F_before = F;
   double lam = 1e-3;
   int status = ACS_STATUS_RUNNING, iters = 0, nfev = 1;
@@ -175,7 +165,8 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
       dx0 = (y0 - L10 * dx1 - L20 * dx2) / L00;
     }
     const double n0 = x0 + dx0, n1 = x1 + dx1, n2 = x2 + dx2;
-    const double Fn = cost_at(n0, n1, n2);
+    double Hn[6], gn[3], Fn;
+    linearize(n0, n1, n2, Hn, gn, Fn);
     ++nfev;
     ++iters;
     const double xn = sqrt(x0 * x0 + x1 * x1 + x2 * x2);
@@ -186,7 +177,12 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
       x1 = n1;
       x2 = n2;
       lam = fmax(lam * 0.1, 1e-15);
-      linearize(x0, x1, x2);
+      F = Fn;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) H[i] = Hn[i];
+      g[0] = gn[0];
+      g[1] = gn[1];
+      g[2] = gn[2];
       if (fconv)
         status = ACS_STATUS_FTOL;
       else if (small)

@@ -35,7 +35,11 @@ def parse():
     ap.add_argument('--cams', type=int, default=6)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
-    ap.add_argument('--fte', action='store_true', help='also time the FTE trajectory solve (configs[2])')
+    ap.add_argument('--fte', action='store_true', default=True, help='also time the FTE solve (configs[2])')
+    ap.add_argument('--no-fte', dest='fte', action='store_false')
+    ap.add_argument('--scale-frames', type=int, default=20000,
+                    help='also time SBA at configs[4] scale on one GPU (0 = skip)')
+    ap.add_argument('--scale-cams', type=int, default=12)
     ap.add_argument('--fte-frames', type=int, default=1000)
     return ap.parse_args()
 
@@ -148,6 +152,8 @@ def main():
 
     if args.fte and world == 1:
         out['fte'] = bench_fte(ctx, torch, stream, n_frames=args.fte_frames)
+    if args.scale_frames > 0 and world == 1:
+        out['sba_at_scale'] = bench_sba_scale(ctx, torch, stream, args.scale_frames, args.scale_cams)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(seq, scene, uv, mask, pts0, args.cpu_seconds)
@@ -175,6 +181,55 @@ def cpu_baseline(seq, scene, uv, mask, pts0, seconds):
     return {'value': reps * seq.N / dt, 'unit': 'frames/s', 'cores': 1, 'kind': 'port',
             'sample': f'{reps} full solves of the same {seq.N}-frame x {C}-cam x 20-kp problem '
                       f'(oracle/sba.py, numpy float64), {dt:.1f} s'}
+
+
+def bench_sba_scale(ctx, torch, stream, n_frames=20000, n_cams=12, steps=10):
+    """configs[4] shape on one GPU (report the roofline fraction where the
+    observation tensor is ~100 MB): 12-camera ring, 20,000 frames x 20 keypoints."""
+    from acinoset_amd import _native, synth
+    scene = synth.ring_scene(n_cams)
+    seq = synth.make_sequence(n_frames, scene, mode='default_nolure', seed=4242)
+    uv, mask, pts0, truth, _ = synth.dense_sba_problem(seq)
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    n_pts, C = mask.shape
+    dev = torch.device('cuda', torch.cuda.current_device())
+    d_cams = torch.from_numpy(cams).to(dev)
+    d_uv = torch.from_numpy(uv).to(dev)
+    d_mask = torch.from_numpy(mask).to(dev)
+    d_pts0 = torch.from_numpy(pts0).to(dev)
+    d_pts = d_pts0.clone()
+    opts = _native.Context.sba_opts()
+    for _ in range(2):
+        d_pts.copy_(d_pts0)
+        ctx.sba_points_dense_dev(d_cams.data_ptr(), C, d_uv.data_ptr(), d_mask.data_ptr(), n_pts, d_pts.data_ptr(),
+                                 opts)
+    d_pts.copy_(d_pts0)
+    rep = ctx.sba_points_dense_dev(d_cams.data_ptr(), C, d_uv.data_ptr(), d_mask.data_ptr(), n_pts,
+                                   d_pts.data_ptr(), opts, report=True)
+    pos_rms = float(np.sqrt(np.mean(np.sum((d_pts.cpu().numpy() - truth) ** 2, 1))))
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        d_pts.copy_(d_pts0, non_blocking=True)
+        ev[i][0].record(stream)
+        ctx.sba_points_dense_dev(d_cams.data_ptr(), C, d_uv.data_ptr(), d_mask.data_ptr(), n_pts,
+                                 d_pts.data_ptr(), opts)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    L = 20
+    bytes_launch = n_frames * (C * L * 17 + 6 * L * 8)
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    return {'workload': f'sba_points C={C} frames={n_frames} L={L} (configs[4] shape, 1 GPU)',
+            'frames_per_s': n_frames / dt, 'ms_per_step': dt * 1e3, 'n_points': int(n_pts),
+            'obs': int(mask.sum()),
+            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': achieved / HBM_PEAK_GBS, 'kernel': 'k_sba_lm', 'kernel_ms': kern_ms,
+                         'bytes_per_launch': bytes_launch},
+            'iters_max': rep['iters_max'], 'gn_steps_mean': rep['iters_sum'] / max(1, rep['n_problems']),
+            'status': rep['status_counts'], 'pos_rms_vs_truth_m': pos_rms}
 
 
 def bench_fte(ctx, torch, stream, n_frames=1000, steps=5):

@@ -32,4 +32,17 @@ if [[ $STEPS == *all* || $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
   run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_${TAG}" -o run -- python3 "$REPO/bench.py" --no-cpu-baseline --steps 200 --warmup 20 ${BENCH_ARGS:-}
 fi
+if [[ $STEPS == *list* ]]; then
+  run counters 120 rocprofv3 -L
+fi
+if [[ $STEPS == *pmc* ]]; then
+  # HBM traffic (guide: separate passes; FETCH_SIZE x2 on gfx950) and FP64 VALU counts
+  export TMPDIR=/tmp
+  PMC_ARGS="--no-cpu-baseline --no-fte --steps 3 --warmup 1"
+  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_${TAG}_fetch" -o run -- python3 "$REPO/bench.py" $PMC_ARGS
+  run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_${TAG}_write" -o run -- python3 "$REPO/bench.py" $PMC_ARGS
+  if [[ -n "${PMC_VALU:-}" ]]; then
+    run pmc_valu 600 rocprofv3 --pmc $PMC_VALU --output-format csv -d "$OUT/pmc_${TAG}_valu" -o run -- python3 "$REPO/bench.py" $PMC_ARGS
+  fi
+fi
 echo done
