@@ -34,7 +34,7 @@ SYMBOLS = (
     'acs_abi_version', 'acs_device_count', 'acs_sba_default_opts', 'acs_project_fisheye',
     'acs_sba_residuals', 'acs_sba_points', 'acs_sba_points_dense', 'acs_redescending_loss', 'acs_fk',
     'acs_fte_default_opts', 'acs_fte_solve', 'acs_fte_eval', 'acs_triangulate_pairs', 'acs_triangulate_dense',
-    'acs_sba_ext_default_opts', 'acs_sba_extrinsics',
+    'acs_sba_ext_default_opts', 'acs_sba_extrinsics', 'acs_sba_points_dense_io',
 )
 
 
@@ -115,6 +115,8 @@ def _declare(lib):
                                      C.POINTER(Report), u32]),
         'acs_sba_points_dense': (C.c_int, [_P, _P, i32, _P, _P, i64, _P, C.POINTER(SbaOpts), C.POINTER(Report),
                                            u32]),
+        'acs_sba_points_dense_io': (C.c_int, [_P, _P, i32, _P, _P, i64, _P, _P, C.POINTER(SbaOpts),
+                                              C.POINTER(Report), u32]),
         'acs_redescending_loss': (C.c_int, [_P, _P, i64, dbl, dbl, dbl, _P, _P, u32]),
         'acs_fk': (C.c_int, [_P, _P, i64, _P, i64, _P, _P, _P, _P, i64, i32, i32, _P, _P, u32]),
         'acs_fte_default_opts': (None, [C.POINTER(FteOpts)]),
@@ -275,14 +277,23 @@ class Context:
                                                  C.byref(opts), C.byref(rep), 0), 'acs_sba_points_dense')
         return pts, rep.as_dict()
 
-    def sba_points_dense_dev(self, cams_p, n_cams, uv_p, mask_p, n_pts, pts_p, opts=None, report=False):
-        """Device-pointer variant (inputs resident in HBM; asynchronous unless report)."""
+    def sba_points_dense_dev(self, cams_p, n_cams, uv_p, mask_p, n_pts, pts_p, opts=None, report=False,
+                             pts_in_p=None):
+        """Device-pointer variant (inputs resident in HBM; asynchronous unless report).
+        With `pts_in_p` the initial points are read from there and the solution written
+        to `pts_p` (acs_sba_points_dense_io); otherwise `pts_p` is in/out."""
         opts = opts or self.sba_opts()
         rep = Report() if report else None
-        self.check(self.lib.acs_sba_points_dense(self.h, C.c_void_p(cams_p), n_cams, C.c_void_p(uv_p),
-                                                 C.c_void_p(mask_p), n_pts, C.c_void_p(pts_p), C.byref(opts),
-                                                 C.byref(rep) if rep is not None else None, ACS_DEVICE_PTRS),
-                   'acs_sba_points_dense')
+        rp = C.byref(rep) if rep is not None else None
+        if pts_in_p is None:
+            rc = self.lib.acs_sba_points_dense(self.h, C.c_void_p(cams_p), n_cams, C.c_void_p(uv_p),
+                                               C.c_void_p(mask_p), n_pts, C.c_void_p(pts_p), C.byref(opts), rp,
+                                               ACS_DEVICE_PTRS)
+        else:
+            rc = self.lib.acs_sba_points_dense_io(self.h, C.c_void_p(cams_p), n_cams, C.c_void_p(uv_p),
+                                                  C.c_void_p(mask_p), n_pts, C.c_void_p(pts_in_p),
+                                                  C.c_void_p(pts_p), C.byref(opts), rp, ACS_DEVICE_PTRS)
+        self.check(rc, 'acs_sba_points_dense')
         return rep.as_dict() if rep is not None else None
 
     # ---- a6 -------------------------------------------------------------------------

@@ -85,8 +85,9 @@ __device__ __forceinline__ void fisheye_project(const double* __restrict__ c, do
   const double Y0 = fma(c[8], X0, fma(c[9], X1, fma(c[10], X2, c[17])));
   const double Y1 = fma(c[11], X0, fma(c[12], X1, fma(c[13], X2, c[18])));
   const double Y2 = fma(c[14], X0, fma(c[15], X1, fma(c[16], X2, c[19])));
-  const double a = Y0 / Y2;
-  const double b = Y1 / Y2;
+  const double iz = 1.0 / Y2;
+  const double a = Y0 * iz;
+  const double b = Y1 * iz;
   const double r2 = a * a + b * b;
   const double k1 = c[4], k2 = c[5], k3 = c[6], k4 = c[7];
   double r = FTE_FORM ? sqrt(r2 + 1e-12) : sqrt(r2);
@@ -95,7 +96,8 @@ __device__ __forceinline__ void fisheye_project(const double* __restrict__ c, do
   const double poly = 1.0 + th2 * (k1 + th2 * (k2 + th2 * (k3 + th2 * k4)));
   const double thd = th * poly;
   const bool big = FTE_FORM ? true : (r > 1e-8);
-  const double s = big ? thd / r : 1.0;
+  const double ir = big ? 1.0 / r : 1.0;
+  const double s = big ? thd * ir : 1.0;
   o.u = c[0] * (a * s) + c[2];
   o.v = c[1] * (b * s) + c[3];
   if (JAC) {
@@ -104,15 +106,14 @@ __device__ __forceinline__ void fisheye_project(const double* __restrict__ c, do
     double spr;
     if (FTE_FORM) {
       // r = sqrt(a^2+b^2+eps): dr/da = a/r, same formula with this r
-      spr = (dthd * r / (1.0 + r * r) - thd) / (r * r * r);
+      spr = (dthd * r / (1.0 + r * r) - thd) * (ir * ir * ir);
     } else {
-      spr = (r2 > 1e-16) ? (dthd * r / (1.0 + r2) - thd) / (r * r2) : 0.0;
+      spr = (r2 > 1e-16) ? (dthd * r / (1.0 + r2) - thd) * (ir * ir * ir) : 0.0;
     }
     const double duda = c[0] * (s + a * a * spr);
     const double dudb = c[0] * (a * b * spr);
     const double dvda = c[1] * (a * b * spr);
     const double dvdb = c[1] * (s + b * b * spr);
-    const double iz = 1.0 / Y2;
     // d(u,v)/dY = J_uv_ab * [[iz, 0, -a iz], [0, iz, -b iz]]
     const double u0 = duda * iz, u1 = dudb * iz, u2 = -(duda * a + dudb * b) * iz;
     const double v0 = dvda * iz, v1 = dvdb * iz, v2 = -(dvda * a + dvdb * b) * iz;
@@ -170,11 +171,24 @@ __device__ __forceinline__ LossOut redescending(double err, double a, double b, 
   return o;
 }
 
-// Butterfly sum inside an aligned group of G lanes. IEEE addition is commutative, so
-// every lane of the group ends with bit-identical sums.
+// Sum inside an aligned group of G lanes; every lane ends with the bit-identical total
+// (each step adds a lane's value to its partner's, and IEEE addition is commutative).
+// Within a 16-lane row the partners come from DPP lane permutes (quad xor 1, quad xor 2,
+// half-row mirror, row mirror) on the VALU; wider groups finish with LDS-routed shuffles.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
 template <int G>
 __device__ __forceinline__ double group_sum(double v) {
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, G);
+  if (G >= 2) v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (G >= 4) v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (G >= 8) v += dpp_f64<0x141>(v);  // row_half_mirror: quad 0 <-> quad 1 (quads uniform)
+  if (G >= 16) v += dpp_f64<0x140>(v); // row_mirror: half 0 <-> half 1
+  if (G >= 32) v += __shfl_xor(v, 16, G);
+  if (G >= 64) v += __shfl_xor(v, 32, G);
   return v;
 }

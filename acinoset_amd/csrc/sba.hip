@@ -36,7 +36,8 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
                                                 const double2* __restrict__ uv,
                                                 const uint8_t* __restrict__ mask,
                                                 const uint8_t* __restrict__ camid, int64_t n_pts,
-                                                double* __restrict__ pts, SbaParams prm,
+                                                const double* pts_in, double* pts,  // may alias
+                                                SbaParams prm,
                                                 double* __restrict__ cost0, double* __restrict__ cost1,
                                                 int* __restrict__ stat) {
   extern __shared__ double s_cam[];
@@ -72,9 +73,12 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     }
   }
   const double nobs = group_sum<G>((double)mine);
-  double x0 = pts[3 * p], x1 = pts[3 * p + 1], x2 = pts[3 * p + 2];
+  double x0 = pts_in[3 * p], x1 = pts_in[3 * p + 1], x2 = pts_in[3 * p + 2];
   if (nobs == 0.0) {
     if (lane == 0) {
+      pts[3 * p] = x0;
+      pts[3 * p + 1] = x1;
+      pts[3 * p + 2] = x2;
       cost0[p] = 0.0;
       cost1[p] = 0.0;
       stat[3 * p] = ACS_STATUS_NOOBS;
@@ -100,12 +104,13 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
       ProjOut o;
       fisheye_project<true>(oc[s], X0, X1, X2, o);
       const double r[2] = {o.u - ou[s], o.v - ov[s]};
+      const double zu = r[0] * r[0] * if2, zv = r[1] * r[1] * if2;
+      Fl += log1p(zu + zv + zu * zv);  // log1p(zu) + log1p(zv) with one logarithm
 #pragma unroll
       for (int d = 0; d < 2; ++d) {
-        const double z = r[d] * r[d] * if2;
+        const double z = d ? zv : zu;
         const double w = 1.0 / (1.0 + z);                   // rho'(z): gradient weight
         const double wh = fmax((1.0 - z) * w * w, 0.1 * w);  // rho' + 2 z rho'' (Triggs), floored
-        Fl += log1p(z);
         const double j0 = o.J[3 * d], j1 = o.J[3 * d + 1], j2 = o.J[3 * d + 2];
         const double hj0 = wh * j0, hj1 = wh * j1, hj2 = wh * j2;
         Ho[0] += hj0 * j0;
@@ -146,23 +151,33 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     const double dl = 1.0 + lam;
     const double a00 = H[0] * dl, a11 = H[3] * dl, a22 = H[5] * dl;
     bool pd = a00 > 0.0;
-    const double L00 = pd ? sqrt(a00) : 1.0;
-    const double L10 = H[1] / L00, L20 = H[2] / L00;
+    const double i00 = pd ? 1.0 / sqrt(a00) : 1.0;  // reciprocal Cholesky diagonal
+    const double L10 = H[1] * i00, L20 = H[2] * i00;
     const double d11 = a11 - L10 * L10;
     pd = pd && d11 > 0.0;
-    const double L11 = pd ? sqrt(d11) : 1.0;
-    const double L21 = (H[4] - L20 * L10) / L11;
+    const double i11 = pd ? 1.0 / sqrt(d11) : 1.0;
+    const double L21 = (H[4] - L20 * L10) * i11;
     const double d22 = a22 - L20 * L20 - L21 * L21;
     pd = pd && d22 > 0.0;
-    const double L22 = pd ? sqrt(d22) : 1.0;
+    const double i22 = pd ? 1.0 / sqrt(d22) : 1.0;
     double dx0 = 0.0, dx1 = 0.0, dx2 = 0.0;
     if (pd) {
-      const double y0 = -g[0] / L00;
-      const double y1 = (-g[1] - L10 * y0) / L11;
-      const double y2 = (-g[2] - L20 * y0 - L21 * y1) / L22;
-      dx2 = y2 / L22;
-      dx1 = (y1 - L21 * dx2) / L11;
-      dx0 = (y0 - L10 * dx1 - L20 * dx2) / L00;
+      const double y0 = -g[0] * i00;
+      const double y1 = (-g[1] - L10 * y0) * i11;
+      const double y2 = (-g[2] - L20 * y0 - L21 * y1) * i22;
+      dx2 = y2 * i22;
+      dx1 = (y1 - L21 * dx2) * i11;
+      dx0 = (y0 - L10 * dx1 - L20 * dx2) * i00;
+      // model decrease of the step, -g.dx - dx.H.dx/2: below the resolution of the
+      // float64 cost the step can only be accepted or rejected by rounding -> converged
+      const double Hd0 = H[0] * dx0 + H[1] * dx1 + H[2] * dx2;
+      const double Hd1 = H[1] * dx0 + H[3] * dx1 + H[4] * dx2;
+      const double Hd2 = H[2] * dx0 + H[4] * dx1 + H[5] * dx2;
+      const double pred = -(g[0] * dx0 + g[1] * dx1 + g[2] * dx2) - 0.5 * (dx0 * Hd0 + dx1 * Hd1 + dx2 * Hd2);
+      if (pred <= ACS_COST_RES * F) {
+        status = ACS_STATUS_FTOL;
+        break;
+      }
     }
     const double n0 = x0 + dx0, n1 = x1 + dx1, n2 = x2 + dx2;
     double Hn[6], gn[3], Fn;
@@ -322,20 +337,20 @@ static int next_pow2(int v) {
 
 template <int G, int S, bool CAMID>
 static void launch_lm_t(acs_ctx* ctx, int blocks, int block, const double* cams, int C, int K, const double2* uv,
-                        const uint8_t* mask, const uint8_t* camid, int64_t n_pts, double* pts, SbaParams prm,
-                        double* c0, double* c1, int* st) {
+                        const uint8_t* mask, const uint8_t* camid, int64_t n_pts, const double* pts_in, double* pts,
+                        SbaParams prm, double* c0, double* c1, int* st) {
   hipLaunchKernelGGL((k_sba_lm<G, S, CAMID>), dim3(blocks), dim3(block), sizeof(double) * ACS_CAM_STRIDE * C,
-                     ctx->stream, cams, C, K, uv, mask, camid, n_pts, pts, prm, c0, c1, st);
+                     ctx->stream, cams, C, K, uv, mask, camid, n_pts, pts_in, pts, prm, c0, c1, st);
 }
 
 template <int S, bool CAMID>
 static int launch_lm_g(acs_ctx* ctx, int G, int blocks, int block, const double* cams, int C, int K,
-                       const double2* uv, const uint8_t* mask, const uint8_t* camid, int64_t n_pts, double* pts,
-                       SbaParams prm, double* c0, double* c1, int* st) {
+                       const double2* uv, const uint8_t* mask, const uint8_t* camid, int64_t n_pts,
+                       const double* pts_in, double* pts, SbaParams prm, double* c0, double* c1, int* st) {
   switch (G) {
 #define ACS_G(g)                                                                                      \
   case g:                                                                                             \
-    launch_lm_t<g, S, CAMID>(ctx, blocks, block, cams, C, K, uv, mask, camid, n_pts, pts, prm, c0, c1, st); \
+    launch_lm_t<g, S, CAMID>(ctx, blocks, block, cams, C, K, uv, mask, camid, n_pts, pts_in, pts, prm, c0, c1, st); \
     break;
     ACS_G(2) ACS_G(4) ACS_G(8) ACS_G(16) ACS_G(32) ACS_G(64)
 #undef ACS_G
@@ -345,9 +360,11 @@ static int launch_lm_g(acs_ctx* ctx, int G, int blocks, int block, const double*
   return ACS_OK;
 }
 
-// Launch the LM kernel over an (n_pts, K) slot tensor already on the device.
+// Launch the LM kernel over an (n_pts, K) slot tensor already on the device; initial points
+// from dpts_in, solution to dpts (may alias).
 static int run_lm(acs_ctx* ctx, const double* dcams, int C, int K, const double2* duv, const uint8_t* dmask,
-                  const uint8_t* dcamid, int64_t n_pts, double* dpts, const acs_sba_opts* opts, double** c0_out,
+                  const uint8_t* dcamid, int64_t n_pts, const double* dpts_in, double* dpts,
+                  const acs_sba_opts* opts, double** c0_out,
                   double** c1_out, int** st_out) {
   acs_sba_opts o;
   acs_sba_default_opts(&o);
@@ -372,14 +389,14 @@ static int run_lm(acs_ctx* ctx, const double* dcams, int C, int K, const double2
   const int blocks = acs_grid(threads, block);
   int rc;
   if (dcamid) {
-    rc = (S == 1) ? launch_lm_g<1, true>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts, prm,
+    rc = (S == 1) ? launch_lm_g<1, true>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in, dpts, prm,
                                          c0, c1, st)
-                  : launch_lm_g<4, true>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts, prm,
+                  : launch_lm_g<4, true>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in, dpts, prm,
                                          c0, c1, st);
   } else {
-    rc = (S == 1) ? launch_lm_g<1, false>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts,
+    rc = (S == 1) ? launch_lm_g<1, false>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in, dpts,
                                           prm, c0, c1, st)
-                  : launch_lm_g<4, false>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts,
+                  : launch_lm_g<4, false>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in, dpts,
                                           prm, c0, c1, st);
   }
   if (rc) return rc;
@@ -451,32 +468,40 @@ int acs_obs_to_slots(acs_ctx* ctx, const double* duv, const int32_t* dpi, const 
 
 extern "C" {
 
-int acs_sba_points_dense(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv, const uint8_t* mask,
-                         int64_t n_pts, double* pts, const acs_sba_opts* opts, acs_report* report, uint32_t flags) {
+int acs_sba_points_dense_io(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
+                            const uint8_t* mask, int64_t n_pts, const double* pts_in, double* pts_out,
+                            const acs_sba_opts* opts, acs_report* report, uint32_t flags) {
   ACS_CHECK(ctx, n_pts >= 0 && n_cams >= 1 && n_cams <= 64, "acs_sba_points_dense: n_pts=%lld n_cams=%d (1..64)",
             (long long)n_pts, n_cams);
   if (n_pts == 0) {
     if (report) std::memset(report, 0, sizeof(*report));
     return ACS_OK;
   }
-  void *dc, *duv, *dm, *dp;
+  void *dc, *duv, *dm, *dpi;
   int rc;
   if ((rc = acs_stage_in(ctx, WS_CAMS, cams, sizeof(double) * ACS_CAM_STRIDE * n_cams, flags, &dc))) return rc;
   if ((rc = acs_stage_in(ctx, WS_UV, uv, sizeof(double) * 2 * n_pts * n_cams, flags, &duv))) return rc;
   if ((rc = acs_stage_in(ctx, WS_MASK, mask, (size_t)n_pts * n_cams, flags, &dm))) return rc;
-  if ((rc = acs_stage_in(ctx, WS_PTS, pts, sizeof(double) * 3 * n_pts, flags, &dp))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_PTS, pts_in, sizeof(double) * 3 * n_pts, flags, &dpi))) return rc;
+  double* dpo = (double*)acs_out_buf(ctx, WS_OUT0, pts_out, sizeof(double) * 3 * n_pts, flags);
+  if (!dpo) return ACS_E_NOMEM;
   double *c0, *c1;
   int* st;
   if ((rc = run_lm(ctx, (const double*)dc, n_cams, n_cams, (const double2*)duv, (const uint8_t*)dm, nullptr, n_pts,
-                   (double*)dp, opts, &c0, &c1, &st)))
+                   (const double*)dpi, dpo, opts, &c0, &c1, &st)))
     return rc;
-  if ((rc = acs_stage_out(ctx, pts, dp, sizeof(double) * 3 * n_pts, flags))) return rc;
+  if ((rc = acs_stage_out(ctx, pts_out, dpo, sizeof(double) * 3 * n_pts, flags))) return rc;
   if (report) {
     if ((rc = run_report(ctx, c0, c1, st, n_pts, report))) return rc;
   } else if (!(flags & ACS_DEVICE_PTRS)) {
     ACS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
   return ACS_OK;
+}
+
+int acs_sba_points_dense(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv, const uint8_t* mask,
+                         int64_t n_pts, double* pts, const acs_sba_opts* opts, acs_report* report, uint32_t flags) {
+  return acs_sba_points_dense_io(ctx, cams, n_cams, uv, mask, n_pts, pts, pts, opts, report, flags);
 }
 
 int acs_sba_points(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv, const int32_t* pt_idx,
@@ -517,7 +542,8 @@ int acs_sba_points(acs_ctx* ctx, const double* cams, int32_t n_cams, const doubl
 
   double *c0, *c1;
   int* st;
-  if ((rc = run_lm(ctx, (const double*)dc, n_cams, K, uvp, mk, cid, n_pts, (double*)dp, opts, &c0, &c1, &st)))
+  if ((rc = run_lm(ctx, (const double*)dc, n_cams, K, uvp, mk, cid, n_pts, (const double*)dp, (double*)dp, opts, &c0,
+                   &c1, &st)))
     return rc;
 
   double* dra = nullptr;

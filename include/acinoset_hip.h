@@ -54,6 +54,11 @@ extern "C" {
 #define ACS_STATUS_NOOBS 6
 #define ACS_N_STATUS 7
 
+/* LM steps whose model decrease -g.dx - dx.H.dx/2 is <= ACS_COST_RES * cost are below the
+ * resolution of a float64 cost sum: the problem stops as converged (ACS_STATUS_FTOL)
+ * instead of letting rounding accept or reject the step (points-only SBA).              */
+#define ACS_COST_RES 1e-14
+
 typedef struct acs_ctx acs_ctx;
 
 typedef struct {
@@ -115,6 +120,11 @@ int acs_sba_points(acs_ctx* ctx, const double* cams, int32_t n_cams, const doubl
 int acs_sba_points_dense(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
                          const uint8_t* mask, int64_t n_pts, double* pts,
                          const acs_sba_opts* opts, acs_report* report, uint32_t flags);
+/* Same solve with separate initial (pts_in) and solution (pts_out) buffers, so a repeated
+ * solve from one initialisation needs no reset copy (pts_in == pts_out is allowed).    */
+int acs_sba_points_dense_io(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
+                            const uint8_t* mask, int64_t n_pts, const double* pts_in, double* pts_out,
+                            const acs_sba_opts* opts, acs_report* report, uint32_t flags);
 
 /* ---- a9: redescending loss (src/lib/misc.py:329-343), elementwise ------------------ */
 int acs_redescending_loss(acs_ctx* ctx, const double* err, int64_t n, double a, double b, double c,

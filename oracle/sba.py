@@ -19,7 +19,9 @@ Marquardt damping H + lam*diag(H); accept only on strict cost decrease. Spec sha
 `acinoset_amd/csrc/sba.hip`:
 
     lam0 = 1e-3; accept: lam = max(lam/10, 1e-15); reject: lam *= 10; xtol default 1e-9
-    stop: |g|_inf <= gtol | accepted and (dF <= ftol*F or |dx| <= xtol*(xtol+|x|))
+    stop: |g|_inf <= gtol | model decrease -g.dx - dx.H.dx/2 <= 1e-14 F (ftol: below the
+          float64 cost resolution, checked before the trial) |
+          accepted and (dF <= ftol*F or |dx| <= xtol*(xtol+|x|))
           | rejected and |dx| <= xtol*(xtol+|x|) | lam > 1e16 | iters >= max_iters
 """
 import numpy as np
@@ -28,6 +30,7 @@ from .fisheye import project, project_jac
 
 # status codes (same values as include/acinoset_hip.h ACS_STATUS_*)
 RUNNING, GTOL, FTOL, XTOL, STALLED, MAXITER, NOOBS = 0, 1, 2, 3, 4, 5, 6
+COST_RES = 1e-14  # include/acinoset_hip.h ACS_COST_RES
 
 
 def cost_func_points_only(params, n_points, point_3d_indices, camera_indices, k_arr, d_arr, r_arr, t_arr,
@@ -124,6 +127,13 @@ def sba_points(points_2d, points_3d, point_idx, cam_idx, K, D, R, t, f_scale=50.
         y = np.linalg.solve(np.where(ok[:, None, None], L, np.eye(3)), -g[ia][..., None])
         step = np.linalg.solve(np.swapaxes(np.where(ok[:, None, None], L, np.eye(3)), 1, 2), y)[..., 0]
         dx[ia] = np.where(ok[:, None], step, 0.0)
+        # model decrease below the float64 cost resolution -> converged (ACS_COST_RES)
+        pred = -np.einsum('ni,ni->n', g, dx) - 0.5 * np.einsum('ni,nij,nj->n', dx, H, dx)
+        res = np.zeros(n_pts, bool)
+        res[ia] = ok & (pred[ia] <= COST_RES * F[ia])
+        status[res] = FTOL
+        act &= ~res
+        dx[res] = 0.0
         xn = x + dx
         Fn = np.where(act, cost(np.where(act[:, None], xn, x)), F)
         nfev += act

@@ -133,3 +133,26 @@ def test_sba_edge_cases(ctx):
     # out-of-range point index -> error, not a crash
     with pytest.raises(RuntimeError):
         ctx.sba_points(cams, g['points_2d'], g['point_indices'] + 10 ** 6, g['camera_indices'], g['points_3d'])
+
+
+def test_sba_dense_io_matches_inplace(ctx):
+    """acs_sba_points_dense_io: separate initial/solution buffers give the in-place result
+    bit for bit and leave the initial points untouched (incl. a point with no views)."""
+    import torch
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(50, scene, seed=11)
+    uv, mask, pts0, _, _ = synth.dense_sba_problem(seq)
+    mask = mask.copy()
+    mask[3] = 0  # no observations: passes through
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    ref, _ = ctx.sba_points_dense(cams, uv, mask, pts0)
+    dev = torch.device('cuda', 0)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
+         dict(cams=cams, uv=uv, mask=mask, pts0=pts0).items()}
+    out = torch.full_like(d['pts0'], float('nan'))
+    ctx.sba_points_dense_dev(d['cams'].data_ptr(), len(cams), d['uv'].data_ptr(), d['mask'].data_ptr(), len(pts0),
+                             out.data_ptr(), pts_in_p=d['pts0'].data_ptr())
+    ctx.sync()
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(d['pts0'].cpu().numpy(), pts0)
+    np.testing.assert_array_equal(ref[3], pts0[3])
