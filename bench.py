@@ -121,6 +121,7 @@ def main():
     bytes_launch = args.frames * b_frame
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     iters_mean = rep['iters_sum'] / max(1, rep['n_problems'])
+    traffic, pmc = pmc_per_launch('k_sba_lm', n_pts * _group(C))
 
     out = {
         'metric': 'frames/sec to SBA convergence, 6-cam x 20-kp (points-only SBA, configs[1])',
@@ -139,8 +140,9 @@ def main():
                    'n_points_per_rank': int(n_pts), 'obs_slots_per_rank': int(n_pts * C),
                    'parallelism': f'frame-shard x{world}'},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                     'kernel': 'k_sba_lm', 'kernel_ms': kern_ms, 'bytes_per_launch': bytes_launch},
+                     'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                     'kernel': 'k_sba_lm', 'kernel_ms': kern_ms, 'bytes_per_launch': bytes_launch,
+                     'traffic_source': pmc['source'] if pmc else None},
         'convergence': {'status': rep['status_counts'], 'iters_max': rep['iters_max'],
                         'gn_steps_mean': iters_mean, 'cost_before': rep['cost_before'],
                         'cost_after': rep['cost_after'], 'pos_rms_vs_truth_m': pos_rms},
@@ -157,6 +159,34 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+FP64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak (spec sheet)
+
+
+def pmc_per_launch(kernel, grid):
+    """HBM bytes / FP64 flops per launch of `kernel` at `grid` threads from the newest
+    committed PMC summary (profiles/r*/traffic.json, tools/pmc_summary.py: separate
+    FETCH_SIZE (x2, gfx950) and WRITE_SIZE passes of this bench). None if not profiled."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r*',
+                                          'traffic.json')))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    r = d['per_launch'].get(f'{kernel}@{grid}')
+    if r is None:
+        return None, None
+    return r.get('hbm_bytes'), dict(fp64_flops=r.get('fp64_flops'), source=os.path.relpath(files[-1],
+                                                                                           os.path.dirname(files[0])))
+
+
+def _group(C):
+    g = 2
+    while g < C:
+        g *= 2
+    return g
 
 
 def cpu_baseline(seq, scene, uv, mask, pts0, seconds):
@@ -216,12 +246,19 @@ def bench_sba_scale(ctx, torch, stream, n_frames=20000, n_cams=12, steps=10):
     L = 20
     bytes_launch = n_frames * (C * L * 17 + 6 * L * 8)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    traffic, pmc = pmc_per_launch('k_sba_lm', n_pts * _group(C))
+    fp64 = None
+    if pmc and pmc.get('fp64_flops'):
+        tfs = pmc['fp64_flops'] / (kern_ms * 1e-3) / 1e12
+        fp64 = {'bound': 'fp64-valu', 'achieved': tfs, 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
+                'frac': tfs / FP64_VALU_PEAK_TFS, 'flops_per_launch': pmc['fp64_flops'], 'source': pmc['source']}
     return {'workload': f'sba_points C={C} frames={n_frames} L={L} (configs[4] shape, 1 GPU)',
             'frames_per_s': n_frames / dt, 'ms_per_step': dt * 1e3, 'n_points': int(n_pts),
             'obs': int(mask.sum()),
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'kernel': 'k_sba_lm', 'kernel_ms': kern_ms,
-                         'bytes_per_launch': bytes_launch},
+                         'bytes_per_launch': bytes_launch, 'traffic': traffic},
+            'roofline_fp64': fp64,
             'iters_max': rep['iters_max'], 'gn_steps_mean': rep['iters_sum'] / max(1, rep['n_problems']),
             'status': rep['status_counts'], 'pos_rms_vs_truth_m': pos_rms}
 

@@ -39,10 +39,12 @@ if [[ $STEPS == *pmc* ]]; then
   # HBM traffic (guide: separate passes; FETCH_SIZE x2 on gfx950) and FP64 VALU counts
   export TMPDIR=/tmp
   PMC_ARGS="--no-cpu-baseline --no-fte --steps 3 --warmup 1"
+  PMC_VALU=${PMC_VALU:-"SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAVES SQ_INSTS_SALU SQ_WAVE_CYCLES"}
   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_${TAG}_fetch" -o run -- python3 "$REPO/bench.py" $PMC_ARGS
   run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_${TAG}_write" -o run -- python3 "$REPO/bench.py" $PMC_ARGS
   if [[ -n "${PMC_VALU:-}" ]]; then
     run pmc_valu 600 rocprofv3 --pmc $PMC_VALU --output-format csv -d "$OUT/pmc_${TAG}_valu" -o run -- python3 "$REPO/bench.py" $PMC_ARGS
   fi
+  python tools/pmc_summary.py "$OUT/pmc_${TAG}" "$OUT/traffic_${TAG}.json" > "$OUT/pmc_summary_${TAG}.log" 2>&1 || true
 fi
 echo done

@@ -1,0 +1,56 @@
+"""Summarise rocprofv3 --pmc passes (tools/gpu_session.sh STEPS=pmc) into
+profiles/<round>/traffic.json: per (kernel, grid size) HBM bytes per launch and FP64 VALU
+flops per launch.
+
+HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
+WRITE_SIZE come from separate passes, are reported in KiB, and on gfx950 FETCH_SIZE counts
+half of the bytes of wide coalesced reads (x2 correction; WRITE_SIZE is exact).
+FP64 flops = 64 lanes x (2 FMA + ADD + MUL + TRANS) wave instructions (SQ_INSTS_VALU_*_F64;
+an upper bound when lanes are masked off).
+
+    python tools/pmc_summary.py gpurun_out/pmc_<tag> profiles/r01/traffic.json
+"""
+import json
+import sys
+
+import pandas as pd
+
+
+def load(prefix, kind):
+    d = pd.read_csv(f'{prefix}_{kind}/run_counter_collection.csv')
+    d['kernel'] = d.Kernel_Name.str.extract(r'(k_[a-z0-9_]+)')[0]
+    return d.dropna(subset=['kernel'])
+
+
+def main(prefix, out):
+    rows = {}
+    for kind in ('fetch', 'write', 'valu'):
+        try:
+            d = load(prefix, kind)
+        except FileNotFoundError:
+            continue
+        g = d.groupby(['kernel', 'Grid_Size', 'Counter_Name']).Counter_Value.mean()
+        for (k, grid, c), v in g.items():
+            rows.setdefault(f'{k}@{grid}', {})[c] = float(v)
+    res = {}
+    for key, c in rows.items():
+        r = {}
+        if 'FETCH_SIZE' in c:
+            r['fetch_bytes'] = 2 * 1024 * c['FETCH_SIZE']
+        if 'WRITE_SIZE' in c:
+            r['write_bytes'] = 1024 * c['WRITE_SIZE']
+        if 'fetch_bytes' in r and 'write_bytes' in r:
+            r['hbm_bytes'] = r['fetch_bytes'] + r['write_bytes']
+        if 'SQ_INSTS_VALU_FMA_F64' in c:
+            r['fp64_flops'] = 64 * (2 * c['SQ_INSTS_VALU_FMA_F64'] + c.get('SQ_INSTS_VALU_ADD_F64', 0)
+                                    + c.get('SQ_INSTS_VALU_MUL_F64', 0) + c.get('SQ_INSTS_VALU_TRANS_F64', 0))
+            r['valu_insts'] = c.get('SQ_INSTS_VALU')
+        r['counters'] = c
+        res[key] = r
+    with open(out, 'w') as f:
+        json.dump({'source': prefix, 'per_launch': res}, f, indent=1, sort_keys=True)
+    print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != 'counters'} for k, v in res.items()}, indent=1))
+
+
+if __name__ == '__main__':
+    main(sys.argv[1], sys.argv[2])
