@@ -35,6 +35,8 @@ SYMBOLS = (
     'acs_sba_residuals', 'acs_sba_points', 'acs_sba_points_dense', 'acs_redescending_loss', 'acs_fk',
     'acs_fte_default_opts', 'acs_fte_solve', 'acs_fte_eval', 'acs_triangulate_pairs', 'acs_triangulate_dense',
     'acs_sba_ext_default_opts', 'acs_sba_extrinsics', 'acs_sba_points_dense_io',
+    'acs_fte_dist_create', 'acs_fte_dist_init', 'acs_fte_dist_phase1', 'acs_fte_dist_phase2', 'acs_fte_dist_phase3',
+    'acs_fte_dist_phase4', 'acs_fte_dist_result', 'acs_fte_dist_destroy',
 )
 
 
@@ -127,6 +129,15 @@ def _declare(lib):
         'acs_triangulate_pairs': (C.c_int, [_P, _P, i32, _P, _P, _P, _P, i64, _P, u32]),
         'acs_triangulate_dense': (C.c_int, [_P, _P, i32, _P, _P, i64, _P, _P, u32]),
         'acs_sba_ext_default_opts': (None, [C.POINTER(SbaExtOpts)]),
+        'acs_fte_dist_create': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, dbl, _P, i32, i32, _P, _P,
+                                          C.POINTER(FteOpts), i32, i32, C.POINTER(_P), C.POINTER(i64), u32]),
+        'acs_fte_dist_init': (C.c_int, [_P, _P]),
+        'acs_fte_dist_phase1': (C.c_int, [_P, _P]),
+        'acs_fte_dist_phase2': (C.c_int, [_P, _P, _P]),
+        'acs_fte_dist_phase3': (C.c_int, [_P, _P, _P]),
+        'acs_fte_dist_phase4': (C.c_int, [_P, _P, i32, C.POINTER(i32)]),
+        'acs_fte_dist_result': (C.c_int, [_P, _P, _P, C.POINTER(FteReport), u32]),
+        'acs_fte_dist_destroy': (C.c_int, [_P]),
         'acs_sba_extrinsics': (C.c_int, [_P, _P, i32, _P, _P, _P, i64, _P, i64, C.POINTER(SbaExtOpts), _P, _P,
                                          C.POINTER(SbaExtReport), u32]),
     }

@@ -23,6 +23,8 @@
 //   k_cr_trial       [n blocks]  trial state X + delta, tau clipped to [-Ts, Ts]
 //   k_fte_cost       [N blocks]  exact objective at the trial state (per-frame partials)
 //   k_fte_lm         [1 block ]  fixed-order reduction, accept/reject, lambda, stop tests
+#include <climits>
+
 #include "fk.hpp"
 #include "mfma64.hpp"
 
@@ -109,11 +111,11 @@ __global__ __launch_bounds__(256) void k_fte_linearize(FteDims d, const int* __r
                                                        const double* __restrict__ wts,
                                                        const double* __restrict__ Xbuf,
                                                        const double* __restrict__ taubuf,
-                                                       const FteState* __restrict__ st, int force,
+                                                       const FteState* __restrict__ st, int force, int k0,
                                                        double* __restrict__ Hloc, double* __restrict__ gloc,
                                                        double* __restrict__ Floc) {
   if (!force && (st->status != 0 || !st->relin)) return;
-  const int k = blockIdx.x;
+  const int k = blockIdx.x + k0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int P = d.P, C = d.C, L = d.L;
   const int cur = force ? 0 : st->cur;
@@ -247,13 +249,16 @@ __global__ __launch_bounds__(256) void k_fte_linearize(FteDims d, const int* __r
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* __restrict__ Xbuf,
                                                       const double* __restrict__ qinv,
-                                                      const FteState* __restrict__ st, int force,
-                                                      const double* __restrict__ Hloc,
+                                                      const FteState* __restrict__ st, int force, int f0, int lo,
+                                                      int hi, const double* __restrict__ Hloc,
                                                       const double* __restrict__ gloc, double* __restrict__ Ab,
                                                       double* __restrict__ gb, double* __restrict__ Bt,
                                                       double* __restrict__ gmaxp) {
+  // Terms are owned by the lowest X row they touch: frame k (rows k..k+2) iff lo <= k < hi,
+  // model stencil m (rows m-3..m) iff lo <= m-3 < hi. The single-GPU solve owns all terms;
+  // a frame-window rank owns the terms starting in its window (dist path below).
   if (!force && (st->status != 0 || !st->relin)) return;
-  const int f = blockIdx.x;
+  const int f = blockIdx.x + f0;
   const int tid = threadIdx.x, nth = blockDim.x;
   const int P = d.P, Cg = d.Cg, N = d.N;
   const int cur = force ? 0 : st->cur;
@@ -267,7 +272,8 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
   for (int i = tid; i < P; i += nth) g[i] = 0.0;
   __syncthreads();
   const int kown = f - 2, kprev = f - 1, kprev2 = f;
-  if (kown >= 0 && kown < N) {
+  auto owned = [&](int k) { return k >= 0 && k < N && k >= lo && k < hi; };
+  if (owned(kown)) {
     const double* H = Hloc + (size_t)kown * FTE_NZP * FTE_NZP;
     for (int i = tid; i < P * P; i += nth) {
       const int r = i / P, c = i % P;
@@ -285,7 +291,7 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
     for (int i = tid; i < P; i += nth) g[i] += gloc[(size_t)kown * FTE_NZP + i];
   }
   __syncthreads();
-  if (kprev >= 0 && kprev < N) {
+  if (owned(kprev)) {
     const double* H = Hloc + (size_t)kprev * FTE_NZP * FTE_NZP;
     for (int i = tid; i < 9; i += nth) {
       const int r = i / 3, c = i % 3;
@@ -299,7 +305,7 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
     for (int i = tid; i < 3; i += nth) g[i] += gloc[(size_t)kprev * FTE_NZP + P + i];
   }
   __syncthreads();
-  if (kprev2 >= 0 && kprev2 < N) {
+  if (owned(kprev2)) {
     const double* H = Hloc + (size_t)kprev2 * FTE_NZP * FTE_NZP;
     for (int i = tid; i < 9; i += nth) {
       const int r = i / 3, c = i % 3;
@@ -320,7 +326,7 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
     double hd[4] = {0.0, 0.0, 0.0, 0.0};
     for (int i = 0; i < 4; ++i) {
       const int m = f + i;
-      if (m < 3 || m > d.M - 1) continue;
+      if (m < 3 || m > d.M - 1 || m - 3 < lo || m - 3 >= hi) continue;
       const double sm = (X[m * P + p] - 3.0 * X[(m - 1) * P + p] + 3.0 * X[(m - 2) * P + p] - X[(m - 3) * P + p]) * its2;
       gm += 2.0 * qinv[p] * cf[i] * its2 * sm;
       for (int dd = 0; dd < 4 && i + dd < 4; ++dd) hd[dd] += 2.0 * qinv[p] * cf[i] * cf[i + dd] * its2 * its2;
@@ -358,9 +364,11 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
 __global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __restrict__ st,
                                                   const double* __restrict__ Ab, const double* __restrict__ gb,
                                                   const double* __restrict__ Bt, double* __restrict__ Dc,
-                                                  double* __restrict__ Ec, double* __restrict__ GBc) {
+                                                  double* __restrict__ Ec, double* __restrict__ GBc, int b0,
+                                                  int end_l, int end_r) {
   if (st->status != 0) return;
-  const int i = blockIdx.x;
+  const int i = blockIdx.x + b0;
+  const bool damp = i != end_l && i != end_r;  // chain ends are damped in the reduced system
   const int tid = threadIdx.x, nth = blockDim.x;
   const int P = d.P, PP = P * P, BP = d.BP, GR = d.GR, Cg = d.Cg;
   const double lam = st->lam;
@@ -376,7 +384,7 @@ __global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __r
     if (rin && cin) {
       v = (ar >= ac) ? Ab[(size_t)fr * 4 * PP + (ar - ac) * PP + pr * P + pc]
                      : Ab[(size_t)fc * 4 * PP + (ac - ar) * PP + pc * P + pr];
-      if (r == c) v += lam * fmax(v, 1e-12);
+      if (r == c && damp) v += lam * fmax(v, 1e-12);
     } else if (r == c) {
       v = 1.0;  // padding: identity
     }
@@ -404,13 +412,16 @@ __global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __r
 }
 
 // LDS budget (BP <= 96): sD + one staged panel, both (BP x BP+1) doubles
-__global__ __launch_bounds__(1024) void k_cr_elim(FteDims d, int s, const FteState* __restrict__ st,
+__global__ __launch_bounds__(1024) void k_cr_elim(FteDims d, int s, int a0, int bend,
+                                                  const FteState* __restrict__ st,
                                                   const double* __restrict__ Dc, const double* __restrict__ Ec,
                                                   const double* __restrict__ GBc, double* __restrict__ Wc,
                                                   double* __restrict__ Tau, int* __restrict__ bad) {
+  // chain [a0, bend]: a0 is a multiple of 2s, so i is an odd multiple of s as in a
+  // whole-sequence reduction; the chain end bend survives every level of the chain
   if (st->status != 0) return;
-  const int i = s * (2 * blockIdx.x + 1);
-  const int r = (i + s < d.nblk) ? i + s : -1;
+  const int i = a0 + s * (2 * blockIdx.x + 1);
+  const int r = (i + s <= bend && i + s < d.nblk) ? i + s : -1;
   const int BP = d.BP, GR = d.GR, WL = 2 * BP + GR, LD = BP + 1;
   extern __shared__ double lds[];
   double* sD = lds;                 // BP x LD
@@ -452,13 +463,14 @@ __global__ __launch_bounds__(1024) void k_cr_elim(FteDims d, int s, const FteSta
   });
 }
 
-__global__ __launch_bounds__(1024) void k_cr_update(FteDims d, int s, const FteState* __restrict__ st,
+__global__ __launch_bounds__(1024) void k_cr_update(FteDims d, int s, int a0, int bend,
+                                                    const FteState* __restrict__ st,
                                                     double* __restrict__ Dc, double* __restrict__ Ec,
                                                     double* __restrict__ GBc, const double* __restrict__ Wc) {
   if (st->status != 0) return;
-  const int j = 2 * s * blockIdx.x;
-  const int a = j - s >= 0 ? j - s : -1;
-  const int c = j + s < d.nblk ? j + s : -1;
+  const int j = a0 + 2 * s * blockIdx.x;
+  const int a = j - s >= a0 ? j - s : -1;
+  const int c = (j + s <= bend && j + s < d.nblk) ? j + s : -1;
   const int BP = d.BP, GR = d.GR, WL = 2 * BP + GR, LD = BP + 1;
   extern __shared__ double lds[];
   double* sA = lds;             // BP x LD
@@ -523,14 +535,18 @@ __global__ __launch_bounds__(1024) void k_cr_update(FteDims d, int s, const FteS
 __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteState* __restrict__ st,
                                                         const double* __restrict__ Hloc,
                                                         const double* __restrict__ gloc,
-                                                        const double* __restrict__ Tau, double* __restrict__ part) {
+                                                        const double* __restrict__ Tau, double* __restrict__ part,
+                                                        int k_lo, int k_hi, int b_lo, int b_hi) {
+  // frames [k_lo, k_hi) (tau blocks of their normal matrices / gradients) and eliminated
+  // super-blocks [b_lo, b_hi) (tau Schur terms), each range cut into CR_NCHUNK chunks
   if (st->status != 0) return;
   const int ch = blockIdx.x;
   const int P = d.P, Cg = d.Cg, GR = d.GR;
   const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
-  const int fc = (d.N + CR_NCHUNK - 1) / CR_NCHUNK, bc = (d.nblk + CR_NCHUNK - 1) / CR_NCHUNK;
-  const int k0 = ch * fc, k1 = min(d.N, k0 + fc);
-  const int b0 = max(1, ch * bc), b1 = min(d.nblk, ch * bc + bc);
+  const int nf = max(0, k_hi - k_lo), nb = max(0, b_hi - b_lo);
+  const int fc = (nf + CR_NCHUNK - 1) / CR_NCHUNK, bc = (nb + CR_NCHUNK - 1) / CR_NCHUNK;
+  const int k0 = k_lo + ch * fc, k1 = min(k_hi, k0 + fc);
+  const int b0 = b_lo + ch * bc, b1 = min(b_hi, b0 + bc);
   for (int e = threadIdx.x; e < nE; e += blockDim.x) {
     double v = 0.0;
     if (e < nH) {
@@ -624,12 +640,13 @@ __global__ __launch_bounds__(256) void k_cr_top(FteDims d, FteState* __restrict_
   }
 }
 
-__global__ __launch_bounds__(256) void k_cr_back(FteDims d, int s, const FteState* __restrict__ st,
+__global__ __launch_bounds__(256) void k_cr_back(FteDims d, int s, int a0, int bend,
+                                                 const FteState* __restrict__ st,
                                                  const double* __restrict__ Wc, const double* __restrict__ dtau,
                                                  double* __restrict__ dcv) {
   if (st->status != 0) return;
-  const int i = s * (2 * blockIdx.x + 1);
-  const int l = i - s, r = (i + s < d.nblk) ? i + s : -1;
+  const int i = a0 + s * (2 * blockIdx.x + 1);
+  const int l = i - s, r = (i + s <= bend && i + s < d.nblk) ? i + s : -1;
   const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
   const double* W = Wc + (size_t)i * BP * WL;
   __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32];
@@ -698,9 +715,13 @@ __global__ __launch_bounds__(64) void k_fte_cost(FteDims d, const int* __restric
                                                  const double* __restrict__ wts, const double* __restrict__ Xbuf,
                                                  const double* __restrict__ taubuf, const double* __restrict__ qinv,
                                                  const FteState* __restrict__ st, int which /*0 cur, 1 trial*/,
+                                                 int k0, int lo, int hi,
                                                  double* __restrict__ Fm, double* __restrict__ Fq) {
+  // block k: measurement of frame k (owned iff lo <= k < hi) and the model stencil ending
+  // at row k + 2 (rows k-1..k+2, owned iff lo <= k-1 < hi)
   if (which == 1 && st->status != 0) return;
-  const int k = blockIdx.x;
+  const int k = blockIdx.x + k0;
+  const bool own_meas = k >= lo && k < hi, own_model = k >= 1 && k - 1 >= lo && k - 1 < hi;
   const int tid = threadIdx.x;
   const int P = d.P, C = d.C, L = d.L;
   const int buf = which == 1 ? (st->cur ^ 1) : st->cur;
@@ -719,7 +740,7 @@ __global__ __launch_bounds__(64) void k_fte_cost(FteDims d, const int* __restric
   fk_frame(s, X + f * P, fk, tid, blockDim.x);
   __syncthreads();
   double rho = 0.0;
-  for (int o = tid; o < C * L; o += blockDim.x) {
+  for (int o = own_meas ? tid : C * L; o < C * L; o += blockDim.x) {
     const int c = o / L, l = o - (o / L) * L;
     const int node = s.outn[l];
     const double tc = d.Cg ? tau[c] : 0.0;
@@ -737,7 +758,7 @@ __global__ __launch_bounds__(64) void k_fte_cost(FteDims d, const int* __restric
     rho += redescending(wt * (po.u - mu), d.la, d.lb, d.lc).f + redescending(wt * (po.v - mv), d.la, d.lb, d.lc).f;
   }
   double q = 0.0;
-  if (k >= 1) {
+  if (own_model) {
     const double its2 = 1.0 / (d.Ts * d.Ts);
     for (int p = tid; p < P; p += blockDim.x) {
       const double sm = (X[f * P + p] - 3.0 * X[(f - 1) * P + p] + 3.0 * X[(f - 2) * P + p] - X[(f - 3) * P + p]) * its2;
@@ -829,10 +850,14 @@ struct FteSetup {
   FteBuffers b;
 };
 
+// Dimensions, device buffers and initial state of one FTE problem. With `owned` == NULL
+// the buffers live in the context workspace (acs_fte_solve / acs_fte_eval); otherwise one
+// hipMalloc block is allocated for them and returned in *owned (the distributed handles,
+// several of which may share a context).
 static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
                      int64_t n_reals, const double* cams, int32_t n_cams, const double* meas, const double* w,
                      int32_t N, int32_t sd, double Ts, const double* qinv, int32_t intermode, const double* X,
-                     const double* tau, double la, double lb, double lc, uint32_t flags) {
+                     const double* tau, double la, double lb, double lc, uint32_t flags, void** owned = nullptr) {
   int hdr[FK_HDR];
   if (flags & ACS_DEVICE_PTRS)
     ACS_HIP(ctx, hipMemcpy(hdr, skel_ints, sizeof(hdr), hipMemcpyDeviceToHost));
@@ -868,20 +893,6 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   for (int s = 1; s < d.nblk; s <<= 1) d.nlev++;
   const int M = d.M, C = d.C, BP = d.BP, GR = d.GR, n = d.nblk;
   FteBuffers& b = S.b;
-  int rc;
-  void* p;
-  if ((rc = acs_stage_in(ctx, WS_FTE0, skel_ints, sizeof(int32_t) * n_ints, flags, &p))) return rc;
-  b.I = (int*)p;
-  if ((rc = acs_stage_in(ctx, WS_FTE1, skel_reals, sizeof(double) * n_reals, flags, &p))) return rc;
-  b.Rl = (double*)p;
-  if ((rc = acs_stage_in(ctx, WS_CAMS, cams, sizeof(double) * ACS_CAM_STRIDE * C, flags, &p))) return rc;
-  b.cams = (double*)p;
-  if ((rc = acs_stage_in(ctx, WS_FTE2, meas, sizeof(double) * (size_t)N * C * L * 2, flags, &p))) return rc;
-  b.meas = (double*)p;
-  if ((rc = acs_stage_in(ctx, WS_FTE3, w, sizeof(double) * (size_t)N * C * L, flags, &p))) return rc;
-  b.w = (double*)p;
-  if ((rc = acs_stage_in(ctx, WS_FTE4, qinv, sizeof(double) * P, flags, &p))) return rc;
-  b.qinv = (double*)p;
   size_t off = 0;
   auto take = [&](size_t cnt) {
     size_t o = off;
@@ -894,10 +905,50 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
                ogb = take((size_t)M * P), oBt = take((size_t)M * P * Cg1), ogm = take(M),
                oD = take((size_t)n * BP * BP), oE = take((size_t)n * BP * BP), oG = take((size_t)n * BP * GR),
                oW = take((size_t)n * BP * (2 * BP + GR)), oTau = take((size_t)n * GR * GR),
-               odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)), onp = take(2 * (size_t)n), oFm = take(N), oFq = take(N),
-               ost = take(16), oint = take(8);
-  double* arena = (double*)acs_ws(ctx, WS_FTE5, off * sizeof(double));
-  if (!arena) return ACS_E_NOMEM;
+               odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)),
+               onp = take(2 * (size_t)n), oFm = take(N), oFq = take(N), ost = take(16), oint = take(8);
+  // staged inputs (owned mode only)
+  const size_t oI = take((n_ints + 1) / 2 + 1), oR = take(n_reals), oC = take((size_t)ACS_CAM_STRIDE * C),
+               oMe = take((size_t)N * C * L * 2), oWt = take((size_t)N * C * L), oQ = take(P);
+  double* arena;
+  const size_t inputs_from = oI;
+  hipStream_t s = ctx->stream;
+  const hipMemcpyKind kin = (flags & ACS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  int rc;
+  if (owned) {
+    void* p = nullptr;
+    ACS_HIP(ctx, hipMalloc(&p, off * sizeof(double)));
+    *owned = p;
+    arena = (double*)p;
+    b.I = (int*)(arena + oI);
+    b.Rl = arena + oR;
+    b.cams = arena + oC;
+    b.meas = arena + oMe;
+    b.w = arena + oWt;
+    b.qinv = arena + oQ;
+    ACS_HIP(ctx, hipMemcpyAsync(b.I, skel_ints, sizeof(int32_t) * n_ints, kin, s));
+    ACS_HIP(ctx, hipMemcpyAsync(b.Rl, skel_reals, sizeof(double) * n_reals, kin, s));
+    ACS_HIP(ctx, hipMemcpyAsync(b.cams, cams, sizeof(double) * ACS_CAM_STRIDE * C, kin, s));
+    ACS_HIP(ctx, hipMemcpyAsync(b.meas, meas, sizeof(double) * (size_t)N * C * L * 2, kin, s));
+    ACS_HIP(ctx, hipMemcpyAsync(b.w, w, sizeof(double) * (size_t)N * C * L, kin, s));
+    ACS_HIP(ctx, hipMemcpyAsync(b.qinv, qinv, sizeof(double) * P, kin, s));
+  } else {
+    void* p;
+    if ((rc = acs_stage_in(ctx, WS_FTE0, skel_ints, sizeof(int32_t) * n_ints, flags, &p))) return rc;
+    b.I = (int*)p;
+    if ((rc = acs_stage_in(ctx, WS_FTE1, skel_reals, sizeof(double) * n_reals, flags, &p))) return rc;
+    b.Rl = (double*)p;
+    if ((rc = acs_stage_in(ctx, WS_CAMS, cams, sizeof(double) * ACS_CAM_STRIDE * C, flags, &p))) return rc;
+    b.cams = (double*)p;
+    if ((rc = acs_stage_in(ctx, WS_FTE2, meas, sizeof(double) * (size_t)N * C * L * 2, flags, &p))) return rc;
+    b.meas = (double*)p;
+    if ((rc = acs_stage_in(ctx, WS_FTE3, w, sizeof(double) * (size_t)N * C * L, flags, &p))) return rc;
+    b.w = (double*)p;
+    if ((rc = acs_stage_in(ctx, WS_FTE4, qinv, sizeof(double) * P, flags, &p))) return rc;
+    b.qinv = (double*)p;
+    arena = (double*)acs_ws(ctx, WS_FTE5, inputs_from * sizeof(double));
+    if (!arena) return ACS_E_NOMEM;
+  }
   b.X = arena + oX;
   b.tau = arena + oT;
   b.Hloc = arena + oH;
@@ -920,8 +971,6 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.Fq = arena + oFq;
   b.st = (FteState*)(arena + ost);
   b.bad = (int*)(arena + oint);
-  hipStream_t s = ctx->stream;
-  const hipMemcpyKind kin = (flags & ACS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   ACS_HIP(ctx, hipMemcpyAsync(b.X, X, sizeof(double) * M * P, kin, s));
   if (tau)
     ACS_HIP(ctx, hipMemcpyAsync(b.tau, tau, sizeof(double) * C, kin, s));
@@ -938,9 +987,9 @@ static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
   hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
-                     b.st, force, b.Hloc, b.gloc, b.Floc);
-  hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.qinv, b.st, force, b.Hloc, b.gloc, b.Ab,
-                     b.gb, b.Bt, b.gmaxp);
+                     b.st, force, 0, b.Hloc, b.gloc, b.Floc);
+  hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.qinv, b.st, force, 0, 0, INT_MAX, b.Hloc,
+                     b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp);
 }
 
 // one LM iteration: linearise (if the last step was accepted), cyclic-reduction solve,
@@ -951,25 +1000,285 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   fte_enqueue_linearize(S, s, 0);
   const size_t lds_elim = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1) + 512);
   const size_t lds_upd = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1));
-  hipLaunchKernelGGL(k_cr_build, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc);
+  hipLaunchKernelGGL(k_cr_build, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, 0, -1,
+                     -1);
+  const int bend = d.nblk - 1;
   for (int lv = 0, st = 1; lv < d.nlev; ++lv, st <<= 1) {
     const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
     const int ns = (d.nblk + 2 * st - 1) / (2 * st);
-    hipLaunchKernelGGL(k_cr_elim, dim3(ne), dim3(1024), lds_elim, s, d, st, b.st, b.Dc, b.Ec, b.GBc, b.Wc, b.Tau, b.bad);
-    hipLaunchKernelGGL(k_cr_update, dim3(ns), dim3(1024), lds_upd, s, d, st, b.st, b.Dc, b.Ec, b.GBc, b.Wc);
+    hipLaunchKernelGGL(k_cr_elim, dim3(ne), dim3(1024), lds_elim, s, d, st, 0, bend, b.st, b.Dc, b.Ec, b.GBc, b.Wc,
+                       b.Tau, b.bad);
+    hipLaunchKernelGGL(k_cr_update, dim3(ns), dim3(1024), lds_upd, s, d, st, 0, bend, b.st, b.Dc, b.Ec, b.GBc, b.Wc);
   }
-  hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part);
+  hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
+                     d.N, 1, d.nblk);
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, d, b.st, b.Dc, b.GBc, b.part, b.gmaxp, b.dcv, b.dtau,
                      b.bad);
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
-    hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(256), 0, s, d, st, b.st, b.Wc, b.dtau, b.dcv);
+    hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(256), 0, s, d, st, 0, bend, b.st, b.Wc, b.dtau, b.dcv);
   }
   hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.X, b.tau, b.normp);
   hipLaunchKernelGGL(k_fte_cost, dim3(d.N), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau, b.qinv,
-                     b.st, 1, b.Fm, b.Fq);
+                     b.st, 1, 0, 0, INT_MAX, b.Fm, b.Fq);
   hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 0, b.Fm, b.Fq, b.normp);
+}
+
+// =======================================================================================
+// frame-window distributed solve (spec: oracle/fte_dist.py)
+//
+// Super-blocks are split into R chains [a_r, a_r + 2^k] that share their end blocks
+// (a_r = r 2^k; blocks past the sequence are phantoms). A term is owned by the chain
+// containing its lowest row, so every term is counted on exactly one rank and the
+// chain-end blocks hold partial sums. Per LM iteration:
+//   phase 1  linearise owned frames, assemble chain rows, block cyclic reduction of the
+//            chain interior down to its two ends (ends undamped), pack the ends' blocks,
+//            raw diagonals / gradients, tau partial sums and an interior |g| max into
+//            payload 1 (zeros elsewhere)                                 -> all-reduce
+//   phase 2  every rank: reduced block-tridiagonal system over the R+1 chain ends + tau
+//            (damped with the summed raw diagonals), solved with the same CR kernels;
+//            back substitution down its own chain; its rows of delta into payload 2
+//                                                                        -> all-reduce
+//   phase 3  trial state on every rank (replicated X), cost of the owned terms
+//                                                        -> all-reduce (2 doubles)
+//   phase 4  the same accept/reject decision on every rank
+// =======================================================================================
+struct DistLayout {
+  size_t oD, oE, oG, oGraw, oRdiag, oTau, oGmax, n1, n2, n3;
+};
+
+static DistLayout dist_layout(const FteDims& d, int R) {
+  DistLayout L;
+  const size_t nb = R + 1, BP = d.BP, GR = d.GR, nE = (size_t)d.Cg * d.Cg + d.Cg + (size_t)GR * GR;
+  L.oD = 0;
+  L.oE = L.oD + nb * BP * BP;
+  L.oG = L.oE + nb * BP * BP;
+  L.oGraw = L.oG + nb * BP * GR;
+  L.oRdiag = L.oGraw + nb * BP;
+  L.oTau = L.oRdiag + nb * BP;
+  L.oGmax = L.oTau + nE;
+  L.n1 = L.oGmax + R;
+  L.n2 = (size_t)d.nblk * BP;
+  L.n3 = 2;
+  return L;
+}
+
+// chain ends -> payload slots `rank` (left end a0) and `rank + 1` (right end bend)
+__global__ __launch_bounds__(256) void k_dist_pack(FteDims d, const FteState* __restrict__ st, DistLayout Lo,
+                                                   int rank, int a0, int bend, const double* __restrict__ Dc,
+                                                   const double* __restrict__ Ec, const double* __restrict__ GBc,
+                                                   const double* __restrict__ Ab, const double* __restrict__ gb,
+                                                   double* __restrict__ p1) {
+  if (st->status != 0) return;
+  const int side = blockIdx.y;  // 0 left end, 1 right end
+  const int blk = side ? bend : a0, q = rank + side;
+  if (blk >= d.nblk) return;
+  const int BP = d.BP, GR = d.GR, P = d.P, PP = P * P;
+  const size_t nBB = (size_t)BP * BP;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < nBB; e += (size_t)gridDim.x * blockDim.x) {
+    p1[Lo.oD + q * nBB + e] = Dc[(size_t)blk * nBB + e];
+    if (side) p1[Lo.oE + q * nBB + e] = Ec[(size_t)blk * nBB + e];
+  }
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)BP * GR;
+       e += (size_t)gridDim.x * blockDim.x)
+    p1[Lo.oG + (size_t)q * BP * GR + e] = GBc[(size_t)blk * BP * GR + e];
+  if (blockIdx.x == 0) {
+    for (int r = threadIdx.x; r < BP; r += blockDim.x) {
+      const int fr = 3 * blk + r / P, pr = r % P;
+      const bool in = r < 3 * P && fr < d.M;
+      p1[Lo.oGraw + (size_t)q * BP + r] = in ? gb[(size_t)fr * P + pr] : 0.0;
+      p1[Lo.oRdiag + (size_t)q * BP + r] = in ? Ab[(size_t)fr * 4 * PP + pr * P + pr] : 0.0;
+    }
+  }
+}
+
+// tau partial sums of the chain (fixed chunk order) and the |g| max of its interior rows
+__global__ __launch_bounds__(256) void k_dist_pack_small(FteDims d, const FteState* __restrict__ st, DistLayout Lo,
+                                                         int rank, int a0, int bend,
+                                                         const double* __restrict__ part,
+                                                         const double* __restrict__ gmaxp,
+                                                         double* __restrict__ p1) {
+  if (st->status != 0) return;
+  __shared__ double s_red[256];
+  const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
+  for (int e = threadIdx.x; e < nE; e += blockDim.x) {
+    double v = 0.0;
+    for (int ch = 0; ch < CR_NCHUNK; ++ch) v += part[(size_t)ch * nE + e];
+    p1[Lo.oTau + e] = v;
+  }
+  const int f0 = 3 * (a0 + 1), f1 = min(3 * min(bend, d.nblk), d.M);
+  double mx = 0.0;
+  for (int f = f0 + threadIdx.x; f < f1; f += blockDim.x) mx = fmax(mx, gmaxp[f]);
+  mx = block_max(mx, s_red);
+  if (threadIdx.x == 0) p1[Lo.oGmax + rank] = mx;
+}
+
+// reduced system over the chain ends e_q = q 2^k (q = 0..R) from the summed payload
+__global__ __launch_bounds__(256) void k_red_build(FteDims d, const FteState* __restrict__ st, DistLayout Lo, int R,
+                                                   int span, const double* __restrict__ p1, double* __restrict__ Dr,
+                                                   double* __restrict__ Er, double* __restrict__ GBr,
+                                                   double* __restrict__ gmaxr) {
+  if (st->status != 0) return;
+  __shared__ double s_red[256];
+  const int q = blockIdx.x, e = q * span;
+  const int BP = d.BP, GR = d.GR, P = d.P;
+  const size_t nBB = (size_t)BP * BP;
+  const double lam = st->lam;
+  // rows of block x that are real unknowns (not padding / phantom)
+  auto live = [&](int x, int r) { return x >= 0 && x < d.nblk && r < 3 * P && 3 * x + r / P < d.M; };
+  for (size_t x = threadIdx.x; x < nBB; x += blockDim.x) {
+    const int r = (int)(x / BP), c = (int)(x % BP);
+    double v = (r == c) ? 1.0 : 0.0;
+    if (live(e, r) && live(e, c)) {
+      v = p1[Lo.oD + q * nBB + x];
+      if (r == c) v += lam * fmax(p1[Lo.oRdiag + (size_t)q * BP + r], 1e-12);
+    }
+    Dr[q * nBB + x] = v;
+    Er[q * nBB + x] = (q > 0 && live(e, r) && live(e - span, c)) ? p1[Lo.oE + q * nBB + x] : 0.0;
+  }
+  for (size_t x = threadIdx.x; x < (size_t)BP * GR; x += blockDim.x) {
+    const int r = (int)(x / GR);
+    GBr[(size_t)q * BP * GR + x] = live(e, r) ? p1[Lo.oG + (size_t)q * BP * GR + x] : 0.0;
+  }
+  if (q == 0) {
+    double mx = 0.0;
+    for (int t = threadIdx.x; t < R; t += blockDim.x) mx = fmax(mx, p1[Lo.oGmax + t]);
+    for (int t = threadIdx.x; t < (R + 1) * BP; t += blockDim.x) {
+      const int qq = t / BP, r = t % BP, ee = qq * span;
+      if (ee < d.nblk && r < 3 * P && 3 * ee + r / P < d.M) mx = fmax(mx, fabs(p1[Lo.oGraw + t]));
+    }
+    mx = block_max(mx, s_red);
+    if (threadIdx.x == 0) gmaxr[0] = mx;
+  }
+}
+
+__global__ void k_red_part(int nE, const DistLayout Lo, const FteState* __restrict__ st,
+                           const double* __restrict__ p1, double* __restrict__ partr) {
+  if (st->status != 0) return;
+  for (int e = threadIdx.x; e < nE; e += blockDim.x) partr[e] += p1[Lo.oTau + e];
+}
+
+__global__ void k_dist_scatter(FteDims d, const FteState* __restrict__ st, int rank, int a0, int bend,
+                               const double* __restrict__ dcvr, double* __restrict__ dcv) {
+  if (st->status != 0) return;
+  for (int r = threadIdx.x; r < d.BP; r += blockDim.x) {
+    if (a0 < d.nblk) dcv[(size_t)a0 * d.BP + r] = dcvr[(size_t)rank * d.BP + r];
+    if (bend < d.nblk) dcv[(size_t)bend * d.BP + r] = dcvr[(size_t)(rank + 1) * d.BP + r];
+  }
+}
+
+// this rank's rows of the step: blocks [a0, bend) (the last rank also its end block)
+__global__ __launch_bounds__(256) void k_dist_delta_out(FteDims d, const FteState* __restrict__ st, int b_lo,
+                                                        int b_hi, const double* __restrict__ dcv,
+                                                        double* __restrict__ p2) {
+  if (st->status != 0) return;
+  const size_t n0 = (size_t)b_lo * d.BP, n1 = (size_t)b_hi * d.BP;
+  for (size_t e = n0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n1; e += (size_t)gridDim.x * blockDim.x)
+    p2[e] = dcv[e];
+}
+
+__global__ __launch_bounds__(256) void k_dist_cost_pack(const FteState* __restrict__ st, int which, int k0, int k1,
+                                                        const double* __restrict__ Fm, const double* __restrict__ Fq,
+                                                        double* __restrict__ p3) {
+  if (which == 1 && st->status != 0) return;
+  __shared__ double s_red[256];
+  double a = 0.0, b = 0.0;
+  for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
+    a += Fm[k];
+    b += Fq[k];
+  }
+  a = block_sum(a, s_red);
+  b = block_sum(b, s_red);
+  if (threadIdx.x == 0) {
+    p3[0] = a;
+    p3[1] = b;
+  }
+}
+
+// k_fte_lm with the all-reduced costs (every rank takes the same decision)
+__global__ __launch_bounds__(256) void k_fte_lm_dist(FteDims d, FteState* __restrict__ st, FteOptsDev o, int init,
+                                                     const double* __restrict__ p3,
+                                                     const double* __restrict__ normp) {
+  __shared__ double s_red[256];
+  const int tid = threadIdx.x;
+  const double fm = p3[0], fq = p3[1];
+  if (init) {
+    if (tid == 0) {
+      st->F = st->F0 = fm + fq;
+      st->Fmeas = fm;
+      st->Fmodel = fq;
+    }
+    return;
+  }
+  if (st->status != 0) return;
+  double dn = 0.0, xn = 0.0;
+  for (int w = tid; w < d.nblk; w += blockDim.x) {
+    dn += normp[2 * w];
+    xn += normp[2 * w + 1];
+  }
+  dn = block_sum(dn, s_red);
+  xn = block_sum(xn, s_red);
+  if (tid != 0) return;
+  if (st->gmax <= o.gtol) {
+    st->status = ACS_STATUS_GTOL;
+    return;
+  }
+  const double Fn = fm + fq;
+  st->iters += 1;
+  st->dnorm = sqrt(dn);
+  st->xnorm = sqrt(xn);
+  const bool small = sqrt(dn) <= o.xtol * (o.xtol + sqrt(xn));
+  if (Fn < st->F) {
+    const bool fconv = (st->F - Fn) <= o.ftol * fabs(st->F);
+    st->nacc += 1;
+    st->F = Fn;
+    st->Fmeas = fm;
+    st->Fmodel = fq;
+    st->cur ^= 1;
+    st->lam = fmax(st->lam * 0.1, 1e-15);
+    st->relin = 1;
+    if (fconv)
+      st->status = ACS_STATUS_FTOL;
+    else if (small)
+      st->status = ACS_STATUS_XTOL;
+  } else {
+    st->lam *= 10.0;
+    st->relin = 0;
+    if (st->lam > 1e16) st->status = ACS_STATUS_STALLED;
+  }
+  if (st->status == 0 && st->iters >= o.max_iters) st->status = ACS_STATUS_MAXITER;
+}
+
+struct acs_fte_dist {
+  acs_ctx* ctx;
+  FteSetup S;
+  void* own = nullptr;
+  void* own_red = nullptr;
+  FteDims dr;        // reduced system dims (R + 1 blocks)
+  FteBuffers r;      // reduced arrays (Dc, Ec, GBc, Wc, Tau, dcv, part, gmaxp)
+  DistLayout Lo;
+  FteOptsDev o;
+  int R, rank, span, a0, bend, klev;
+  int k_lo, k_hi, f_lo, f_hi, b_hi_build, c_lo, c_hi, own_lo, own_hi, out_lo, out_hi;
+};
+
+static void dist_local_cr(acs_fte_dist* h) {
+  const FteDims& d = h->S.d;
+  FteBuffers& b = h->S.b;
+  hipStream_t s = h->ctx->stream;
+  const size_t lds_elim = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1) + 512);
+  const size_t lds_upd = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1));
+  const int top = std::min(h->bend, d.nblk - 1);  // last existing block of the chain
+  for (int lv = 0, st = 1; lv < h->klev; ++lv, st <<= 1) {
+    int ne = 0, ns = 0;
+    for (int i = h->a0 + st; i < std::min(h->bend, d.nblk); i += 2 * st) ++ne;
+    for (int j = h->a0; j <= top; j += 2 * st) ++ns;
+    if (ne) hipLaunchKernelGGL(k_cr_elim, dim3(ne), dim3(1024), lds_elim, s, d, st, h->a0, h->bend, b.st, b.Dc, b.Ec,
+                               b.GBc, b.Wc, b.Tau, b.bad);
+    if (ns) hipLaunchKernelGGL(k_cr_update, dim3(ns), dim3(1024), lds_upd, s, d, st, h->a0, h->bend, b.st, b.Dc,
+                               b.Ec, b.GBc, b.Wc);
+  }
 }
 
 extern "C" {
@@ -1010,7 +1319,7 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   ACS_HIP(ctx, hipMemcpyAsync(b.st, &st0, sizeof(st0), hipMemcpyHostToDevice, s));
   FteOptsDev o{op.max_iters, op.ftol, op.xtol, op.gtol};
   hipLaunchKernelGGL(k_fte_cost, dim3(d.N), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau, b.qinv,
-                     b.st, 0, b.Fm, b.Fq);
+                     b.st, 0, 0, 0, INT_MAX, b.Fm, b.Fq);
   hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 1, b.Fm, b.Fq, b.normp);
   ACS_HIP(ctx, hipGetLastError());
   // capture `chunk` iterations into one hipGraph (kernels read the LM state from device
@@ -1095,7 +1404,7 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
   ACS_HIP(ctx, hipMemcpyAsync(b.st, &st0, sizeof(st0), hipMemcpyHostToDevice, s));
   fte_enqueue_linearize(S, s, 1);
   hipLaunchKernelGGL(k_fte_cost, dim3(d.N), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau, b.qinv,
-                     b.st, 0, b.Fm, b.Fq);
+                     b.st, 0, 0, 0, INT_MAX, b.Fm, b.Fq);
   ACS_HIP(ctx, hipGetLastError());
   const int M = d.M, P = d.P, Cg = d.Cg, N = d.N, PP = P * P;
   std::vector<double> Ab((size_t)M * 4 * PP), gb((size_t)M * P), Bt((size_t)M * P * (Cg ? Cg : 1)),
@@ -1150,6 +1459,261 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
         for (int k = 0; k < N; ++k) v += Hl[(size_t)k * FTE_NZP * FTE_NZP + (P + 6 + r) * FTE_NZP + P + 6 + c];
         H[(size_t)(M * P + r) * nv + M * P + c] = v;
       }
+  }
+  return ACS_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// distributed handle API (include/acinoset_hip.h, §8(e)); payloads are device pointers
+// ---------------------------------------------------------------------------------------
+extern "C" {
+
+int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
+                        int64_t n_reals, const double* cams, int32_t n_cams, const double* meas, const double* w,
+                        int32_t n_frames, int32_t shutter_delay, double Ts, const double* qinv, int32_t sd_mode,
+                        int32_t intermode, const double* X, const double* tau, const acs_fte_opts* opts, int32_t rank,
+                        int32_t world, acs_fte_dist** out, int64_t* payload_sizes, uint32_t flags) {
+  acs_fte_opts op;
+  acs_fte_default_opts(&op);
+  if (opts) op = *opts;
+  ACS_CHECK(ctx, sd_mode == 0, "fte: only shutter_delay_mode='const' (0) is implemented");
+  ACS_CHECK(ctx, op.max_iters >= 0, "fte: max_iters < 0");
+  ACS_CHECK(ctx, world >= 1 && world <= 1024 && rank >= 0 && rank < world, "fte_dist: rank %d / world %d", rank,
+            world);
+  acs_fte_dist* h = new acs_fte_dist();
+  h->ctx = ctx;
+  int rc = fte_setup(ctx, h->S, skel_ints, n_ints, skel_reals, n_reals, cams, n_cams, meas, w, n_frames,
+                     shutter_delay, Ts, qinv, intermode, X, tau, op.redesc_a, op.redesc_b, op.redesc_c, flags, &h->own);
+  if (rc) {
+    if (h->own) (void)hipFree(h->own);
+    delete h;
+    return rc;
+  }
+  const FteDims& d = h->S.d;
+  h->R = world;
+  h->rank = rank;
+  h->o = FteOptsDev{op.max_iters, op.ftol, op.xtol, op.gtol};
+  // chain length 2^k: smallest k >= 1 with R 2^k >= nblk - 1
+  h->klev = 1;
+  while ((int64_t)world * (1 << h->klev) < d.nblk - 1) h->klev++;
+  h->span = 1 << h->klev;
+  h->a0 = rank * h->span;
+  h->bend = h->a0 + h->span;
+  const int N = d.N, M = d.M;
+  auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+  h->own_lo = 3 * h->a0;                    // owned terms: lowest row in [own_lo, own_hi)
+  h->own_hi = rank == world - 1 ? INT_MAX / 2 : 3 * h->bend;  // the last rank owns the tail
+  h->k_lo = clampi(h->own_lo, 0, N);        // frames to linearise
+  h->k_hi = clampi(h->own_hi, 0, N);
+  h->f_lo = clampi(3 * h->a0, 0, M);        // rows to assemble (chain incl. its right end)
+  h->f_hi = clampi(3 * h->bend + 3, 0, M);
+  h->c_lo = clampi(h->own_lo, 0, N);        // cost blocks: frames [lo, hi) and stencils up to hi
+  h->c_hi = clampi(h->own_hi + 1, 0, N);
+  h->out_lo = clampi(h->a0, 0, d.nblk);     // step rows this rank publishes
+  h->out_hi = clampi(rank == world - 1 ? h->bend + 1 : h->bend, 0, d.nblk);
+  h->Lo = dist_layout(d, world);
+  // reduced system arrays
+  FteDims& dr = h->dr;
+  dr = d;
+  dr.nblk = world + 1;
+  dr.M = 1;
+  dr.N = 0;
+  dr.nlev = 0;
+  for (int s = 1; s < dr.nblk; s <<= 1) dr.nlev++;
+  const size_t nb = dr.nblk, BP = d.BP, GR = d.GR;
+  size_t off = 0;
+  auto take = [&](size_t cnt) {
+    size_t o = off;
+    off += ((cnt * sizeof(double) + 255) / 256) * 256 / sizeof(double);
+    return o;
+  };
+  const size_t oD = take(nb * BP * BP), oE = take(nb * BP * BP), oG = take(nb * BP * GR),
+               oW = take(nb * BP * (2 * BP + GR)), oT = take(nb * GR * GR), odc = take(nb * BP),
+               op_ = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)), ogm = take(4);
+  void* p = nullptr;
+  if (hipMalloc(&p, off * sizeof(double)) != hipSuccess) {
+    (void)hipFree(h->own);
+    delete h;
+    return acs_fail(ctx, ACS_E_NOMEM, "fte_dist: reduced-system allocation failed");
+  }
+  h->own_red = p;
+  double* a = (double*)p;
+  h->r = h->S.b;
+  h->r.Dc = a + oD;
+  h->r.Ec = a + oE;
+  h->r.GBc = a + oG;
+  h->r.Wc = a + oW;
+  h->r.Tau = a + oT;
+  h->r.dcv = a + odc;
+  h->r.part = a + op_;
+  h->r.gmaxp = a + ogm;
+  FteState st0;
+  std::memset(&st0, 0, sizeof(st0));
+  st0.lam = op.lambda0;
+  st0.relin = 1;
+  ACS_HIP(ctx, hipMemcpyAsync(h->S.b.st, &st0, sizeof(st0), hipMemcpyHostToDevice, ctx->stream));
+  ACS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (payload_sizes) {
+    payload_sizes[0] = (int64_t)h->Lo.n1;
+    payload_sizes[1] = (int64_t)h->Lo.n2;
+    payload_sizes[2] = (int64_t)h->Lo.n3;
+  }
+  *out = h;
+  return ACS_OK;
+}
+
+int acs_fte_dist_destroy(acs_fte_dist* h) {
+  if (!h) return ACS_OK;
+  (void)hipStreamSynchronize(h->ctx->stream);
+  if (h->own) (void)hipFree(h->own);
+  if (h->own_red) (void)hipFree(h->own_red);
+  delete h;
+  return ACS_OK;
+}
+
+// cost of the owned terms at the current state -> p3 (before the first phase 4, init = 1)
+int acs_fte_dist_init(acs_fte_dist* h, double* p3) {
+  acs_ctx* ctx = h->ctx;
+  const FteDims& d = h->S.d;
+  FteBuffers& b = h->S.b;
+  hipStream_t s = ctx->stream;
+  if (h->c_hi > h->c_lo)
+    hipLaunchKernelGGL(k_fte_cost, dim3(h->c_hi - h->c_lo), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
+                       b.tau, b.qinv, b.st, 0, h->c_lo, h->own_lo, h->own_hi, b.Fm, b.Fq);
+  hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 0, h->c_lo, h->c_hi, b.Fm, b.Fq, p3);
+  ACS_HIP(ctx, hipGetLastError());
+  return ACS_OK;
+}
+
+int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
+  acs_ctx* ctx = h->ctx;
+  const FteDims& d = h->S.d;
+  FteBuffers& b = h->S.b;
+  hipStream_t s = ctx->stream;
+  ACS_HIP(ctx, hipMemsetAsync(p1, 0, sizeof(double) * h->Lo.n1, s));
+  if (h->a0 < d.nblk) {
+    if (h->k_hi > h->k_lo)
+      hipLaunchKernelGGL(k_fte_linearize, dim3(h->k_hi - h->k_lo), dim3(256), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w,
+                         b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc);
+    hipLaunchKernelGGL(k_fte_assemble, dim3(h->f_hi - h->f_lo), dim3(256), 0, s, d, b.X, b.qinv, b.st, 0, h->f_lo,
+                       h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp);
+    const int top = std::min(h->bend, d.nblk - 1);
+    hipLaunchKernelGGL(k_cr_build, dim3(top - h->a0 + 1), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec,
+                       b.GBc, h->a0, h->a0, h->bend);
+    dist_local_cr(h);
+    hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part,
+                       h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk));
+    hipLaunchKernelGGL(k_dist_pack, dim3(32, 2), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.Dc, b.Ec,
+                       b.GBc, b.Ab, b.gb, p1);
+    hipLaunchKernelGGL(k_dist_pack_small, dim3(1), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.part,
+                       b.gmaxp, p1);
+  }
+  ACS_HIP(ctx, hipGetLastError());
+  return ACS_OK;
+}
+
+int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
+  acs_ctx* ctx = h->ctx;
+  const FteDims& d = h->S.d;
+  const FteDims& dr = h->dr;
+  FteBuffers& b = h->S.b;
+  FteBuffers& r = h->r;
+  hipStream_t s = ctx->stream;
+  const size_t lds_elim = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1) + 512);
+  const size_t lds_upd = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1));
+  // reduced system (identical on every rank)
+  hipLaunchKernelGGL(k_red_build, dim3(dr.nblk), dim3(256), 0, s, d, b.st, h->Lo, h->R, h->span, p1, r.Dc, r.Ec,
+                     r.GBc, r.gmaxp);
+  const int rb = dr.nblk - 1;
+  for (int lv = 0, st = 1; lv < dr.nlev; ++lv, st <<= 1) {
+    const int ne = (dr.nblk - st + 2 * st - 1) / (2 * st);
+    const int ns = (dr.nblk + 2 * st - 1) / (2 * st);
+    hipLaunchKernelGGL(k_cr_elim, dim3(ne), dim3(1024), lds_elim, s, dr, st, 0, rb, b.st, r.Dc, r.Ec, r.GBc, r.Wc,
+                       r.Tau, b.bad);
+    hipLaunchKernelGGL(k_cr_update, dim3(ns), dim3(1024), lds_upd, s, dr, st, 0, rb, b.st, r.Dc, r.Ec, r.GBc, r.Wc);
+  }
+  hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, dr, b.st, r.Hloc, r.gloc, r.Tau, r.part, 0,
+                     0, 1, dr.nblk);
+  const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
+  hipLaunchKernelGGL(k_red_part, dim3(1), dim3(256), 0, s, nE, h->Lo, b.st, p1, r.part);
+  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, dr, b.st, r.Dc, r.GBc, r.part, r.gmaxp, r.dcv, b.dtau, b.bad);
+  for (int lv = dr.nlev - 1; lv >= 0; --lv) {
+    const int st = 1 << lv;
+    const int ne = (dr.nblk - st + 2 * st - 1) / (2 * st);
+    hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(256), 0, s, dr, st, 0, rb, b.st, r.Wc, b.dtau, r.dcv);
+  }
+  // this chain: ends from the reduced solve, interior by back substitution
+  ACS_HIP(ctx, hipMemsetAsync(p2, 0, sizeof(double) * h->Lo.n2, s));
+  if (h->a0 < d.nblk) {
+    hipLaunchKernelGGL(k_dist_scatter, dim3(1), dim3(128), 0, s, d, b.st, h->rank, h->a0, h->bend, r.dcv, b.dcv);
+    for (int lv = h->klev - 1; lv >= 0; --lv) {
+      const int st = 1 << lv;
+      int ne = 0;
+      for (int i = h->a0 + st; i < std::min(h->bend, d.nblk); i += 2 * st) ++ne;
+      if (ne) hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(256), 0, s, d, st, h->a0, h->bend, b.st, b.Wc, b.dtau, b.dcv);
+    }
+    if (h->out_hi > h->out_lo)
+      hipLaunchKernelGGL(k_dist_delta_out, dim3(64), dim3(256), 0, s, d, b.st, h->out_lo, h->out_hi, b.dcv, p2);
+  }
+  ACS_HIP(ctx, hipGetLastError());
+  return ACS_OK;
+}
+
+int acs_fte_dist_phase3(acs_fte_dist* h, const double* p2, double* p3) {
+  acs_ctx* ctx = h->ctx;
+  const FteDims& d = h->S.d;
+  FteBuffers& b = h->S.b;
+  hipStream_t s = ctx->stream;
+  hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, p2, b.dtau, b.X, b.tau, b.normp);
+  if (h->c_hi > h->c_lo)
+    hipLaunchKernelGGL(k_fte_cost, dim3(h->c_hi - h->c_lo), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
+                       b.tau, b.qinv, b.st, 1, h->c_lo, h->own_lo, h->own_hi, b.Fm, b.Fq);
+  hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 1, h->c_lo, h->c_hi, b.Fm, b.Fq, p3);
+  ACS_HIP(ctx, hipGetLastError());
+  return ACS_OK;
+}
+
+int acs_fte_dist_phase4(acs_fte_dist* h, const double* p3, int32_t init, int32_t* status) {
+  acs_ctx* ctx = h->ctx;
+  const FteDims& d = h->S.d;
+  FteBuffers& b = h->S.b;
+  hipStream_t s = ctx->stream;
+  hipLaunchKernelGGL(k_fte_lm_dist, dim3(1), dim3(256), 0, s, d, b.st, h->o, init, p3, b.normp);
+  ACS_HIP(ctx, hipGetLastError());
+  int32_t stv = 0;
+  ACS_HIP(ctx, hipMemcpyAsync(&stv, &b.st->status, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  ACS_HIP(ctx, hipStreamSynchronize(s));
+  if (status) *status = stv;
+  return ACS_OK;
+}
+
+int acs_fte_dist_result(acs_fte_dist* h, double* X, double* tau, acs_fte_report* report, uint32_t flags) {
+  acs_ctx* ctx = h->ctx;
+  const FteDims& d = h->S.d;
+  FteBuffers& b = h->S.b;
+  hipStream_t s = ctx->stream;
+  FteState hs;
+  ACS_HIP(ctx, hipMemcpyAsync(&hs, b.st, sizeof(hs), hipMemcpyDeviceToHost, s));
+  ACS_HIP(ctx, hipStreamSynchronize(s));
+  const hipMemcpyKind kout = (flags & ACS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  if (X) ACS_HIP(ctx, hipMemcpyAsync(X, b.X + (size_t)hs.cur * d.M * d.P, sizeof(double) * d.M * d.P, kout, s));
+  if (tau) ACS_HIP(ctx, hipMemcpyAsync(tau, b.tau + hs.cur * d.C, sizeof(double) * d.C, kout, s));
+  int nbad = 0;
+  ACS_HIP(ctx, hipMemcpyAsync(&nbad, b.bad, sizeof(int), hipMemcpyDeviceToHost, s));
+  ACS_HIP(ctx, hipStreamSynchronize(s));
+  if (report) {
+    report->status = hs.status == 0 ? ACS_STATUS_MAXITER : hs.status;
+    report->iters = hs.iters;
+    report->n_accepted = hs.nacc;
+    report->n_bad_pivots = nbad;
+    report->cost_before = hs.F0;
+    report->cost_after = hs.F;
+    report->cost_meas = hs.Fmeas;
+    report->cost_model = hs.Fmodel;
+    report->grad_max = hs.gmax;
+    report->lambda_final = hs.lam;
   }
   return ACS_OK;
 }

@@ -1,0 +1,189 @@
+"""Frame-window distributed FTE solve (BASELINE configs[3]).
+
+One process per GPU (torchrun); ranks split the trajectory's 3-frame super-blocks into
+chains that share their end blocks (include/acinoset_hip.h, acs_fte_dist_*). Every LM
+iteration exchanges three sums over the ranks:
+
+  p1  the chain ends' reduced normal-equation blocks + tau border (~1 MB at 8 ranks)
+  p2  the step (each rank fills its own rows)
+  p3  the costs of the owned terms (2 doubles)
+
+with `torch.distributed.all_reduce` (RCCL over xGMI on the "nccl" backend; gloo in the CPU
+tests). Every rank then runs the same reduced solve and the same accept/reject decision,
+so the state stays replicated without any broadcast.
+
+`lm_loop` is the protocol, independent of the backend: the HIP ranks below, or the numpy
+restatement in oracle/fte_dist.py that the CPU tests plug in.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _native
+
+
+def lm_loop(ranks, allreduce):
+    """Drive the distributed LM. `ranks`: the backends living in this process (one per
+    process under torch.distributed, several for the single-process emulation);
+    `allreduce(list_of_payloads)` sums the i-th payload over all ranks in place."""
+    p3 = [r.init() for r in ranks]
+    allreduce(p3)
+    for r, p in zip(ranks, p3):
+        r.phase4(p, init=True)
+    while True:
+        p1 = [r.phase1() for r in ranks]
+        allreduce(p1)
+        p2 = [r.phase2(a) for r, a in zip(ranks, p1)]
+        allreduce(p2)
+        p3 = [r.phase3(a) for r, a in zip(ranks, p2)]
+        allreduce(p3)
+        st = [r.phase4(a) for r, a in zip(ranks, p3)]
+        assert len(set(st)) == 1, f'ranks diverged: {st}'
+        if st[0] != 0:
+            return st[0]
+
+
+class HipFteRank:
+    """One rank of the distributed solve on a HIP context (payloads are torch device
+    tensors, so torch.distributed can reduce them in place)."""
+
+    def __init__(self, ctx, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutter_delay=True, intermode=1,
+                 opts=None, rank=0, world=1):
+        import torch
+        self.ctx = ctx
+        self.torch = torch
+        ints, reals, cams, meas, w, qinv, N, Cn = ctx._fte_args(table, cams, meas, w, Ts, qinv, shutter_delay,
+                                                                intermode)
+        self.N, self.P, self.C = N, table.P, Cn
+        X = _native._c64(X0).reshape(N + 2, table.P)
+        tau = np.zeros(Cn) if tau0 is None else _native._c64(tau0)
+        opts = opts or ctx.fte_default_opts()
+        h = C.c_void_p()
+        sizes = (C.c_int64 * 3)()
+        P_ = _native._ptr
+        ctx.check(ctx.lib.acs_fte_dist_create(ctx.h, P_(ints), len(ints), P_(reals), len(reals), P_(cams), Cn,
+                                              P_(meas), P_(w), N, int(bool(shutter_delay)), float(Ts), P_(qinv), 0,
+                                              int(intermode), P_(X), P_(tau), C.byref(opts), int(rank), int(world),
+                                              C.byref(h), sizes, 0), 'acs_fte_dist_create')
+        self.h = h
+        dev = torch.device('cuda', ctx.device)
+        self.p = [torch.zeros(int(n), dtype=torch.float64, device=dev) for n in sizes]
+
+    def _ptr(self, t):
+        return C.c_void_p(t.data_ptr())
+
+    def init(self):
+        self.ctx.check(self.ctx.lib.acs_fte_dist_init(self.h, self._ptr(self.p[2])), 'acs_fte_dist_init')
+        return self.p[2]
+
+    def phase1(self):
+        self.ctx.check(self.ctx.lib.acs_fte_dist_phase1(self.h, self._ptr(self.p[0])), 'acs_fte_dist_phase1')
+        return self.p[0]
+
+    def phase2(self, p1):
+        self.ctx.check(self.ctx.lib.acs_fte_dist_phase2(self.h, self._ptr(p1), self._ptr(self.p[1])),
+                       'acs_fte_dist_phase2')
+        return self.p[1]
+
+    def phase3(self, p2):
+        self.ctx.check(self.ctx.lib.acs_fte_dist_phase3(self.h, self._ptr(p2), self._ptr(self.p[2])),
+                       'acs_fte_dist_phase3')
+        return self.p[2]
+
+    def phase4(self, p3, init=False):
+        st = C.c_int32(0)
+        self.ctx.check(self.ctx.lib.acs_fte_dist_phase4(self.h, self._ptr(p3), int(bool(init)), C.byref(st)),
+                       'acs_fte_dist_phase4')
+        return st.value
+
+    def result(self):
+        X = np.empty((self.N + 2, self.P))
+        tau = np.empty(self.C)
+        rep = _native.FteReport()
+        self.ctx.check(self.ctx.lib.acs_fte_dist_result(self.h, _native._ptr(X), _native._ptr(tau), C.byref(rep), 0),
+                       'acs_fte_dist_result')
+        return X, tau, rep.as_dict()
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.ctx.lib.acs_fte_dist_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def torch_allreduce(group=None):
+    """All-reduce (sum) of this process's single payload over the process group."""
+    import torch.distributed as dist
+
+    def f(payloads):
+        assert len(payloads) == 1
+        dist.all_reduce(payloads[0], op=dist.ReduceOp.SUM, group=group)
+    return f
+
+
+def local_allreduce(payloads):
+    """Single-process emulation: sum in rank order, every rank receives the total (numpy
+    arrays or torch tensors)."""
+    tot = payloads[0] * 1
+    for p in payloads[1:]:
+        tot = tot + p
+    for p in payloads:
+        p[...] = tot
+
+
+class _on_torch_stream:
+    """Run the context's kernels and torch's collectives on one explicit stream."""
+
+    def __init__(self, ctx):
+        import torch
+        self.ctx, self.torch = ctx, torch
+        self.stream = torch.cuda.Stream(device=torch.device('cuda', ctx.device))
+
+    def __enter__(self):
+        self.cm = self.torch.cuda.stream(self.stream)
+        self.cm.__enter__()
+        self.ctx.set_stream(self.stream.cuda_stream)
+        return self
+
+    def __exit__(self, *exc):
+        self.stream.synchronize()
+        self.ctx.set_stream(0)
+        return self.cm.__exit__(*exc)
+
+
+def fte_solve_dist(ctx, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutter_delay=True, intermode=1, opts=None,
+                   group=None):
+    """Drop-in for Context.fte_solve under torch.distributed (one rank per GPU): returns
+    (X, tau, report), identical on every rank."""
+    import torch.distributed as tdist
+    rank, world = tdist.get_rank(group), tdist.get_world_size(group)
+    with _on_torch_stream(ctx):
+        r = HipFteRank(ctx, table, cams, meas, w, Ts, qinv, X0, tau0, shutter_delay, intermode, opts, rank, world)
+        try:
+            lm_loop([r], torch_allreduce(group))
+            return r.result()
+        finally:
+            r.close()
+
+
+def fte_solve_virtual(ctx, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutter_delay=True, intermode=1,
+                      opts=None, world=2):
+    """The distributed algorithm with `world` ranks emulated in one process on one device
+    (parity tests of the decomposition without a multi-GPU node)."""
+    with _on_torch_stream(ctx):
+        ranks = [HipFteRank(ctx, table, cams, meas, w, Ts, qinv, X0, tau0, shutter_delay, intermode, opts, r, world)
+                 for r in range(world)]
+        try:
+            lm_loop(ranks, local_allreduce)
+            outs = [r.result() for r in ranks]
+            for X, tau, _ in outs[1:]:
+                assert np.array_equal(X, outs[0][0]) and np.array_equal(tau, outs[0][1])
+            return outs[0]
+        finally:
+            for r in ranks:
+                r.close()

@@ -181,6 +181,34 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
                  const double* qinv, int32_t sd_mode, int32_t intermode, const double* X,
                  const double* tau, double* cost3, double* grad, double* H, uint32_t flags);
 
+/* ---- §8(e): frame-window distributed FTE (configs[3]) --------------------------------
+ * One handle per rank (rank of world); every rank gets the full-size inputs of
+ * acs_fte_solve and keeps the state replicated. The super-blocks of 3 frames are split
+ * into `world` chains that share their end blocks; a term belongs to the chain holding its
+ * lowest row. One LM iteration:
+ *   phase1(p1) -> all-reduce(p1, sum) -> phase2(p1, p2) -> all-reduce(p2, sum)
+ *   -> phase3(p2, p3) -> all-reduce(p3, sum) -> phase4(p3, 0, &status)
+ * starting with init(p3) -> all-reduce(p3) -> phase4(p3, 1, NULL). Payloads are DEVICE
+ * buffers of payload_sizes[0..2] doubles (p1: chain-end blocks of the reduced system,
+ * ~ (world+1) (2 BP^2 + BP GR) doubles; p2: the step, n_blocks x BP; p3: 2 costs). Every
+ * rank runs the same reduced solve on the summed p1 and takes the same decisions; the
+ * result equals acs_fte_solve up to summation order. Phases are asynchronous on the
+ * context stream except phase4, which returns the LM status (0 = running).            */
+typedef struct acs_fte_dist acs_fte_dist;
+int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
+                        int64_t n_reals, const double* cams, int32_t n_cams, const double* meas,
+                        const double* w, int32_t n_frames, int32_t shutter_delay, double Ts,
+                        const double* qinv, int32_t sd_mode, int32_t intermode, const double* X,
+                        const double* tau, const acs_fte_opts* opts, int32_t rank, int32_t world,
+                        acs_fte_dist** out, int64_t* payload_sizes, uint32_t flags);
+int acs_fte_dist_init(acs_fte_dist* h, double* p3);
+int acs_fte_dist_phase1(acs_fte_dist* h, double* p1);
+int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2);
+int acs_fte_dist_phase3(acs_fte_dist* h, const double* p2, double* p3);
+int acs_fte_dist_phase4(acs_fte_dist* h, const double* p3, int32_t init, int32_t* status);
+int acs_fte_dist_result(acs_fte_dist* h, double* X, double* tau, acs_fte_report* report, uint32_t flags);
+int acs_fte_dist_destroy(acs_fte_dist* h);
+
 /* ---- next: fisheye triangulation -------------------------------------
  * acs_triangulate_pairs: triangulate_points_fisheye (src/lib/calib.py:120-129) for n
  * (view a, view b) pairs; uv_a/uv_b (n, 2) pixels, cam_a/cam_b (n) camera ids, out (n, 3).

@@ -104,16 +104,26 @@ class Problem:
                                fte_form=True).reshape(self.N, self.L, 2)
         return self.w[..., None] * (uv - self.meas)                    # e (N, C, L, 2)
 
-    def cost(self, X, tau):
+    def cost(self, X, tau, frames=None, stencils=None):
+        """(total, measurement, model). `frames` (N,) / `stencils` (N-1,) boolean masks keep
+        only those terms (the terms one rank owns in oracle/fte_dist.py)."""
         e = self.residuals(X, tau)
-        meas = okin.redescending_loss(e, self.a, self.b, self.c).sum()
+        rho = okin.redescending_loss(e, self.a, self.b, self.c)
+        if frames is not None:
+            rho = rho * np.asarray(frames, bool)[:, None, None, None]
+        meas = rho.sum()
         s = self.model_slack(X)
-        model = (s * s * self.qinv).sum()
+        q = s * s * self.qinv
+        if stencils is not None:
+            q = q * np.asarray(stencils, bool)[:, None]
+        model = q.sum()
         return meas + model, meas, model
 
     # ---- linearisation ----------------------------------------------------------------
-    def linearize(self, X, tau):
+    def linearize(self, X, tau, frames=None, stencils=None):
+        """(cost, H, g) of the GN model; with masks, of the owned terms only (see cost)."""
         N, C, L, P, M, Ts = self.N, self.C, self.L, self.P, self.M, self.Ts
+        fm = np.ones(N) if frames is None else np.asarray(frames, bool).astype(np.float64)
         x, dx, ddx = self.derivs(X)
         pos = okin.marker_positions(self.mode, x)                      # (N, L, 3)
         Jfk = okin.marker_jacobian(self.mode, x)                       # (N, L, 3, P)
@@ -130,8 +140,8 @@ class Problem:
             e = self.w[:, c, :, None] * (uv - self.meas[:, c])          # (N, L, 2)
             rho = okin.redescending_loss(e, self.a, self.b, self.c)
             d1, d2 = okin.loss_derivs(e, self.a, self.b, self.c)
-            F_meas += rho.sum()
-            wl = self.w[:, c, :, None]                                   # (N, L, 1)
+            F_meas += (rho * fm[:, None, None]).sum()
+            wl = self.w[:, c, :, None] * fm[:, None, None]               # (N, L, 1)
             sq = np.sqrt(curvature(e, d1, d2)) * wl                      # scale of J rows
             gs = d1 * wl                                                 # scale of gradient rows
             # d proj / d x_k (own frame)
@@ -186,10 +196,11 @@ class Problem:
             mvals.append(np.full(nm * P, ci))
         Dm = sp.csr_matrix((np.concatenate(mvals), (np.concatenate(mrows), np.concatenate(mcols))),
                            shape=(nm * P, self.nv))
-        qd = sp.diags(np.tile(self.qinv, nm))
+        sm = np.ones(nm) if stencils is None else np.asarray(stencils, bool).astype(np.float64)
+        qd = sp.diags(np.tile(self.qinv, nm) * np.repeat(sm, P))
         H = H + 2.0 * (Dm.T @ qd @ Dm)
         grad += 2.0 * (Dm.T @ (qd @ s.ravel()))
-        F_model = float((s * s * self.qinv).sum())
+        F_model = float((s * s * self.qinv * sm[:, None]).sum())
         return F_meas + F_model, H.tocsr(), grad
 
     def pack(self, X, tau):

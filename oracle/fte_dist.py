@@ -1,0 +1,183 @@
+"""Oracle: the frame-window decomposition of the FTE Levenberg-Marquardt step.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Spec of the distributed solve in acinoset_amd/csrc/fte.hip (acs_fte_dist_*, SURVEY.md
+§8(e)), restated densely with numpy so the CPU tests can run the product's protocol
+(acinoset_amd.dist.lm_loop) over torch.distributed/gloo and compare it with the
+monolithic oracle (oracle/fte.py solve):
+
+* super-blocks of 3 X rows (n = ceil((N+2)/3)); rank r's chain = blocks [r 2^k, (r+1) 2^k]
+  with the smallest k >= 1 such that R 2^k >= n - 1; adjacent chains share an end block;
+* a term (measurement of frame k: rows k..k+2; model stencil i: rows i..i+3) is owned by
+  the rank whose chain holds its lowest row in [3 a_r, 3 (a_r + 2^k)) (the last rank: all
+  rows from 3 a_r on), so the rank matrices sum to the full normal matrix;
+* each rank eliminates its chain interior (damped: lam * max(diag, 1e-12)) and
+  contributes the Schur complement on (chain-end rows, tau), their raw diagonals and
+  gradients, and max |g| over its interior rows to payload 1 (a sum over ranks);
+* the summed reduced system is damped with the summed raw diagonals, tau_0 pinned, and
+  solved identically on every rank; interiors are back-substituted; payload 2 = the step
+  rows each rank publishes (blocks [a_r, a_r + 2^k), the last rank also its end);
+* payload 3 = the owned terms' (measurement, model) cost at the trial state; the
+  accept/reject rule is oracle/fte.py solve's.
+
+The payload layouts are this module's own (dense); only their sums cross ranks.
+"""
+import numpy as np
+
+from .fte import Problem  # noqa: F401  (type of `prob`)
+
+
+def chains(nblk, world):
+    k = 1
+    while world * (1 << k) < nblk - 1:
+        k += 1
+    return 1 << k
+
+
+class OracleFteRank:
+    def __init__(self, prob, X0, tau0=None, rank=0, world=1, max_iters=200, ftol=1e-12, xtol=1e-12, gtol=1e-8,
+                 lam0=1e-3):
+        self.prob = p = prob
+        self.rank, self.world = rank, world
+        self.opts = dict(max_iters=max_iters, ftol=ftol, xtol=xtol, gtol=gtol)
+        self.X = np.array(X0, np.float64).reshape(p.M, p.P)
+        self.tau = np.zeros(p.C) if tau0 is None else np.array(tau0, np.float64)
+        self.tau[0] = 0.0
+        self.lam, self.status, self.iters, self.nacc, self.relin = lam0, 0, 0, 0, True
+        M, P = p.M, p.P
+        nblk = (M + 2) // 3
+        span = chains(nblk, world)
+        a0, bend = rank * span, (rank + 1) * span
+        self.lo = 3 * a0
+        self.hi = 3 * bend if rank < world - 1 else 1 << 40  # the last rank owns the tail
+        rows = lambda b0, b1: [f for f in range(3 * b0, 3 * b1) if f < M]  # noqa: E731
+        var = lambda fs: np.array([f * P + q for f in fs for q in range(P)], np.int64)  # noqa: E731
+        self.I = var(rows(a0 + 1, min(bend, nblk)))                      # interior unknowns
+        ends = sorted(set(rows(a0, a0 + 1)) | set(rows(bend, bend + 1)))
+        self.ntau = p.C if p.sd else 0
+        tau_idx = np.arange(self.ntau) + M * P
+        self.B = np.concatenate([var(ends), tau_idx]).astype(np.int64)  # border unknowns
+        # global reduced index space: rows of every chain end e_q = q span (q = 0..R) + tau
+        all_ends = [f for q in range(world + 1) for f in rows(q * span, q * span + 1)]
+        self.S = np.concatenate([var(all_ends), tau_idx]).astype(np.int64)
+        self.pos = {v: i for i, v in enumerate(self.S)}
+        self.Bpos = np.array([self.pos[v] for v in self.B], np.int64)
+        self.frames = (np.arange(p.N) >= self.lo) & (np.arange(p.N) < self.hi)
+        self.stencils = (np.arange(p.N - 1) >= self.lo) & (np.arange(p.N - 1) < self.hi)
+        out_hi = bend + 1 if rank == world - 1 else bend
+        self.out = var(rows(a0, min(out_hi, nblk)))
+        nS = len(self.S)
+        self.n1 = nS * nS + 3 * nS + world
+        self.n2 = M * P
+        self.n3 = 2
+
+    # ---- protocol ----------------------------------------------------------------------
+    def init(self):
+        _, fm, fq = self.prob.cost(self.X, self.tau, self.frames, self.stencils)
+        return np.array([fm, fq])
+
+    def phase1(self):
+        p = self.prob
+        if self.relin:
+            _, H, g = p.linearize(self.X, self.tau, self.frames, self.stencils)
+            self.H, self.g = H.toarray(), g
+        H, g, I, B, lam = self.H, self.g, self.I, self.B, self.lam
+        HII = H[np.ix_(I, I)].copy()
+        HII[np.diag_indices_from(HII)] += lam * np.maximum(np.diag(HII), 1e-12)
+        HIB, HBB = H[np.ix_(I, B)], H[np.ix_(B, B)]
+        self.HII, self.HIB = HII, HIB
+        if len(I):
+            Z = np.linalg.solve(HII, np.concatenate([HIB, -g[I][:, None]], 1))
+            Sb = HBB - HIB.T @ Z[:, :-1]
+            rb = -g[B] - HIB.T @ Z[:, -1]
+        else:
+            Sb, rb = HBB, -g[B]
+        nS = len(self.S)
+        out = np.zeros(self.n1)
+        S = np.zeros((nS, nS))
+        S[np.ix_(self.Bpos, self.Bpos)] = Sb
+        out[:nS * nS] = S.ravel()
+        out[nS * nS + self.Bpos] = rb
+        out[nS * nS + nS + self.Bpos] = np.diag(HBB)
+        out[nS * nS + 2 * nS + self.Bpos] = g[B]
+        out[nS * nS + 3 * nS + self.rank] = np.abs(g[I]).max() if len(I) else 0.0
+        return out
+
+    def phase2(self, p1):
+        p, lam = self.prob, self.lam
+        nS = len(self.S)
+        S = p1[:nS * nS].reshape(nS, nS).copy()
+        rhs = p1[nS * nS:nS * nS + nS].copy()
+        rdiag = p1[nS * nS + nS:nS * nS + 2 * nS]
+        graw = p1[nS * nS + 2 * nS:nS * nS + 3 * nS].copy()
+        S[np.diag_indices_from(S)] += lam * np.maximum(rdiag, 1e-12)
+        if self.ntau:
+            t0 = nS - self.ntau                       # tau_0 pinned (src/core/fte.py:304-318)
+            S[t0, :] = 0.0
+            S[:, t0] = 0.0
+            S[t0, t0] = 1.0
+            rhs[t0] = 0.0
+            graw[t0] = 0.0
+        self.gmax = max(np.abs(graw).max(), p1[nS * nS + 3 * nS:].max())
+        dS = np.linalg.solve(S, rhs)
+        d = np.zeros(p.nv)
+        d[self.S] = dS
+        if len(self.I):
+            d[self.I] = np.linalg.solve(self.HII, -self.g[self.I] - self.HIB @ dS[self.Bpos])
+        self.dtau = dS[nS - self.ntau:] if self.ntau else np.zeros(0)
+        out = np.zeros(self.n2)
+        out[self.out] = d[self.out]
+        return out
+
+    def phase3(self, p2):
+        p = self.prob
+        dX = p2.reshape(p.M, p.P)
+        self.Xn = self.X + dX
+        if p.sd:
+            self.taun = np.clip(self.tau + self.dtau, -p.Ts, p.Ts)
+            self.taun[0] = 0.0
+        else:
+            self.taun = self.tau
+        d = np.concatenate([p2, self.dtau])
+        self.dn = np.linalg.norm(d)
+        self.xn = np.linalg.norm(p.pack(self.X, self.tau))
+        _, fm, fq = p.cost(self.Xn, self.taun, self.frames, self.stencils)
+        return np.array([fm, fq])
+
+    def phase4(self, p3, init=False):
+        o = self.opts
+        Fn = float(p3[0] + p3[1])
+        if init:
+            self.F = self.F0 = Fn
+            return 0
+        if self.status:
+            return self.status
+        if self.gmax <= o['gtol']:
+            self.status = 1
+            return self.status
+        self.iters += 1
+        small = self.dn <= o['xtol'] * (o['xtol'] + self.xn)
+        if Fn < self.F:
+            fconv = (self.F - Fn) <= o['ftol'] * abs(self.F)
+            self.nacc += 1
+            self.F = Fn
+            self.X, self.tau = self.Xn, self.taun
+            self.lam = max(self.lam * 0.1, 1e-15)
+            self.relin = True
+            if fconv:
+                self.status = 2
+            elif small:
+                self.status = 3
+        else:
+            self.lam *= 10.0
+            self.relin = False
+            if self.lam > 1e16:
+                self.status = 4
+        if self.status == 0 and self.iters >= o['max_iters']:
+            self.status = 5
+        return self.status
+
+    def result(self):
+        return self.X, self.tau, dict(status=self.status, iters=self.iters, n_accepted=self.nacc, cost_before=self.F0,
+                                      cost_after=self.F, lam=self.lam)

@@ -1,0 +1,96 @@
+"""GPU parity of the frame-window distributed FTE solve (acs_fte_dist_*).
+
+* `fte_solve_virtual`: W ranks emulated in one process on one GPU (payload sums in rank
+  order) must reproduce the single-GPU acs_fte_solve iterate for iterate: same iteration
+  count and status, X within 1e-9, tau within 1e-12 s, cost 1e-11 relative (the
+  decomposition only reorders sums).
+* one LM step of the distributed HIP path against the oracle restatement of the same
+  decomposition (oracle/fte_dist.py): 1e-9.
+* world_size 2 through torch.distributed (gloo on the device tensors; the multi-GPU run
+  uses the same calls over RCCL): two processes on the one GPU reach the same result.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import fte as ofte, fte_dist as odist
+from acinoset_amd import _native, dist, kinematics as pkin, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(N, mode='default_nolure', sd=True, inter='vel', seed=2):
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(N, scene, mode=mode, seed=seed, tau_max=0.004 if sd else 0.0)
+    w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
+    prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter)
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    X0 = ofte.initial_state(prob, np.arange(N), seq.pos3d[:, 0, 0])
+    return prob, cams, X0
+
+
+@pytest.mark.parametrize('mode,N,sd,inter', [('default_nolure', 40, True, 'vel'), ('head', 61, True, 'acc'),
+                                             ('default_nolure', 31, False, 'pos')])
+@pytest.mark.parametrize('world', [2, 3, 8])
+def test_fte_dist_virtual_matches_single(ctx, mode, N, sd, inter, world):
+    prob, cams, X0 = _problem(N, mode, sd, inter)
+    table = pkin.build_table(mode)
+    X1, t1, r1 = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, shutter_delay=sd,
+                               intermode=prob.im)
+    Xd, td, rd = dist.fte_solve_virtual(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
+                                        shutter_delay=sd, intermode=prob.im, world=world)
+    assert rd['iters'] == r1['iters'] and rd['n_accepted'] == r1['n_accepted'], (rd, r1)
+    assert rd['status'] == r1['status'] and rd['n_bad_pivots'] == 0
+    assert abs(rd['cost_after'] - r1['cost_after']) <= 1e-11 * r1['cost_after']
+    np.testing.assert_allclose(Xd, X1, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(td, t1, rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize('world', [2, 5])
+def test_fte_dist_one_step_matches_oracle_decomposition(ctx, world):
+    prob, cams, X0 = _problem(40)
+    table = pkin.build_table(prob.mode)
+    Xd, td, rd = dist.fte_solve_virtual(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
+                                        opts=ctx.fte_default_opts(max_iters=1), world=world)
+    ranks = [odist.OracleFteRank(prob, X0, None, r, world, max_iters=1) for r in range(world)]
+    dist.lm_loop(ranks, dist.local_allreduce)
+    Xo, to, io = ranks[0].result()
+    assert rd['n_accepted'] == io['n_accepted'] == 1
+    np.testing.assert_allclose(Xd, Xo, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(td, to, rtol=0, atol=1e-12)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as tdist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        ctx = _native.Context(0)
+        prob, cams, X0 = _problem(40)
+        table = pkin.build_table(prob.mode)
+        X, tau, rep = dist.fte_solve_dist(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0)
+        np.savez(os.path.join(out_dir, f'rank{rank}.npz'), X=X, tau=tau, iters=rep['iters'])
+        del torch
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_fte_dist_two_processes(ctx, tmp_path):
+    import torch.multiprocessing as mp
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method='spawn')
+    prob, cams, X0 = _problem(40)
+    table = pkin.build_table(prob.mode)
+    X1, t1, r1 = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0)
+    a, b = (np.load(tmp_path / f'rank{r}.npz') for r in range(2))
+    assert np.array_equal(a['X'], b['X']) and np.array_equal(a['tau'], b['tau'])
+    assert int(a['iters']) == r1['iters']
+    np.testing.assert_allclose(a['X'], X1, rtol=0, atol=1e-9)
