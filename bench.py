@@ -37,6 +37,10 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--fte', action='store_true', default=True, help='also time the FTE solve (configs[2])')
     ap.add_argument('--no-fte', dest='fte', action='store_false')
+    ap.add_argument('--window-frames', type=int, default=10000,
+                    help='configs[3]: FTE over this many frames, frame windows sharded over the ranks (0 = skip)')
+    ap.add_argument('--exchange', default='nccl', choices=('nccl', 'gloo'),
+                    help='backend of the FTE window all-reduces (nccl = RCCL over xGMI)')
     ap.add_argument('--scale-frames', type=int, default=20000,
                     help='also time SBA at configs[4] scale on one GPU (0 = skip)')
     ap.add_argument('--scale-cams', type=int, default=12)
@@ -57,6 +61,9 @@ def main():
         # control plane only (barrier + max of the timed interval); the SBA data path
         # has no collective. gloo keeps RCCL out of a path that does not need it.
         dist.init_process_group('gloo')
+    # one GPU per rank; wrapping onto fewer devices only happens in a rehearsal on a
+    # single-GPU box (torchrun --nproc-per-node 2 ... --exchange gloo)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     ctx = _native.Context(local)
     # one explicit (non-null) stream carries the copies, the kernels and the timing events
@@ -150,6 +157,8 @@ def main():
 
     if args.fte and world == 1:
         out['fte'] = bench_fte(ctx, torch, stream, n_frames=args.fte_frames)
+    if args.window_frames > 0:
+        out['fte_window'] = bench_fte_window(ctx, torch, stream, args.window_frames, world, rank, args.exchange)
     if args.scale_frames > 0 and world == 1:
         out['sba_at_scale'] = bench_sba_scale(ctx, torch, stream, args.scale_frames, args.scale_cams)
 
@@ -261,6 +270,71 @@ def bench_sba_scale(ctx, torch, stream, n_frames=20000, n_cams=12, steps=10):
             'roofline_fp64': fp64,
             'iters_max': rep['iters_max'], 'gn_steps_mean': rep['iters_sum'] / max(1, rep['n_problems']),
             'status': rep['status_counts'], 'pos_rms_vs_truth_m': pos_rms}
+
+
+def _fte_problem(ctx, n_frames, seed=77):
+    """Synthetic FTE input (6 cams, 20 kp, default_nolure) initialised as core.fte does:
+    GPU pairwise triangulation of the nose + line fit (src/core/fte.py:254-292)."""
+    import importlib
+    import pandas as pd
+    from acinoset_amd import _native, synth
+    from acinoset_amd.kinematics import build_table
+    cfte = importlib.import_module('acinoset_amd.core.fte')
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(n_frames, scene, mode='default_nolure', seed=seed, tau_max=0.004)
+    w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
+    meas = np.nan_to_num(seq.uv)
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    N = seq.uv.shape[0]
+    valid = (seq.likelihood > 0.5) & np.isfinite(seq.uv).all(-1)
+    xyz, cnt = ctx.triangulate_dense(cams, seq.uv[:, :, 0], valid[:, :, 0])
+    ok = cnt > 0
+    nose_df = pd.DataFrame({'frame': np.arange(N)[ok], 'marker': 'nose', 'x': xyz[ok, 0], 'y': xyz[ok, 1],
+                            'z': xyz[ok, 2]})
+    X0 = cfte.initial_state(nose_df, 'default_nolure', 0, N - 1)
+    return seq, cams, meas, w, X0, build_table('default_nolure'), cfte.model_weights('default_nolure')
+
+
+def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl', steps=3):
+    """configs[3]: one FTE trajectory of `n_frames` frames; with W ranks its super-blocks
+    are split into W frame windows (acinoset_amd.dist, three all-reduces per LM step over
+    RCCL). Strong scaling: the total work is fixed. W = 1 runs acs_fte_solve."""
+    import torch.distributed as tdist
+    from acinoset_amd import dist as adist
+    seq, cams, meas, w, X0, table, qinv = _fte_problem(ctx, n_frames)
+    group = tdist.new_group(backend=exchange) if world > 1 else None
+
+    def run():
+        if world == 1:
+            return ctx.fte_solve(table, cams, meas, w, seq.Ts, qinv, X0)
+        r = adist.HipFteRank(ctx, table, cams, meas, w, seq.Ts, qinv, X0, rank=rank, world=world)
+        try:
+            adist.lm_loop([r], adist.torch_allreduce(group))
+            return r.result()
+        finally:
+            r.close()
+    X, tau, rep = run()                                             # warm-up + result
+    pos = ctx.fk(table, X[2:])
+    pos_rms = float(np.sqrt(np.mean(np.sum((pos - seq.pos3d[:, 0]) ** 2, -1))))
+    if world > 1:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    dt = (time.perf_counter() - t0) / steps
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    return {'workload': f'fte C=6 frames={n_frames} L=20 P={table.P} sd=const intermode=vel (configs[3])',
+            'ranks': world, 'scaling': 'strong', 'frames_per_s': n_frames / dt, 'ms_per_solve': dt * 1e3,
+            'status': rep['status_name'], 'iters': rep['iters'], 'cost_after': rep['cost_after'],
+            'pos_rms_vs_truth_m': pos_rms, 'tau_err_max_s': float(np.abs(tau - seq.tau).max()),
+            'exchange': 'none' if world == 1 else f'torch.distributed {exchange} all-reduce x3 per LM step'}
 
 
 def bench_fte(ctx, torch, stream, n_frames=1000, steps=5):
