@@ -223,8 +223,11 @@ __global__ __launch_bounds__(256) void k_ext_schur(ExtDims d, const ExtState* __
 
 __global__ __launch_bounds__(256) void k_ext_solve(ExtDims d, ExtState* __restrict__ st, int nchunk,
                                                    const double* __restrict__ part, const double* __restrict__ Vg,
+                                                   int n_gp, const double* __restrict__ slots, int n_slots,
                                                    double* __restrict__ dc, double* __restrict__ Sg,
                                                    int* __restrict__ bad) {
+  // part: nchunk partials of [S | b | diag U | g_c]; the point-gradient max comes from
+  // Vg (n_gp points) and/or per-rank slots (distributed: points live on their ranks)
   if (st->status != 0) return;
   const int NC = 6 * d.C, NP = ((NC + 15) / 16) * 16, nE = NC * NC + 3 * NC, LD = NP + 1;
   const double lam = st->lam;
@@ -260,8 +263,9 @@ __global__ __launch_bounds__(256) void k_ext_solve(ExtDims d, ExtState* __restri
     sb[r] = v;
     gm = fmax(gm, fabs(g));
   }
-  for (int p = threadIdx.x; p < d.n; p += blockDim.x)
+  for (int p = threadIdx.x; p < n_gp; p += blockDim.x)
     for (int j = 0; j < 3; ++j) gm = fmax(gm, fabs(Vg[(size_t)p * 10 + 6 + j]));
+  for (int t = threadIdx.x; t < n_slots; t += blockDim.x) gm = fmax(gm, slots[t]);
   __syncthreads();
   {  // block max
     s_red[threadIdx.x] = gm;
@@ -479,7 +483,8 @@ static void ext_enqueue(hipStream_t s, const ExtDims& d, ExtState* st, const Ext
   const size_t lds_solve = sizeof(double) * ((size_t)NP * (NP + 1) + NP + 512 + 256);
   hipLaunchKernelGGL((k_ext_linearize<G>), dim3(blocks), dim3(256), 0, s, d, st, cams, pts, uv, mk, cid, Q, Vg, Fp);
   hipLaunchKernelGGL(k_ext_schur, dim3(nchunk), dim3(256), lds, s, d, st, Q, Vg, mk, cid, part);
-  hipLaunchKernelGGL(k_ext_solve, dim3(1), dim3(256), lds_solve, s, d, st, nchunk, part, Vg, dc, Sg, bad);
+  hipLaunchKernelGGL(k_ext_solve, dim3(1), dim3(256), lds_solve, s, d, st, nchunk, part, Vg, d.n, nullptr, 0, dc, Sg,
+                     bad);
   hipLaunchKernelGGL(k_ext_back, dim3(acs_grid(d.n, 256)), dim3(256), 0, s, d, st, Q, Vg, mk, cid, dc, pts, normp);
   hipLaunchKernelGGL(k_ext_cam, dim3(1), dim3(64), 0, s, d, st, dc, cams, camnorm);
   hipLaunchKernelGGL((k_ext_cost<G>), dim3(blocks), dim3(256), 0, s, d, st, 1, cams, pts, uv, mk, cid, Fp);
@@ -635,6 +640,331 @@ int acs_sba_extrinsics(acs_ctx* ctx, double* cams, int32_t n_cams, const double*
   ACS_HIP(ctx, hipMemcpyAsync(pts, fpts, sizeof(double) * 3 * n_pts, kout, s));
   int nbad = 0;
   ACS_HIP(ctx, hipMemcpyAsync(&nbad, bad, sizeof(int), hipMemcpyDeviceToHost, s));
+  ACS_HIP(ctx, hipStreamSynchronize(s));
+  if (report) {
+    report->status = hs.status == 0 ? ACS_STATUS_MAXITER : hs.status;
+    report->iters = hs.iters;
+    report->n_accepted = hs.nacc;
+    report->n_bad_pivots = nbad;
+    report->cost_before = hs.F0;
+    report->cost_after = hs.F;
+    report->grad_max = hs.gmax;
+    report->lambda_final = hs.lam;
+  }
+  return ACS_OK;
+}
+
+}  // extern "C"
+
+// =======================================================================================
+// distributed points + extrinsics: points are split over the ranks,
+// cameras replicated. Per LM step one all-reduce of the reduced camera system (p1 =
+// [S | b | diag U | g_c | per-rank point |g| max]) and one of 3 doubles (cost, point
+// step norms). Every rank solves the same camera system and takes the same decision.
+// Spec: oracle/sba_ext_dist.py.
+// =======================================================================================
+__global__ __launch_bounds__(256) void k_ext_pack1(ExtDims d, const ExtState* __restrict__ st, int nchunk,
+                                                   const double* __restrict__ part, const double* __restrict__ Vg,
+                                                   int rank, double* __restrict__ p1) {
+  if (st->status != 0) return;
+  __shared__ double s_red[256];
+  const int NC = 6 * d.C, nE = NC * NC + 3 * NC;
+  for (int e = threadIdx.x; e < nE; e += blockDim.x) {
+    double v = 0.0;
+    for (int ch = 0; ch < nchunk; ++ch) v += part[(size_t)ch * nE + e];
+    p1[e] = v;
+  }
+  double gm = 0.0;
+  for (int p = threadIdx.x; p < d.n; p += blockDim.x)
+    for (int j = 0; j < 3; ++j) gm = fmax(gm, fabs(Vg[(size_t)p * 10 + 6 + j]));
+  s_red[threadIdx.x] = gm;
+  __syncthreads();
+  for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+    if (threadIdx.x < h) s_red[threadIdx.x] = fmax(s_red[threadIdx.x], s_red[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) p1[nE + rank] = s_red[0];
+}
+
+__global__ __launch_bounds__(256) void k_ext_pack3(ExtDims d, const ExtState* __restrict__ st, int which,
+                                                   const double* __restrict__ Fp, const double* __restrict__ normp,
+                                                   double* __restrict__ p3) {
+  if (which == 1 && st->status != 0) return;
+  __shared__ double s_red[3][256];
+  double a = 0.0, b = 0.0, c = 0.0;
+  for (int p = threadIdx.x; p < d.n; p += blockDim.x) {
+    a += Fp[p];
+    if (which) {
+      b += normp[2 * p];
+      c += normp[2 * p + 1];
+    }
+  }
+  s_red[0][threadIdx.x] = a;
+  s_red[1][threadIdx.x] = b;
+  s_red[2][threadIdx.x] = c;
+  __syncthreads();
+  for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+    if (threadIdx.x < h)
+      for (int k = 0; k < 3; ++k) s_red[k][threadIdx.x] += s_red[k][threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 3; ++k) p3[k] = s_red[k][0];
+}
+
+__global__ void k_ext_lm_dist(ExtDims d, ExtState* __restrict__ st, ExtOpts o, int init,
+                              const double* __restrict__ p3, const double* __restrict__ camnorm) {
+  if (threadIdx.x != 0) return;
+  const double f = p3[0];
+  if (init) {
+    st->F = st->F0 = f;
+    return;
+  }
+  if (st->status != 0) return;
+  double dn = p3[1], xn = p3[2];
+  for (int c = 0; c < d.C; ++c) {
+    dn += camnorm[2 * c];
+    xn += camnorm[2 * c + 1];
+  }
+  if (st->gmax <= o.gtol) {
+    st->status = ACS_STATUS_GTOL;
+    return;
+  }
+  st->iters += 1;
+  st->dnorm = sqrt(dn);
+  st->xnorm = sqrt(xn);
+  const bool small = sqrt(dn) <= o.xtol * (o.xtol + sqrt(xn));
+  if (f < st->F) {
+    const bool fconv = (st->F - f) <= o.ftol * fabs(st->F);
+    st->nacc += 1;
+    st->F = f;
+    st->cur ^= 1;
+    st->lam = fmax(st->lam * 0.1, EXT_LAM_MIN);
+    st->relin = 1;
+    if (fconv)
+      st->status = ACS_STATUS_FTOL;
+    else if (small)
+      st->status = ACS_STATUS_XTOL;
+  } else {
+    st->lam *= 10.0;
+    st->relin = 0;
+    if (st->lam > 1e16) st->status = ACS_STATUS_STALLED;
+  }
+  if (st->status == 0 && st->iters >= o.max_iters) st->status = ACS_STATUS_MAXITER;
+}
+
+struct acs_sba_ext_dist {
+  acs_ctx* ctx;
+  void* own = nullptr;
+  ExtDims d;
+  ExtOpts o;
+  int R, rank, nchunk;
+  double *dcams, *dpts, *Q, *Vg, *Fp, *part, *dc, *Sg, *normp, *camnorm;
+  double2* uvp;
+  uint8_t *mk, *cid;
+  ExtState* st;
+  int* bad;
+};
+
+template <int G>
+static void ext_dist_linearize(acs_sba_ext_dist* h, hipStream_t s) {
+  const ExtDims& d = h->d;
+  const int blocks = acs_grid((int64_t)d.n * G, 256);
+  hipLaunchKernelGGL((k_ext_linearize<G>), dim3(blocks), dim3(256), 0, s, d, h->st, h->dcams, h->dpts, h->uvp, h->mk,
+                     h->cid, h->Q, h->Vg, h->Fp);
+}
+
+template <int G>
+static void ext_dist_cost(acs_sba_ext_dist* h, hipStream_t s, int which) {
+  const ExtDims& d = h->d;
+  const int blocks = acs_grid((int64_t)d.n * G, 256);
+  hipLaunchKernelGGL((k_ext_cost<G>), dim3(blocks), dim3(256), 0, s, d, h->st, which, h->dcams, h->dpts, h->uvp,
+                     h->mk, h->cid, h->Fp);
+}
+
+#define EXT_G_SWITCH(G, CALL)                  \
+  switch (G) {                                 \
+    case 2: CALL(2); break;                    \
+    case 4: CALL(4); break;                    \
+    case 8: CALL(8); break;                    \
+    case 16: CALL(16); break;                  \
+    case 32: CALL(32); break;                  \
+    default: CALL(64); break;                  \
+  }
+
+extern "C" {
+
+int acs_sba_ext_dist_create(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
+                            const int32_t* pt_idx, const int32_t* cam_idx, int64_t n_obs, const double* pts,
+                            int64_t n_pts, const acs_sba_ext_opts* opts, int32_t rank, int32_t world,
+                            acs_sba_ext_dist** out, int64_t* payload_sizes, uint32_t flags) {
+  acs_sba_ext_opts op;
+  acs_sba_ext_default_opts(&op);
+  if (opts) op = *opts;
+  ACS_CHECK(ctx, n_cams >= 1 && n_cams <= EXT_MAXC, "sba_ext_dist: n_cams=%d (1..%d)", n_cams, EXT_MAXC);
+  ACS_CHECK(ctx, n_obs >= 1 && n_pts >= 1 && n_obs < (int64_t)INT32_MAX, "sba_ext_dist: bad sizes");
+  ACS_CHECK(ctx, op.f_scale > 0 && op.max_iters >= 0, "sba_ext_dist: bad options");
+  ACS_CHECK(ctx, world >= 1 && rank >= 0 && rank < world, "sba_ext_dist: rank %d / world %d", rank, world);
+  hipStream_t s = ctx->stream;
+  void *dcam0, *duv, *dpi, *dci, *dp0;
+  int rc;
+  if ((rc = acs_stage_in(ctx, WS_CAMS, cams, sizeof(double) * ACS_CAM_STRIDE * n_cams, flags, &dcam0))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_UV, uv, sizeof(double) * 2 * n_obs, flags, &duv))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_PTIDX, pt_idx, sizeof(int32_t) * n_obs, flags, &dpi))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_CAMIDX, cam_idx, sizeof(int32_t) * n_obs, flags, &dci))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_PTS, pts, sizeof(double) * 3 * n_pts, flags, &dp0))) return rc;
+  double2* uvp;
+  uint8_t *mk, *cid;
+  int K;
+  if ((rc = acs_obs_to_slots(ctx, (const double*)duv, (const int32_t*)dpi, (const int32_t*)dci, n_obs, n_pts, n_cams,
+                             &uvp, &mk, &cid, &K)))
+    return rc;
+  ACS_CHECK(ctx, K <= 64, "sba_ext_dist: a point has %d observations (max 64)", K);
+  acs_sba_ext_dist* h = new acs_sba_ext_dist();
+  h->ctx = ctx;
+  ExtDims& d = h->d;
+  d = ExtDims{(int)n_pts, K, n_cams, 2, EXT_CHUNK, op.f_scale * op.f_scale};
+  while (d.G < K) d.G <<= 1;
+  d.chunk = std::max(1, std::min(EXT_CHUNK, (int)(96 * 1024 / (148 * K + 24))));
+  h->nchunk = (int)((n_pts + d.chunk - 1) / d.chunk);
+  h->R = world;
+  h->rank = rank;
+  h->o = ExtOpts{op.max_iters, op.ftol, op.xtol, op.gtol};
+  const int NC = 6 * n_cams, nE = NC * NC + 3 * NC;
+  size_t off = 0;
+  auto take = [&](size_t cnt) {
+    size_t o = off;
+    off += ((cnt * sizeof(double) + 255) / 256) * 256 / sizeof(double);
+    return o;
+  };
+  const size_t oC = take(2 * (size_t)n_cams * ACS_CAM_STRIDE), oP = take(6 * (size_t)n_pts),
+               oQ = take((size_t)n_pts * K * EXT_Q), oV = take((size_t)n_pts * 10), oF = take(n_pts),
+               oPart = take((size_t)h->nchunk * nE), odc = take(96), oSg = take(96 * 96), onp = take(2 * (size_t)n_pts),
+               ocn = take(64), ost = take(16), obad = take(2), ouv = take(2 * (size_t)n_pts * K),
+               omk = take(((size_t)n_pts * K + 7) / 8), ocid = take(((size_t)n_pts * K + 7) / 8);
+  if (hipMalloc(&h->own, off * sizeof(double)) != hipSuccess) {
+    delete h;
+    return acs_fail(ctx, ACS_E_NOMEM, "sba_ext_dist: allocation failed");
+  }
+  double* a = (double*)h->own;
+  h->dcams = a + oC;
+  h->dpts = a + oP;
+  h->Q = a + oQ;
+  h->Vg = a + oV;
+  h->Fp = a + oF;
+  h->part = a + oPart;
+  h->dc = a + odc;
+  h->Sg = a + oSg;
+  h->normp = a + onp;
+  h->camnorm = a + ocn;
+  h->st = (ExtState*)(a + ost);
+  h->bad = (int*)(a + obad);
+  h->uvp = (double2*)(a + ouv);
+  h->mk = (uint8_t*)(a + omk);
+  h->cid = (uint8_t*)(a + ocid);
+  ACS_HIP(ctx, hipMemcpyAsync(h->uvp, uvp, sizeof(double2) * n_pts * K, hipMemcpyDeviceToDevice, s));
+  ACS_HIP(ctx, hipMemcpyAsync(h->mk, mk, (size_t)n_pts * K, hipMemcpyDeviceToDevice, s));
+  ACS_HIP(ctx, hipMemcpyAsync(h->cid, cid, (size_t)n_pts * K, hipMemcpyDeviceToDevice, s));
+  for (int b = 0; b < 2; ++b)
+    ACS_HIP(ctx, hipMemcpyAsync(h->dcams + b * n_cams * ACS_CAM_STRIDE, dcam0, sizeof(double) * ACS_CAM_STRIDE * n_cams,
+                                hipMemcpyDeviceToDevice, s));
+  ACS_HIP(ctx, hipMemcpyAsync(h->dpts, dp0, sizeof(double) * 3 * n_pts, hipMemcpyDeviceToDevice, s));
+  ACS_HIP(ctx, hipMemsetAsync(h->bad, 0, sizeof(int), s));
+  ExtState st0;
+  std::memset(&st0, 0, sizeof(st0));
+  st0.lam = op.lambda0;
+  st0.relin = 1;
+  ACS_HIP(ctx, hipMemcpyAsync(h->st, &st0, sizeof(st0), hipMemcpyHostToDevice, s));
+  ACS_HIP(ctx, hipStreamSynchronize(s));
+  if (payload_sizes) {
+    payload_sizes[0] = nE + world;
+    payload_sizes[1] = 3;
+  }
+  *out = h;
+  return ACS_OK;
+}
+
+int acs_sba_ext_dist_destroy(acs_sba_ext_dist* h) {
+  if (!h) return ACS_OK;
+  (void)hipStreamSynchronize(h->ctx->stream);
+  if (h->own) (void)hipFree(h->own);
+  delete h;
+  return ACS_OK;
+}
+
+int acs_sba_ext_dist_init(acs_sba_ext_dist* h, double* p3) {
+  hipStream_t s = h->ctx->stream;
+#define EXT_COST0(g) ext_dist_cost<g>(h, s, 0)
+  EXT_G_SWITCH(h->d.G, EXT_COST0)
+#undef EXT_COST0
+  hipLaunchKernelGGL(k_ext_pack3, dim3(1), dim3(256), 0, s, h->d, h->st, 0, h->Fp, h->normp, p3);
+  ACS_HIP(h->ctx, hipGetLastError());
+  return ACS_OK;
+}
+
+int acs_sba_ext_dist_phase1(acs_sba_ext_dist* h, double* p1) {
+  acs_ctx* ctx = h->ctx;
+  hipStream_t s = ctx->stream;
+  const ExtDims& d = h->d;
+  const int NC = 6 * d.C, nE = NC * NC + 3 * NC;
+  ACS_HIP(ctx, hipMemsetAsync(p1, 0, sizeof(double) * (nE + h->R), s));
+#define EXT_LIN(g) ext_dist_linearize<g>(h, s)
+  EXT_G_SWITCH(d.G, EXT_LIN)
+#undef EXT_LIN
+  hipLaunchKernelGGL(k_ext_schur, dim3(h->nchunk), dim3(256), ext_schur_lds(d), s, d, h->st, h->Q, h->Vg, h->mk,
+                     h->cid, h->part);
+  hipLaunchKernelGGL(k_ext_pack1, dim3(1), dim3(256), 0, s, d, h->st, h->nchunk, h->part, h->Vg, h->rank, p1);
+  ACS_HIP(ctx, hipGetLastError());
+  return ACS_OK;
+}
+
+int acs_sba_ext_dist_phase2(acs_sba_ext_dist* h, const double* p1, double* p3) {
+  acs_ctx* ctx = h->ctx;
+  hipStream_t s = ctx->stream;
+  const ExtDims& d = h->d;
+  const int NC = 6 * d.C, nE = NC * NC + 3 * NC;
+  const int NP = ((NC + 15) / 16) * 16;
+  const size_t lds_solve = sizeof(double) * ((size_t)NP * (NP + 1) + NP + 512 + 256);
+  hipLaunchKernelGGL(k_ext_solve, dim3(1), dim3(256), lds_solve, s, d, h->st, 1, p1, h->Vg, 0, p1 + nE, h->R, h->dc,
+                     h->Sg, h->bad);
+  hipLaunchKernelGGL(k_ext_back, dim3(acs_grid(d.n, 256)), dim3(256), 0, s, d, h->st, h->Q, h->Vg, h->mk, h->cid,
+                     h->dc, h->dpts, h->normp);
+  hipLaunchKernelGGL(k_ext_cam, dim3(1), dim3(64), 0, s, d, h->st, h->dc, h->dcams, h->camnorm);
+#define EXT_COST1(g) ext_dist_cost<g>(h, s, 1)
+  EXT_G_SWITCH(d.G, EXT_COST1)
+#undef EXT_COST1
+  hipLaunchKernelGGL(k_ext_pack3, dim3(1), dim3(256), 0, s, d, h->st, 1, h->Fp, h->normp, p3);
+  ACS_HIP(ctx, hipGetLastError());
+  return ACS_OK;
+}
+
+int acs_sba_ext_dist_phase3(acs_sba_ext_dist* h, const double* p3, int32_t init, int32_t* status) {
+  acs_ctx* ctx = h->ctx;
+  hipStream_t s = ctx->stream;
+  hipLaunchKernelGGL(k_ext_lm_dist, dim3(1), dim3(64), 0, s, h->d, h->st, h->o, init, p3, h->camnorm);
+  ACS_HIP(ctx, hipGetLastError());
+  int32_t stv = 0;
+  ACS_HIP(ctx, hipMemcpyAsync(&stv, &h->st->status, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  ACS_HIP(ctx, hipStreamSynchronize(s));
+  if (status) *status = stv;
+  return ACS_OK;
+}
+
+int acs_sba_ext_dist_result(acs_sba_ext_dist* h, double* cams, double* pts, acs_sba_ext_report* report,
+                            uint32_t flags) {
+  acs_ctx* ctx = h->ctx;
+  hipStream_t s = ctx->stream;
+  const ExtDims& d = h->d;
+  ExtState hs;
+  ACS_HIP(ctx, hipMemcpyAsync(&hs, h->st, sizeof(hs), hipMemcpyDeviceToHost, s));
+  ACS_HIP(ctx, hipStreamSynchronize(s));
+  const hipMemcpyKind kout = (flags & ACS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  if (cams)
+    ACS_HIP(ctx, hipMemcpyAsync(cams, h->dcams + hs.cur * d.C * ACS_CAM_STRIDE, sizeof(double) * ACS_CAM_STRIDE * d.C,
+                                kout, s));
+  if (pts) ACS_HIP(ctx, hipMemcpyAsync(pts, h->dpts + (size_t)hs.cur * d.n * 3, sizeof(double) * 3 * d.n, kout, s));
+  int nbad = 0;
+  ACS_HIP(ctx, hipMemcpyAsync(&nbad, h->bad, sizeof(int), hipMemcpyDeviceToHost, s));
   ACS_HIP(ctx, hipStreamSynchronize(s));
   if (report) {
     report->status = hs.status == 0 ? ACS_STATUS_MAXITER : hs.status;

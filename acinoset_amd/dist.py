@@ -1,4 +1,7 @@
-"""Frame-window distributed FTE solve (BASELINE configs[3]).
+"""Multi-GPU solves of the hot path: frame-window FTE (BASELINE
+configs[3]) and points + extrinsics SBA with a reduced-camera-system all-reduce.
+
+Frame-window FTE:
 
 One process per GPU (torchrun); ranks split the trajectory's 3-frame super-blocks into
 chains that share their end blocks (include/acinoset_hip.h, acs_fte_dist_*). Every LM
@@ -14,6 +17,10 @@ so the state stays replicated without any broadcast.
 
 `lm_loop` is the protocol, independent of the backend: the HIP ranks below, or the numpy
 restatement in oracle/fte_dist.py that the CPU tests plug in.
+
+Points + extrinsics SBA (`lm_loop2`): points are split over the ranks, cameras replicated;
+per LM step the summed reduced camera system (6C x 6C + vectors, 11 KB at C = 6) and the
+summed cost / step norms (3 doubles).
 """
 import ctypes as C
 
@@ -38,6 +45,23 @@ def lm_loop(ranks, allreduce):
         p3 = [r.phase3(a) for r, a in zip(ranks, p2)]
         allreduce(p3)
         st = [r.phase4(a) for r, a in zip(ranks, p3)]
+        assert len(set(st)) == 1, f'ranks diverged: {st}'
+        if st[0] != 0:
+            return st[0]
+
+
+def lm_loop2(ranks, allreduce):
+    """Two-payload variant of lm_loop (points + extrinsics SBA)."""
+    p3 = [r.init() for r in ranks]
+    allreduce(p3)
+    for r, p in zip(ranks, p3):
+        r.phase3(p, init=True)
+    while True:
+        p1 = [r.phase1() for r in ranks]
+        allreduce(p1)
+        p3 = [r.phase2(a) for r, a in zip(ranks, p1)]
+        allreduce(p3)
+        st = [r.phase3(a) for r, a in zip(ranks, p3)]
         assert len(set(st)) == 1, f'ranks diverged: {st}'
         if st[0] != 0:
             return st[0]
@@ -187,3 +211,123 @@ def fte_solve_virtual(ctx, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutte
         finally:
             for r in ranks:
                 r.close()
+
+
+class HipSbaExtRank:
+    """One rank of the points + extrinsics SBA: its own points (local indices) and their
+    observations; cameras (C, 20) replicated."""
+
+    def __init__(self, ctx, cams, uv, pt_idx, cam_idx, pts, opts=None, rank=0, world=1):
+        import torch
+        self.ctx = ctx
+        cams = _native._c64(cams)
+        uv = _native._c64(uv).reshape(-1, 2)
+        pi = np.ascontiguousarray(pt_idx, np.int32)
+        ci = np.ascontiguousarray(cam_idx, np.int32)
+        pts = _native._c64(pts).reshape(-1, 3)
+        self.n_cams, self.n_pts = len(cams), len(pts)
+        opts = opts or ctx.sba_ext_opts()
+        h = C.c_void_p()
+        sizes = (C.c_int64 * 2)()
+        P_ = _native._ptr
+        ctx.check(ctx.lib.acs_sba_ext_dist_create(ctx.h, P_(cams), len(cams), P_(uv), P_(pi), P_(ci), len(uv), P_(pts),
+                                                  len(pts), C.byref(opts), int(rank), int(world), C.byref(h), sizes,
+                                                  0), 'acs_sba_ext_dist_create')
+        self.h = h
+        dev = torch.device('cuda', ctx.device)
+        self.p = [torch.zeros(int(n), dtype=torch.float64, device=dev) for n in sizes]
+
+    @staticmethod
+    def _ptr(t):
+        return C.c_void_p(t.data_ptr())
+
+    def init(self):
+        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_init(self.h, self._ptr(self.p[1])), 'acs_sba_ext_dist_init')
+        return self.p[1]
+
+    def phase1(self):
+        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_phase1(self.h, self._ptr(self.p[0])), 'acs_sba_ext_dist_phase1')
+        return self.p[0]
+
+    def phase2(self, p1):
+        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_phase2(self.h, self._ptr(p1), self._ptr(self.p[1])),
+                       'acs_sba_ext_dist_phase2')
+        return self.p[1]
+
+    def phase3(self, p3, init=False):
+        st = C.c_int32(0)
+        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_phase3(self.h, self._ptr(p3), int(bool(init)), C.byref(st)),
+                       'acs_sba_ext_dist_phase3')
+        return st.value
+
+    def result(self):
+        cams = np.empty((self.n_cams, _native.ACS_CAM_STRIDE))
+        pts = np.empty((self.n_pts, 3))
+        rep = _native.SbaExtReport()
+        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_result(self.h, _native._ptr(cams), _native._ptr(pts),
+                                                            C.byref(rep), 0), 'acs_sba_ext_dist_result')
+        return cams, pts, rep.as_dict()
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.ctx.lib.acs_sba_ext_dist_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def split_points(pt_idx, n_pts, world):
+    """Contiguous point shards: (per-rank point ranges, per-rank observation ids, local ids)."""
+    pt_idx = np.asarray(pt_idx)
+    bounds = [(n_pts * r) // world for r in range(world + 1)]
+    shards = []
+    for r in range(world):
+        lo, hi = bounds[r], bounds[r + 1]
+        obs = np.nonzero((pt_idx >= lo) & (pt_idx < hi))[0]
+        shards.append((lo, hi, obs, pt_idx[obs] - lo))
+    return shards
+
+
+def sba_extrinsics_dist(ctx, cams, uv, pt_idx, cam_idx, pts, opts=None, group=None):
+    """Points + extrinsics SBA under torch.distributed: every rank passes the full problem
+    and solves its contiguous point shard. Returns (cams, all points, report) on every
+    rank (the points are all-gathered once at the end)."""
+    import torch
+    import torch.distributed as tdist
+    rank, world = tdist.get_rank(group), tdist.get_world_size(group)
+    pts = np.asarray(pts, np.float64).reshape(-1, 3)
+    lo, hi, obs, loc = split_points(pt_idx, len(pts), world)[rank]
+    with _on_torch_stream(ctx):
+        r = HipSbaExtRank(ctx, cams, np.asarray(uv).reshape(-1, 2)[obs], loc, np.asarray(cam_idx)[obs], pts[lo:hi],
+                          opts, rank, world)
+        try:
+            lm_loop2([r], torch_allreduce(group))
+            c, p, rep = r.result()
+        finally:
+            r.close()
+        full = torch.zeros((len(pts), 3), dtype=torch.float64, device=torch.device('cuda', ctx.device))
+        full[lo:hi] = torch.from_numpy(p).to(full.device)
+        tdist.all_reduce(full, group=group)
+        return c, full.cpu().numpy(), rep
+
+
+def sba_extrinsics_virtual(ctx, cams, uv, pt_idx, cam_idx, pts, opts=None, world=2):
+    """The distributed points + extrinsics SBA with `world` ranks emulated in one process."""
+    pts = np.asarray(pts, np.float64).reshape(-1, 3)
+    with _on_torch_stream(ctx):
+        shards = split_points(pt_idx, len(pts), world)
+        ranks = [HipSbaExtRank(ctx, cams, np.asarray(uv).reshape(-1, 2)[obs], loc, np.asarray(cam_idx)[obs],
+                               pts[lo:hi], opts, r, world) for r, (lo, hi, obs, loc) in enumerate(shards)]
+        try:
+            lm_loop2(ranks, local_allreduce)
+            outs = [r.result() for r in ranks]
+        finally:
+            for r in ranks:
+                r.close()
+    for c, _, _ in outs[1:]:
+        assert np.array_equal(c, outs[0][0])
+    return outs[0][0], np.concatenate([o[1] for o in outs]), outs[0][2]

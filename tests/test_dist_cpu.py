@@ -1,11 +1,14 @@
-"""CPU tests of the frame-window distributed FTE protocol (acinoset_amd/dist.py, SURVEY.md
-§8(e)): the product's LM driver `lm_loop` runs the oracle restatement of every rank
-(oracle/fte_dist.py) and must reproduce the monolithic oracle solve (oracle/fte.py) —
-single-process emulation for several rank counts, and world_size 2 over torch.distributed
-with the gloo backend (the same all-reduce calls the GPU ranks make over RCCL).
+"""CPU tests of the multi-GPU protocols (acinoset_amd/dist.py).
 
-Tolerance: the decomposition only reorders sums, so iterates agree to rounding: same
-iteration count and status, cost 1e-12 relative, X 1e-10, tau 1e-12.
+The product's LM drivers (`lm_loop` for the frame-window FTE, `lm_loop2` for points +
+extrinsics SBA) run the oracle restatement of every rank (oracle/fte_dist.py,
+oracle/sba_ext_dist.py) and must reproduce the monolithic oracle solves (oracle/fte.py,
+oracle/sba_ext.py): single-process emulation for several rank counts, and world_size 2
+over torch.distributed with the gloo backend (the same all-reduce calls the GPU ranks make
+over RCCL).
+
+Tolerance: the decompositions only reorder sums, so iterates agree to rounding: same
+iteration count and status, cost 1e-12 relative, X 1e-10 (FTE) / 1e-9 (SBA), tau 1e-12.
 """
 import os
 import socket
@@ -14,7 +17,7 @@ import numpy as np
 import pytest
 
 from acinoset_amd import dist, synth
-from oracle import fte as ofte, fte_dist as odist
+from oracle import fte as ofte, fte_dist as odist, sba_ext_dist as osed
 
 
 def _problem(mode='head', N=40, sd=True, inter='vel', seed=2):
@@ -99,3 +102,68 @@ def test_dist_gloo_world2_matches_monolithic(tmp_path):
     r0 = res[0]
     _check((r0['X'], r0['tau'], dict(iters=int(r0['iters']), n_accepted=int(r0['nacc']), status=int(r0['status']),
                                      cost_after=float(r0['cost']))), ref)
+
+
+# ---- points + extrinsics SBA over ranks (acs_sba_ext_dist_*) ------------------------
+def _ext_problem():
+    from conftest import golden
+    g = golden('sba_extrinsics')
+    return g, g['points_2d'], g['points_3d'], g['point_indices'].astype(np.int64), g['camera_indices'].astype(np.int64)
+
+
+def _ext_ranks(world, max_iters=200):
+    g, uv, X, pi, ci = _ext_problem()
+    ranks = []
+    for r, (lo, hi, obs, loc) in enumerate(dist.split_points(pi, len(X), world)):
+        ranks.append(osed.OracleSbaExtRank(uv[obs], X[lo:hi], loc, ci[obs], g['K'], g['D'], g['R0'], g['t0'], r, world,
+                                           max_iters=max_iters))
+    return ranks
+
+
+@pytest.mark.parametrize('world', [2, 3, 7])
+def test_ext_dist_protocol_matches_monolithic(world):
+    from oracle import sba_ext as ose
+    g, uv, X, pi, ci = _ext_problem()
+    Xm, Rm, tm, im = ose.sba_extrinsics(uv, X, pi, ci, g['K'], g['D'], g['R0'], g['t0'], max_iters=200)
+    ranks = _ext_ranks(world)
+    dist.lm_loop2(ranks, dist.local_allreduce)
+    outs = [r.result() for r in ranks]
+    for o in outs[1:]:
+        assert np.array_equal(o[0], outs[0][0]) and np.array_equal(o[1], outs[0][1])
+    R, t, _, info = outs[0]
+    Xd = np.concatenate([o[2] for o in outs])
+    assert info['iters'] == im['iters'] and info['n_accepted'] == im['n_accepted']
+    assert {2: 'ftol', 3: 'xtol', 5: 'maxiter'}[info['status']] == im['status']
+    assert abs(info['cost_after'] - im['cost_after']) <= 1e-12 * im['cost_after']
+    np.testing.assert_allclose(Xd, Xm, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(R, Rm, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(t, tm, rtol=0, atol=1e-9)
+
+
+def _gloo_ext_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as tdist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        r = _ext_ranks(world)[rank]
+        allreduce = dist.torch_allreduce()
+        dist.lm_loop2([r], lambda ps: allreduce([torch.from_numpy(ps[0])]))
+        R, t, X, info = r.result()
+        np.savez(os.path.join(out_dir, f'ext{rank}.npz'), R=R, t=t, X=X, iters=info['iters'])
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_ext_dist_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+    from oracle import sba_ext as ose
+    mp.start_processes(_gloo_ext_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method='spawn')
+    g, uv, X, pi, ci = _ext_problem()
+    Xm, Rm, tm, im = ose.sba_extrinsics(uv, X, pi, ci, g['K'], g['D'], g['R0'], g['t0'], max_iters=200)
+    a, b = (np.load(tmp_path / f'ext{r}.npz') for r in range(2))
+    assert np.array_equal(a['R'], b['R']) and np.array_equal(a['t'], b['t'])
+    assert int(a['iters']) == im['iters']
+    np.testing.assert_allclose(np.concatenate([a['X'], b['X']]), Xm, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(a['R'], Rm, rtol=0, atol=1e-10)

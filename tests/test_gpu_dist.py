@@ -1,4 +1,6 @@
-"""GPU parity of the frame-window distributed FTE solve (acs_fte_dist_*).
+"""GPU parity of the multi-GPU solves: frame-window FTE (acs_fte_dist_*)
+and points + extrinsics SBA (acs_sba_ext_dist_*, same tolerances as the single-GPU
+extrinsics parity: cost 1e-12 relative, points 1e-9 m, rotations 1e-10).
 
 * `fte_solve_virtual`: W ranks emulated in one process on one GPU (payload sums in rank
   order) must reproduce the single-GPU acs_fte_solve iterate for iterate: same iteration
@@ -92,5 +94,54 @@ def test_fte_dist_two_processes(ctx, tmp_path):
     X1, t1, r1 = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0)
     a, b = (np.load(tmp_path / f'rank{r}.npz') for r in range(2))
     assert np.array_equal(a['X'], b['X']) and np.array_equal(a['tau'], b['tau'])
+    assert int(a['iters']) == r1['iters']
+    np.testing.assert_allclose(a['X'], X1, rtol=0, atol=1e-9)
+
+
+# ---- points + extrinsics SBA over ranks ------------------------------------------------
+def _ext():
+    from conftest import golden
+    g = golden('sba_extrinsics')
+    return g, _native.pack_cameras(g['K'], g['D'], g['R0'], g['t0'])
+
+
+@pytest.mark.parametrize('world', [2, 3, 8])
+def test_sba_ext_dist_virtual_matches_single(ctx, world):
+    g, cams = _ext()
+    o = ctx.sba_ext_opts(max_iters=200)
+    c1, X1, _, _, r1 = ctx.sba_extrinsics(cams, g['points_2d'], g['point_indices'], g['camera_indices'],
+                                          g['points_3d'], o)
+    cd, Xd, rd = dist.sba_extrinsics_virtual(ctx, cams, g['points_2d'], g['point_indices'], g['camera_indices'],
+                                             g['points_3d'], o, world=world)
+    assert rd['iters'] == r1['iters'] and rd['n_accepted'] == r1['n_accepted'] and rd['status'] == r1['status']
+    assert abs(rd['cost_after'] - r1['cost_after']) <= 1e-12 * r1['cost_after']
+    np.testing.assert_allclose(Xd, X1, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(cd[:, 8:17], c1[:, 8:17], rtol=0, atol=1e-10)
+    np.testing.assert_allclose(cd[:, 17:], c1[:, 17:], rtol=0, atol=1e-9)
+
+
+def _ext_worker(rank, world, port, out_dir):
+    import torch.distributed as tdist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        ctx = _native.Context(0)
+        g, cams = _ext()
+        c, X, rep = dist.sba_extrinsics_dist(ctx, cams, g['points_2d'], g['point_indices'], g['camera_indices'],
+                                             g['points_3d'], ctx.sba_ext_opts(max_iters=200))
+        np.savez(os.path.join(out_dir, f'ext{rank}.npz'), cams=c, X=X, iters=rep['iters'])
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_sba_ext_dist_two_processes(ctx, tmp_path):
+    import torch.multiprocessing as mp
+    mp.start_processes(_ext_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method='spawn')
+    g, cams = _ext()
+    c1, X1, _, _, r1 = ctx.sba_extrinsics(cams, g['points_2d'], g['point_indices'], g['camera_indices'],
+                                          g['points_3d'], ctx.sba_ext_opts(max_iters=200))
+    a, b = (np.load(tmp_path / f'ext{r}.npz') for r in range(2))
+    assert np.array_equal(a['cams'], b['cams']) and np.array_equal(a['X'], b['X'])
     assert int(a['iters']) == r1['iters']
     np.testing.assert_allclose(a['X'], X1, rtol=0, atol=1e-9)
