@@ -38,7 +38,7 @@ SYMBOLS = (
     'acs_fte_dist_create', 'acs_fte_dist_init', 'acs_fte_dist_phase1', 'acs_fte_dist_phase2', 'acs_fte_dist_phase3',
     'acs_fte_dist_phase4', 'acs_fte_dist_result', 'acs_fte_dist_destroy',
     'acs_sba_ext_dist_create', 'acs_sba_ext_dist_init', 'acs_sba_ext_dist_phase1', 'acs_sba_ext_dist_phase2',
-    'acs_sba_ext_dist_phase3', 'acs_sba_ext_dist_result', 'acs_sba_ext_dist_destroy',
+    'acs_sba_ext_dist_phase3', 'acs_sba_ext_dist_result', 'acs_sba_ext_dist_destroy', 'acs_ekf_run',
 )
 
 
@@ -148,6 +148,8 @@ def _declare(lib):
         'acs_sba_ext_dist_phase3': (C.c_int, [_P, _P, i32, C.POINTER(i32)]),
         'acs_sba_ext_dist_result': (C.c_int, [_P, _P, _P, C.POINTER(SbaExtReport), u32]),
         'acs_sba_ext_dist_destroy': (C.c_int, [_P]),
+        'acs_ekf_run': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, dbl, dbl, dbl, _P, _P, _P, _P, i32,
+                                  dbl, _P, _P, _P, _P, _P, _P, u32]),
         'acs_sba_extrinsics': (C.c_int, [_P, _P, i32, _P, _P, _P, i64, _P, i64, C.POINTER(SbaExtOpts), _P, _P,
                                          C.POINTER(SbaExtReport), u32]),
     }
@@ -340,6 +342,38 @@ class Context:
                                                _ptr(pts), len(pts), C.byref(opts), _ptr(rb), _ptr(ra),
                                                C.byref(rep), 0), 'acs_sba_extrinsics')
         return cams, pts, rb, ra, rep.as_dict()
+
+    # ---- f2: EKF + RTS smoother ----------------------------------------------------------
+    def ekf_run(self, table, cams, meas, likelihood, fps, thresh, max_pixel_err, r_std_base, Q, P0, s0,
+                ref_numerics=True, eps=1e-3, covariances=False):
+        """meas (S, N, C, L, 2) or (N, C, L, 2); returns dict of x_pred, x_est, x_smooth
+        (S, N, n) [, P_est, P_smooth (S, N, n, n)], outliers (S,)."""
+        cams = _c64(cams)
+        meas = _c64(meas)
+        single = meas.ndim == 4
+        if single:
+            meas = meas[None]
+        S, N, Cn, L, _ = meas.shape
+        assert L == table.L and Cn == len(cams), (meas.shape, table.L, len(cams))
+        lik = _c64(likelihood).reshape(S, N, Cn, L)
+        n = 3 * table.P
+        s0 = _c64(s0).reshape(S, n)
+        out = {k: np.empty((S, N, n)) for k in ('x_pred', 'x_est', 'x_smooth')}
+        if covariances:
+            out.update(P_est=np.empty((S, N, n, n)), P_smooth=np.empty((S, N, n, n)))
+        outl = np.zeros(S, np.int64)
+        ints = np.ascontiguousarray(table.ints, np.int32)
+        reals = np.ascontiguousarray(table.reals, np.float64)
+        self.check(self.lib.acs_ekf_run(self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), _ptr(cams), Cn,
+                                        _ptr(meas), _ptr(lik), S, N, float(fps), float(thresh), float(max_pixel_err),
+                                        _ptr(_c64(r_std_base)), _ptr(_c64(Q)), _ptr(_c64(P0)), _ptr(s0),
+                                        int(bool(ref_numerics)), float(eps), _ptr(out['x_pred']), _ptr(out['x_est']),
+                                        _ptr(out['x_smooth']), _ptr(out.get('P_est')), _ptr(out.get('P_smooth')),
+                                        _ptr(outl), 0), 'acs_ekf_run')
+        out['outliers'] = outl
+        if single:
+            out = {k: v[0] for k, v in out.items()}
+        return out
 
     # ---- a9 -------------------------------------------------------------------------
     def redescending_loss(self, err, a=3.0, b=10.0, c=20.0, deriv=False):

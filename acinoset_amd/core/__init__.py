@@ -1,3 +1,4 @@
 """Mirror of the reference's `src/core` drivers on the SBA / FTE path."""
 from .sba import sba  # noqa: F401
 from .fte import fte  # noqa: F401
+from .ekf import ekf  # noqa: F401

@@ -87,12 +87,21 @@ __device__ __forceinline__ void mat3_mul(const double* A, const double* B, doubl
 
 // Evaluate one frame. `x` may live in global or shared memory. Caller must
 // __syncthreads() before reading sh (positions / M / om). Positions exclude any
-// shutter-delay shift (callers add it).
+// shutter-delay shift (callers add it). F32_TRIG: cos / sin in float32 of the float32
+// angle (the reference EKF's numerics, src/core/ekf.py:79 + misc.py:381-420).
+template <bool F32_TRIG = false>
 __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int tid, int nth) {
   for (int p = tid; p < s.P; p += nth) {
     double v = x[p];
     sh.xp[p] = v;
-    sincos(v, &sh.sn[p], &sh.cs[p]);
+    if (F32_TRIG) {
+      float sf, cf;
+      sincosf((float)v, &sf, &cf);
+      sh.sn[p] = sf;
+      sh.cs[p] = cf;
+    } else {
+      sincos(v, &sh.sn[p], &sh.cs[p]);
+    }
   }
   __syncthreads();
   for (int j = tid; j < s.J; j += nth) {

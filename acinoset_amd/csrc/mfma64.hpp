@@ -44,7 +44,17 @@ __device__ void wg_mgemm(double* C, int ldc, const double* A, int lda, const dou
 // In-place inverse of an SPD matrix (n = 16*nb, LDS or global, ld) by blocked
 // Gauss-Jordan without pivoting (SPD + LM damping: every pivot block is SPD).
 // tmp: 512 doubles of LDS. Non-positive pivots are counted in *bad.
+template <bool SPD = true>
+__device__ void wg_gj_inverse(double* A, int lda, int nb, double* tmp, int* bad);
+
 __device__ void wg_spd_inverse(double* A, int lda, int nb, double* tmp, int* bad) {
+  wg_gj_inverse<true>(A, lda, nb, tmp, bad);
+}
+
+// Blocked Gauss-Jordan inverse without pivoting. SPD: pivots must be positive; otherwise
+// (symmetric indefinite, e.g. the reference EKF's covariances) any pivot with |p| > 1e-300.
+template <bool SPD>
+__device__ void wg_gj_inverse(double* A, int lda, int nb, double* tmp, int* bad) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
   for (int k = 0; k < nb; ++k) {
@@ -58,7 +68,7 @@ __device__ void wg_spd_inverse(double* A, int lda, int nb, double* tmp, int* bad
       double* nxt = tmp + (((s + 1) & 1) << 8);
       if (tid < 256) {
         double p = cur[s * 16 + s];
-        if (!(p > 0.0)) {
+        if (SPD ? !(p > 0.0) : !(fabs(p) > 1e-300)) {
           if (bad && i == 0 && j == 0) atomicAdd(bad, 1);
           p = 1e-300;
         }

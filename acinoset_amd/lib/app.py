@@ -54,6 +54,18 @@ def save_fte(states, mode, out_dir, scene_fpath, start_frame, intermode='pos', d
     return out_fpath
 
 
+def save_ekf(states, mode, out_dir, scene_fpath, start_frame, directions=True, save_videos=True) -> str:
+    """`src/lib/app.py:298-314`: ekf.pickle = {positions (filtered), smoothed_positions,
+    x, dx, ddx, smoothed_x, smoothed_dx, smoothed_ddx, start_frame} (+ ekf.mat). Labelled
+    videos are out of scope."""
+    positions = [misc.get_3d_marker_coords({'x': x}, directions=directions, mode=mode) for x in states['x']]
+    smoothed = [misc.get_3d_marker_coords({'x': x}, directions=directions, mode=mode) for x in states['smoothed_x']]
+    out_fpath = os.path.join(out_dir, 'ekf.pickle')
+    utils.save_optimised_cheetah(positions, out_fpath, extra_data=dict(smoothed_positions=smoothed, **states,
+                                                                       start_frame=start_frame))
+    return out_fpath
+
+
 def start_logging(out_fpath):
     sys.stdout = misc.Logger(out_fpath)
 

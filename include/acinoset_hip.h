@@ -270,6 +270,22 @@ int acs_sba_ext_dist_result(acs_sba_ext_dist* h, double* cams, double* pts, acs_
                             uint32_t flags);
 int acs_sba_ext_dist_destroy(acs_sba_ext_dist* h);
 
+/* ---- §8(f)-2: EKF + RTS smoother (core.ekf, src/core/ekf.py:26-347) -----------------
+ * n_seq independent sequences of n_frames frames (one workgroup each). State n = 3P:
+ * [x, dx, ddx]. meas (n_seq, n_frames, n_cams, L, 2) pixels (NaN = missing), likelihood
+ * (n_seq, n_frames, n_cams, L); R = diag(s^2) with s = r_std_base[cam] (the reference's
+ * 2 cov_c / min cov, :244-248) or max_pixel_err below `thresh`. Q, P0: n x n; s0: (n_seq, n).
+ * ref_numerics != 0 reproduces the reference's float32 prediction cast and float32
+ * Jacobian perturbation (:79, :81-96); eps = the forward-difference step (1e-3).
+ * Outputs (n_seq, n_frames, n) x_pred (may be NULL), x_est, x_smooth; (.., n, n) P_est,
+ * P_smooth (may be NULL); outliers (n_seq) = the reference's 3-sigma count (may be NULL). */
+int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
+                int64_t n_reals, const double* cams, int32_t n_cams, const double* meas,
+                const double* likelihood, int32_t n_seq, int32_t n_frames, double fps, double thresh,
+                double max_pixel_err, const double* r_std_base, const double* Q, const double* P0,
+                const double* s0, int32_t ref_numerics, double eps, double* x_pred, double* x_est,
+                double* x_smooth, double* P_est, double* P_smooth, int64_t* outliers, uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

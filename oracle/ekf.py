@@ -1,0 +1,168 @@
+"""Oracle: extended Kalman filter + Rauch-Tung-Striebel smoother of src/core/ekf.py.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Restates `core.ekf.ekf` (src/core/ekf.py:26-347) as plain numpy, pinned by the reference's
+own run on synthetic data (tests/golden/ekf_*.npz, tests/golden/make_golden.py):
+
+* state s = [x (P), dx (P), ddx (P)]; constant-acceleration prediction (:73-79) whose
+  result is cast to float32 (`.astype(np.float32)`, :79) — the reference's measurement
+  model then runs on float32 pose values: FK trig in float32 (numpy float32 cos/sin of the
+  float32 angles, matrices and sums in float64), and the forward-difference Jacobian (:81-96,
+  eps = 1e-3) perturbs x_i in float32 (x_i + 1e-3 rounded to float32) while dividing by
+  1e-3. This module reproduces those roundings;
+* P0 (:159-186, including the reference's negative neck-length variance -0.28), Q from
+  the qb list (:188-207), F (:219-224), R = diag((2 cov_c / min cov)^2) with cal_covs of
+  :210-213 and max_pixel_err = cam_res[0] for points below the likelihood threshold
+  (:244-253); residual = nan_to_num(z - h) (:256-257); K = P H^T S^-1 (:267),
+  P = (I - K H) P (:274);
+* initial state from linear fits of the pairwise-triangulated nose and lure (:121-157);
+* RTS smoother (:280-287).
+"""
+import numpy as np
+from scipy.stats import linregress
+
+from .fisheye import project
+from .kinematics import POSE, marker_positions
+
+CAL_COVS = [0.137, 0.236, 0.176, 0.298, 0.087, 0.116]                      # src/core/ekf.py:210
+QB = [5.0, 5.0, 5.0, 10.0, 10.0, 10.0, 5.0, 5.0, 25.0, 5.0, 50.0, 5.0, 50.0, 25.0, 100.0, 30.0, 140.0, 40.0,
+      350.0, 200.0, 350.0, 200.0, 450.0, 400.0, 450.0, 400.0, 5.0, 5.0, 5.0]  # src/core/ekf.py:188-203
+SIGMA_BOUND = 3
+
+
+def n_angular(mode):
+    return len([k for k in POSE[mode] if 'phi' in k or 'theta' in k or 'psi' in k])
+
+
+def initial_covariance(mode):
+    """P0 (src/core/ekf.py:159-186)."""
+    na = n_angular(mode)
+    p_lin_pos, p_ang_pos = np.ones(3) * 9.0, np.ones(na) * (np.pi / 4) ** 2
+    p_lin_vel, p_ang_vel = np.ones(3) * 25.0, np.ones(na) * 9.0
+    p_lin_acc, p_ang_acc = np.ones(3) * 9.0, np.ones(na) * 9.0
+    p_ang_acc[10:] = 25.0
+    if mode == 'default':
+        d = np.concatenate([p_lin_pos, p_ang_pos[:3], [-0.28], p_ang_pos[3:], np.ones(3) * 9.0,
+                            p_lin_vel, p_ang_vel[:3], [0.0], p_ang_vel[3:], np.ones(3) * 25.0,
+                            p_lin_acc, p_ang_acc[:3], [0.0], p_ang_acc[3:], np.ones(3) * 9.0])
+    elif mode == 'head':
+        d = np.concatenate([p_lin_pos, p_ang_pos[:3], p_ang_pos[3:], p_lin_vel, p_ang_vel[:3], p_ang_vel[3:],
+                            p_lin_acc, p_ang_acc[:3], p_ang_acc[3:]])
+    else:
+        raise ValueError(f'the reference EKF defines P0 for default / head only, not {mode!r}')
+    return np.diag(d)
+
+
+def process_noise(P, sT):
+    qb = np.diag(QB[:P]) ** 2
+    return np.block([[sT ** 4 / 4 * qb, sT ** 3 / 2 * qb, sT ** 2 / 2 * qb],
+                     [sT ** 3 / 2 * qb, sT ** 2 * qb, sT * qb],
+                     [sT ** 2 / 2 * qb, sT * qb, qb]])
+
+
+def transition(P, sT):
+    n = 3 * P
+    F = np.eye(n)
+    r = np.arange(n - P)
+    F[r, r + P] = sT
+    r2 = np.arange(n - 2 * P)
+    F[r2, r2 + 2 * P] = sT ** 2 / 2
+    return F
+
+
+def predict(s, sT, P, ref_numerics=True):
+    acc = s[2 * P:]
+    vel = s[P:2 * P] + sT * acc
+    pos = s[:P] + sT * vel + (0.5 * sT ** 2) * acc
+    out = np.concatenate([pos, vel, acc])
+    return out.astype(np.float32).astype(np.float64) if ref_numerics else out
+
+
+def h_function(x, mode, K, D, R, t, ref_numerics=True):
+    """(L, 2) pixels of the pose x (reference numerics: float32 values, FK trig in float32)."""
+    x = np.asarray(x, np.float64)[None]
+    pos = marker_positions(mode, x, f32_trig=ref_numerics)[0]
+    return project(pos, K, D, R, t)
+
+
+def fd_jacobian(x, mode, K, D, R, t, eps=1e-3, ref_numerics=True):
+    """src/core/ekf.py:81-96; reference numerics perturb x_i in float32."""
+    x = np.asarray(x, np.float64)
+    fx = h_function(x, mode, K, D, R, t, ref_numerics).ravel()
+    J = np.empty((fx.size, x.size))
+    for i in range(x.size):
+        xp = x.copy()
+        xp[i] = float(np.float32(xp[i]) + np.float32(eps)) if ref_numerics else xp[i] + eps
+        J[:, i] = (h_function(xp, mode, K, D, R, t, ref_numerics).ravel() - fx) / eps
+    return fx, J
+
+
+def initial_state(mode, frames, markers_idx, xyz, start_frame, sT):
+    """src/core/ekf.py:121-157 from pairwise-triangulated points (frame, marker, xyz)."""
+    idx = {k: i for i, k in enumerate(POSE[mode])}
+    P = len(idx)
+    s = np.zeros(3 * P)
+    from acinoset_amd.kinematics import get_markers   # marker names (src/lib/misc.py:8-37)
+    names = list(get_markers(mode))
+    if 'lure' in names:
+        sel = markers_idx == names.index('lure')
+        if sel.sum() >= 2:
+            sx, ix = linregress(frames[sel], xyz[sel, 0])[:2]
+            sy, iy = linregress(frames[sel], xyz[sel, 1])[:2]
+            s[[idx['x_l'], idx['y_l']]] = [start_frame * sx + ix, start_frame * sy + iy]
+            s[[P + idx['x_l'], P + idx['y_l']]] = [sx / sT, sy / sT]
+    sel = markers_idx == names.index('nose')
+    sx, ix = linregress(frames[sel], xyz[sel, 0])[:2]
+    sy, iy = linregress(frames[sel], xyz[sel, 1])[:2]
+    s[[idx['x_0'], idx['y_0'], idx['psi_0']]] = [start_frame * sx + ix, start_frame * sy + iy, np.arctan2(sy, sx)]
+    s[[P + idx['x_0'], P + idx['y_0']]] = [sx / sT, sy / sT]
+    return s
+
+
+def ekf(meas, likelihood, K, D, R, t, mode, fps, s0, thresh=0.5, max_pixel_err=2704.0, ref_numerics=True):
+    """meas (N, C, L, 2) pixels (NaN = missing), likelihood (N, C, L). Returns a dict with
+    the filtered / predicted / smoothed states and covariances and the outlier count."""
+    N, C, L, _ = meas.shape
+    P = len(POSE[mode])
+    n = 3 * P
+    sT = 1.0 / fps
+    F = transition(P, sT)
+    Q = process_noise(P, sT)
+    Pm = initial_covariance(mode)
+    assert C == len(CAL_COVS)
+    base = np.repeat([2 * c / min(CAL_COVS) for c in CAL_COVS], 2 * L)
+    s = np.asarray(s0, np.float64)
+    out = dict(x_est=np.zeros((N, n)), x_pred=np.zeros((N, n)), P_est=np.zeros((N, n, n)), P_pred=np.zeros((N, n, n)))
+    outliers = 0
+    for i in range(N):
+        s = predict(s, sT, P, ref_numerics)
+        out['x_pred'][i] = s
+        Pm = F @ Pm @ F.T + Q
+        out['P_pred'][i] = Pm
+        H = np.zeros((2 * C * L, n))
+        h = np.zeros(2 * C * L)
+        for c in range(C):
+            h[c * 2 * L:(c + 1) * 2 * L], H[c * 2 * L:(c + 1) * 2 * L, :P] = fd_jacobian(s[:P], mode, K[c], D[c],
+                                                                                        R[c], t[c],
+                                                                                        ref_numerics=ref_numerics)
+        r_std = base.copy()
+        r_std[np.repeat(likelihood[i].ravel() < thresh, 2)] = max_pixel_err
+        Rm = np.diag(r_std ** 2)
+        resid = np.nan_to_num(meas[i].reshape(-1) - h)
+        S = H @ Pm @ H.T + Rm
+        tmp = SIGMA_BOUND * np.sqrt(np.diag(S))
+        outliers += int(np.sum((np.abs(resid[0::2]) > tmp[0::2]) | (np.abs(resid[1::2]) > tmp[1::2])))
+        Kg = Pm @ H.T @ np.linalg.inv(S)
+        s = s + Kg @ resid
+        out['x_est'][i] = s
+        Pm = (np.eye(n) - Kg @ H) @ Pm
+        out['P_est'][i] = Pm
+    xs = out['x_est'].copy()
+    Ps = out['P_est'].copy()
+    for i in range(N - 2, -1, -1):
+        A = out['P_est'][i] @ F.T @ np.linalg.inv(out['P_pred'][i + 1])
+        xs[i] = out['x_est'][i] + A @ (xs[i + 1] - out['x_pred'][i + 1])
+        Ps[i] = out['P_est'][i] + A @ (Ps[i + 1] - out['P_pred'][i + 1]) @ A.T
+    out.update(x_smooth=xs, P_smooth=Ps, outliers=outliers)
+    return out

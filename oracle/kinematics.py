@@ -22,20 +22,29 @@ POSE['head_stabilize'] = POSE['default'][:11]
 POSE['default_nolure'] = POSE['default'][:26]
 
 
-def _rx(a):
-    c, s = np.cos(a), np.sin(a)
+def _cs(a, f32):
+    """cos, sin; with f32 evaluated in float32 on float32-rounded angles (the numerics of the
+    reference EKF, whose predicted states are float32: src/core/ekf.py:79, misc.py:381-420)."""
+    if f32:
+        a32 = np.asarray(a).astype(np.float32)
+        return np.cos(a32).astype(np.float64), np.sin(a32).astype(np.float64)
+    return np.cos(a), np.sin(a)
+
+
+def _rx0(a, f32=False):
+    c, s = _cs(a, f32)
     o, z = np.ones_like(a), np.zeros_like(a)
     return np.stack([np.stack([o, z, z], -1), np.stack([z, c, s], -1), np.stack([z, -s, c], -1)], -2)
 
 
-def _ry(a):
-    c, s = np.cos(a), np.sin(a)
+def _ry0(a, f32=False):
+    c, s = _cs(a, f32)
     o, z = np.ones_like(a), np.zeros_like(a)
     return np.stack([np.stack([c, z, -s], -1), np.stack([z, o, z], -1), np.stack([s, z, c], -1)], -2)
 
 
-def _rz(a):
-    c, s = np.cos(a), np.sin(a)
+def _rz0(a, f32=False):
+    c, s = _cs(a, f32)
     o, z = np.ones_like(a), np.zeros_like(a)
     return np.stack([np.stack([c, s, z], -1), np.stack([-s, c, z], -1), np.stack([z, z, o], -1)], -2)
 
@@ -48,9 +57,13 @@ def _app(R, v):
     return np.einsum('nji,nj->ni', R, v)
 
 
-def marker_positions(mode, x, shift=None, directions=False):
-    """x (n, P) real or complex -> (n, L[+2], 3). `shift` (n,3) is added to p_head."""
+def marker_positions(mode, x, shift=None, directions=False, f32_trig=False):
+    """x (n, P) real or complex -> (n, L[+2], 3). `shift` (n,3) is added to p_head.
+    `f32_trig`: rotation cos/sin in float32 (see _cs)."""
     x = np.atleast_2d(x)
+    _rx = lambda a: _rx0(a, f32_trig)  # noqa: E731
+    _ry = lambda a: _ry0(a, f32_trig)  # noqa: E731
+    _rz = lambda a: _rz0(a, f32_trig)  # noqa: E731
     idx = {k: i for i, k in enumerate(POSE[mode])}
     X = lambda k: x[:, idx[k]]  # noqa: E731
     n = x.shape[0]

@@ -181,6 +181,62 @@ def extrinsics_fixture(n_frames=4):
     print(f'extrinsics: {len(p2)} obs, {len(p3)} pts, ref {dt:.1f}s')
 
 
+def ekf_fixture(mode='default', n_frames=30, seed=31):
+    """Runs the reference's own `core.ekf.ekf` (src/core/ekf.py:26-347). Its module is
+    loaded from the file with stand-ins for what it imports but does not compute with:
+    pyomo / seaborn (imported, unused by the EKF), `core.metrics.save_error_dists` (plots)
+    and `lib.app` (logging, the pickle/video writer and plotting); the stand-in
+    `save_ekf` captures the `states` dict the reference hands to it."""
+    import importlib.util
+    import types
+    from unittest import mock
+    for name in ('pyomo', 'pyomo.environ', 'pyomo.opt', 'seaborn'):
+        sys.modules.setdefault(name, mock.MagicMock())
+    captured = {}
+    app = types.ModuleType('lib.app')
+    app.start_logging = lambda *a, **k: None
+    app.stop_logging = lambda *a, **k: None
+    app.plot_cheetah_states = lambda *a, **k: None
+
+    def save_ekf(states, *a, **k):
+        captured.update({key: np.asarray(v, np.float64) for key, v in states.items()})
+        return 'ekf.pickle'
+    app.save_ekf = save_ekf
+    sys.modules['lib.app'] = app
+    import lib
+    lib.app = app
+    core = types.ModuleType('core')
+    core.__path__ = [os.path.join(REF_SRC, 'core')]
+    metrics = types.ModuleType('core.metrics')
+    metrics.save_error_dists = lambda *a, **k: 0.0
+    sys.modules['core'] = core
+    sys.modules['core.metrics'] = metrics
+    spec = importlib.util.spec_from_file_location('core.ekf', os.path.join(REF_SRC, 'core', 'ekf.py'))
+    ref_ekf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ref_ekf)
+    # the reprojection report after the smoother (ekf.py:326-333) trips over object-typed
+    # columns in pandas 2 (SURVEY §8c, metric.residual_error); it is not part of the fixture
+    ref_ekf.metric = types.SimpleNamespace(residual_error=lambda *a, **k: {})
+
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(n_frames, scene, mode=mode, seed=seed)
+    df = seq.to_df()
+    cam_params = (scene.K, scene.D, scene.R, scene.t, tuple(scene.res), scene.n_cams)
+    scene_path = '/tmp/golden_ekf_scene.json'
+    scene.to_json(scene_path)
+    out_dir = '/tmp/golden_ekf'
+    os.makedirs(out_dir, exist_ok=True)
+    t0 = time.time()
+    ref_ekf.ekf(out_dir, df, mode, cam_params, 0, n_frames - 1, 0.5, scene_path, params={'vid_fps': 90.0})
+    dt = time.time() - t0
+    markers = seq.markers
+    np.savez_compressed(os.path.join(HERE, f'ekf_{mode}.npz'), K=scene.K, D=scene.D, R=scene.R, t=scene.t,
+                        res=np.array(scene.res), fps=90.0, thresh=0.5, n_frames=n_frames,
+                        uv=seq.uv, likelihood=seq.likelihood, marker_names=np.array(markers),
+                        ref_seconds=dt, **{f'out_{k}': v for k, v in captured.items()})
+    print(f'ekf {mode}: {n_frames} frames, ref {dt:.1f}s, keys {sorted(captured)}')
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['loss', 'fk', 'tri', 'cfg1', 'cfg2', 'ext']
     if 'loss' in which:
@@ -195,3 +251,6 @@ if __name__ == '__main__':
         sba_fixture('sba_cfg2', 100, list(range(6)))
     if 'ext' in which:
         extrinsics_fixture()
+    if 'ekf' in which:
+        ekf_fixture('default', 30)
+        ekf_fixture('head', 40)

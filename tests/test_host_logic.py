@@ -51,3 +51,50 @@ def test_states_satisfy_reference_integration_constraints():
 def test_model_weights_are_reference_Q():
     q = cfte.model_weights('head')
     np.testing.assert_allclose(q, 1 / np.array([4, 7, 5, 13, 9, 26], float) ** 2)
+
+
+def test_ekf_model_matrices_match_oracle():
+    """P0 / Q / R std of the drop-in (acinoset_amd.core.ekf) equal the oracle restatement of
+    src/core/ekf.py:159-213."""
+    import importlib
+    from oracle import ekf as oekf
+    cekf = importlib.import_module('acinoset_amd.core.ekf')
+    for mode, P in (('default', 29), ('head', 6)):
+        np.testing.assert_array_equal(cekf.initial_covariance(mode), oekf.initial_covariance(mode))
+        np.testing.assert_array_equal(cekf.process_covariance(P, 1 / 90.0), oekf.process_noise(P, 1 / 90.0))
+    np.testing.assert_allclose(cekf.measurement_std(6), [2 * c / 0.087 for c in oekf.CAL_COVS])
+    assert cekf.initial_covariance('default')[6, 6] == -0.28   # the reference's neck-length entry
+
+
+def test_ekf_initial_state_matches_oracle():
+    import importlib
+    import pandas as pd
+    from conftest import golden
+    from oracle import ekf as oekf, fisheye
+    cekf = importlib.import_module('acinoset_amd.core.ekf')
+    g = golden('ekf_default')
+    N = int(g['n_frames'])
+    uv = g['uv']
+    C, L = uv.shape[1], uv.shape[2]
+    fr, ca, mk = np.meshgrid(np.arange(N), np.arange(C), np.arange(L), indexing='ij')
+    fr_, mk_, xyz = fisheye.pairwise_points(fr.ravel(), ca.ravel(), mk.ravel(), uv[..., 0].ravel(),
+                                            uv[..., 1].ravel(), g['K'], g['D'], g['R'], g['t'])
+    names = list(g['marker_names'])
+    df = pd.DataFrame({'frame': fr_, 'marker': [names[m] for m in mk_], 'x': xyz[:, 0], 'y': xyz[:, 1],
+                       'z': xyz[:, 2]})
+    np.testing.assert_allclose(cekf.initial_state(df, 'default', 0, 90.0),
+                               oekf.initial_state('default', fr_, mk_, xyz, 0, 1 / 90.0), rtol=1e-10, atol=1e-10)
+
+
+def test_ekf_dense_observations_pivot():
+    import importlib
+    from acinoset_amd import synth
+    cekf = importlib.import_module('acinoset_amd.core.ekf')
+    seq = synth.make_sequence(5, synth.load_scene_file(), mode='head', seed=1)
+    df = seq.to_df()
+    df = df.drop(index=[0, 7]).reset_index(drop=True)           # two missing rows -> NaN
+    meas, lik = cekf.dense_observations(df, seq.markers, 6, 5)
+    assert np.isnan(meas).sum() == 4 and np.isnan(lik).sum() == 2
+    ok = ~np.isnan(lik)
+    np.testing.assert_array_equal(lik[ok], seq.likelihood[ok])
+    np.testing.assert_array_equal(meas[ok], seq.uv[ok])

@@ -183,3 +183,48 @@ def test_oracle_sba_extrinsics_beats_reference_cost():
     assert abs(info['cost_before'] - c0) < 1e-9 * c0
     assert info['cost_after'] <= c_ref
     np.testing.assert_allclose(R @ np.swapaxes(R, 1, 2), np.broadcast_to(np.eye(3), R.shape), atol=1e-12)
+
+
+def _ekf_golden(mode):
+    from oracle import ekf as oekf
+    g = golden(f'ekf_{mode}')
+    N = int(g['n_frames'])
+    uv, lik = g['uv'], g['likelihood']
+    C, L = uv.shape[1], uv.shape[2]
+    fr, ca, mk = np.meshgrid(np.arange(N), np.arange(C), np.arange(L), indexing='ij')
+    fr_, mk_, xyz = fisheye.pairwise_points(fr.ravel(), ca.ravel(), mk.ravel(), uv[..., 0].ravel(),
+                                            uv[..., 1].ravel(), g['K'], g['D'], g['R'], g['t'])
+    s0 = oekf.initial_state(mode, fr_, mk_, xyz, 0, 1 / 90.0)
+    return g, s0
+
+
+# EKF tolerances vs the reference run: the filter amplifies rounding-level differences
+# (a 1e-13 relative change of s0 moves x by ~1e-8 two frames later, in float64 too), and
+# the reference rounds its state to float32 each frame. head (40 frames): x 5e-5, dx 5e-4,
+# ddx 5e-3 (|ddx| ~ 50), smoothed x 2e-5. default: the reference run itself diverges after
+# frame ~18 (tail angles run away), so frames 0-9 only: x 1e-3.
+EKF_TOL = {'x': 5e-5, 'dx': 5e-4, 'ddx': 5e-3, 'smoothed_x': 2e-5}
+
+
+def test_oracle_ekf_matches_reference_head():
+    from oracle import ekf as oekf
+    g, s0 = _ekf_golden('head')
+    out = oekf.ekf(g['uv'], g['likelihood'], g['K'], g['D'], g['R'], g['t'], 'head', 90.0, s0, 0.5,
+                   float(g['res'][0]))
+    P = 6
+    xe, xs = out['x_est'], out['x_smooth']
+    np.testing.assert_allclose(xe[:, :P], g['out_x'], atol=EKF_TOL['x'], rtol=0)
+    np.testing.assert_allclose(xe[:, P:2 * P], g['out_dx'], atol=EKF_TOL['dx'], rtol=0)
+    np.testing.assert_allclose(xe[:, 2 * P:], g['out_ddx'], atol=EKF_TOL['ddx'], rtol=0)
+    np.testing.assert_allclose(xs[:, :P], g['out_smoothed_x'], atol=EKF_TOL['smoothed_x'], rtol=0)
+    # first frame: same arithmetic up to float64 rounding
+    np.testing.assert_allclose(xe[0, :P], g['out_x'][0], atol=1e-10, rtol=0)
+
+
+def test_oracle_ekf_matches_reference_default_early_frames():
+    from oracle import ekf as oekf
+    g, s0 = _ekf_golden('default')
+    out = oekf.ekf(g['uv'][:10], g['likelihood'][:10], g['K'], g['D'], g['R'], g['t'], 'default', 90.0, s0, 0.5,
+                   float(g['res'][0]))
+    np.testing.assert_allclose(out['x_est'][:, :29], g['out_x'][:10], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(out['x_est'][:2, :29], g['out_x'][:2], atol=1e-8, rtol=0)
