@@ -26,7 +26,7 @@
 #define EKF_WAVES 8
 
 struct EkfDims {
-  int N, C, L, P, n, npad, Ppad, m, S;
+  int N, C, L, P, n, npad, Ppad, m, mpad, S, n_ints, n_reals;
   double sT, thresh, maxpix, eps;
 };
 
@@ -46,7 +46,8 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
                                                     const double* __restrict__ P0, const double* __restrict__ s0,
                                                     double* __restrict__ xpred, double* __restrict__ xest,
                                                     double* __restrict__ Ppred, double* __restrict__ Pest,
-                                                    double* __restrict__ scratch, long long* __restrict__ outliers) {
+                                                    double* __restrict__ scratch, long long* __restrict__ outliers,
+                                                    unsigned long long* ekf_prof) {
   const int seq = blockIdx.x;
   const int tid = threadIdx.x, nth = blockDim.x, lane = tid & 63, wave = tid >> 6;
   const int n = d.n, P = d.P, m = d.m, LDP = d.npad + 1, Pp = d.Ppad;
@@ -58,17 +59,44 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   double* sPx = U;                                    // npad x Pp: P[:, x] before the update
   double* aug = sPx + (size_t)d.npad * Pp;            // Pp x AW
   double* sA = aug + (size_t)Pp * AW;                 // Pp x Pp
-  double* ss = sA + (size_t)Pp * Pp;                  // n: state
+  // the FK and algebra phases share U; what follows must start past the larger of the two
+  const size_t u_fk = (size_t)EKF_WAVES * sizeof(FkShared) / sizeof(double);
+  const size_t u_la = (size_t)d.npad * Pp + (size_t)Pp * AW + (size_t)Pp * Pp;
+  double* ss = U + (u_fk > u_la ? u_fk : u_la);      // n: state
   double* sx = ss + d.npad;                           // EKF_WAVES x FK_MAXP pose vectors
+  double* sRl = sx + EKF_WAVES * FK_MAXP;             // skeleton table (reals, then ints)
+  int* sI = reinterpret_cast<int*>(sRl + d.n_reals);
   __shared__ int s_piv;
+#ifdef EKF_PROFILE  // per-phase cycle counts (tools/prof_ekf_phases.py)
+  __shared__ unsigned long long s_prof[8];
+  unsigned long long t_last = 0;
+  if (tid < 8) s_prof[tid] = 0;
+#define EKF_TICK(k)                                                   \
+  do {                                                                \
+    __syncthreads();                                                  \
+    const unsigned long long t_now = clock64();                       \
+    if (tid == 0 && t_last) s_prof[(k + 7) % 8] += t_now - t_last;    \
+    t_last = t_now;                                                   \
+  } while (0)
+#else
+#define EKF_TICK(k) \
+  do {              \
+  } while (0)
+#endif
   __shared__ unsigned long long s_out;
-  const SkelView sk = skel_view(I, Rl);
+  for (int e = tid; e < d.n_ints; e += nth) sI[e] = I[e];  // the FK walks the table: keep it in LDS
+  for (int e = tid; e < d.n_reals; e += nth) sRl[e] = Rl[e];
+  __syncthreads();  // skel_view reads the header right away
+  const SkelView sk = skel_view(sI, sRl);
   const double sT = d.sT, h2 = 0.5 * sT * sT;
-  // per-sequence scratch: hpose (P+1) x m, H m x Pp, res m, w m
-  double* hpose = scratch + (size_t)seq * ((size_t)(P + 1) * m + (size_t)m * Pp + 2 * m);
+  // per-sequence scratch: hpose (P+1) x m; H, W H, G = H P_xx (mpad x Pp); res, w (mpad)
+  const int mp = d.mpad;
+  double* hpose = scratch + (size_t)seq * ((size_t)(P + 1) * m + 3 * (size_t)mp * Pp + 2 * mp);
   double* H = hpose + (size_t)(P + 1) * m;
-  double* res = H + (size_t)m * Pp;
-  double* wr = res + m;
+  double* HW = H + (size_t)mp * Pp;
+  double* G = HW + (size_t)mp * Pp;
+  double* res = G + (size_t)mp * Pp;
+  double* wr = res + mp;
   const size_t fstride = (size_t)d.C * d.L;  // measurements per frame
   for (int e = tid; e < d.npad * LDP; e += nth) {
     const int r = e / LDP, c = e % LDP;
@@ -80,6 +108,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
 
   for (int i = 0; i < d.N; ++i) {
     const size_t fo = ((size_t)seq * d.N + i);
+    EKF_TICK(0);
     // ---- 1. prediction --------------------------------------------------------------
     double sn = 0.0;
     if (tid < n) {
@@ -98,37 +127,47 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       ss[tid] = sn;
       xpred[fo * n + tid] = sn;
     }
-    // F X (per column, rows in increasing order read only not-yet-updated rows)
-    if (tid < n) {
-      const int c = tid;
-      for (int r = 0; r < n; ++r) {
-        double v = sP[r * LDP + c];
-        if (r < 2 * P) v += sT * sP[(r + P) * LDP + c];
-        if (r < P) v += h2 * sP[(r + 2 * P) * LDP + c];
-        sP[r * LDP + c] = v;
-      }
+    // F X: row block 0 += sT block 1 + sT^2/2 block 2, then block 1 += sT block 2 (each pass
+    // reads only rows not yet updated); then the same on the columns for (F X) F^T
+    for (int e = tid; e < P * n; e += nth) {
+      const int r = e / n, c = e % n;
+      sP[r * LDP + c] += sT * sP[(r + P) * LDP + c] + h2 * sP[(r + 2 * P) * LDP + c];
     }
     __syncthreads();
-    if (tid < n) {  // (F X) F^T + Q (per row)
-      const int r = tid;
-      for (int c = 0; c < n; ++c) {
-        double v = sP[r * LDP + c];
-        if (c < 2 * P) v += sT * sP[r * LDP + c + P];
-        if (c < P) v += h2 * sP[r * LDP + c + 2 * P];
-        sP[r * LDP + c] = v + Q[r * n + c];
-      }
+    for (int e = tid; e < P * n; e += nth) {
+      const int r = P + e / n, c = e % n;
+      sP[r * LDP + c] += sT * sP[(r + P) * LDP + c];
     }
+    __syncthreads();
+    for (int e = tid; e < P * n; e += nth) {
+      const int r = e / P, c = e % P;
+      sP[r * LDP + c] += sT * sP[r * LDP + c + P] + h2 * sP[r * LDP + c + 2 * P];
+    }
+    __syncthreads();
+    for (int e = tid; e < P * n; e += nth) {
+      const int r = e / P, c = P + e % P;
+      sP[r * LDP + c] += sT * sP[r * LDP + c + P];
+    }
+    __syncthreads();
+    for (int e = tid; e < n * n; e += nth) sP[(e / n) * LDP + e % n] += Q[e];
     __syncthreads();
     for (int e = tid; e < n * n; e += nth) Ppred[fo * n * n + e] = sP[(e / n) * LDP + e % n];
 
+    EKF_TICK(1);
     // ---- 2. poses of the forward-difference Jacobian --------------------------------
     for (int b0 = 0; b0 <= P; b0 += EKF_WAVES) {
       const int q = b0 + wave;
       double* xq = sx + wave * FK_MAXP;
       ekf_pose(ss, P, q <= P ? q : 0, F32, d.eps, xq, lane);
       __syncthreads();
+#ifdef EKF_PROFILE
+      const unsigned long long tf0 = clock64();
+#endif
       fk_frame<F32>(sk, xq, fks[wave], lane, 64);
       __syncthreads();
+#ifdef EKF_PROFILE
+      if (tid == 0) s_prof[7] += clock64() - tf0;   // FK share of the FK/proj phase
+#endif
       if (q <= P) {
         for (int o = lane; o < d.C * d.L; o += 64) {
           const int c = o / d.L, l = o % d.L;
@@ -142,51 +181,56 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       }
       __syncthreads();
     }
-    // H, residual, R^-1 (row r = 2 (c L + l) + d, the reference's ordering)
-    for (int r = tid; r < m; r += nth) {
-      const double h0 = hpose[r];
-      for (int q = 0; q < Pp; ++q) H[(size_t)r * Pp + q] = q < P ? (hpose[(size_t)(q + 1) * m + r] - h0) / d.eps : 0.0;
-      const int o = r >> 1, c = o / d.L;
-      const double z = meas[fo * fstride * 2 + r];
-      double e = z - h0;
-      if (!isfinite(e)) e = (e != e) ? 0.0 : (e > 0 ? 1.7976931348623157e308 : -1.7976931348623157e308);
-      res[r] = e;
-      const double lk = lik[fo * fstride + o];
-      const double sd = (lk < d.thresh) ? d.maxpix : rbase[c];
-      wr[r] = 1.0 / (sd * sd);
+    EKF_TICK(2);
+    // H, W H, residual, R^-1 (row r = 2 (c L + l) + d, the reference's ordering; rows
+    // past m are zero padding for the MFMA products)
+    for (int r = tid; r < mp; r += nth) {
+      if (r < m) {
+        const double h0 = hpose[r];
+        const int o = r >> 1, c = o / d.L;
+        const double z = meas[fo * fstride * 2 + r];
+        double e = z - h0;
+        if (!isfinite(e)) e = (e != e) ? 0.0 : (e > 0 ? 1.7976931348623157e308 : -1.7976931348623157e308);
+        res[r] = e;
+        const double lk = lik[fo * fstride + o];
+        const double sd = (lk < d.thresh) ? d.maxpix : rbase[c];
+        const double w = 1.0 / (sd * sd);
+        wr[r] = w;
+        for (int q = 0; q < Pp; ++q) {
+          const double hq = q < P ? (hpose[(size_t)(q + 1) * m + r] - h0) / d.eps : 0.0;
+          H[(size_t)r * Pp + q] = hq;
+          HW[(size_t)r * Pp + q] = w * hq;
+        }
+      } else {
+        res[r] = 0.0;
+        wr[r] = 0.0;
+        for (int q = 0; q < Pp; ++q) H[(size_t)r * Pp + q] = HW[(size_t)r * Pp + q] = 0.0;
+      }
     }
     __syncthreads();
+    EKF_TICK(3);
     // ---- 3. information-form update -------------------------------------------------
-    for (int e = tid; e < Pp * Pp; e += nth) {  // A = H^T R^-1 H
-      const int a = e / Pp, b = e % Pp;
-      double v = 0.0;
-      if (a < P && b < P)
-        for (int r = 0; r < m; ++r) v += wr[r] * H[(size_t)r * Pp + a] * H[(size_t)r * Pp + b];
-      sA[e] = v;
-    }
+    wg_mgemm<true, false>(sA, Pp, HW, Pp, H, Pp, Pp, Pp, mp, 1.0, 0.0);        // A = H^T R^-1 H
+    wg_mgemm<false, false>(G, Pp, H, Pp, sP, LDP, mp, Pp, Pp, 1.0, 0.0);       // G = H P[0:Pp, 0:Pp]
     for (int e = tid; e < d.npad * Pp; e += nth) {  // P[:, x]
       const int r = e / Pp, c = e % Pp;
       sPx[e] = (r < n && c < P) ? sP[r * LDP + c] : 0.0;
     }
-    for (int a = tid; a < Pp; a += nth) {  // b = H^T R^-1 r
+    for (int a = wave; a < Pp; a += EKF_WAVES) {  // b = H^T R^-1 r (fixed-order wave sums)
       double v = 0.0;
       if (a < P)
-        for (int r = 0; r < m; ++r) v += wr[r] * H[(size_t)r * Pp + a] * res[r];
-      aug[a * AW + Pp + d.npad] = v;
+        for (int r = lane; r < mp; r += 64) v += HW[(size_t)r * Pp + a] * res[r];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) aug[a * AW + Pp + d.npad] = v;
     }
-    // 3-sigma outlier count (:259-264): diag S = H_x P_xx H_x^T + R
+    // 3-sigma outlier count (:259-264): diag S = rows of H_x P_xx . H_x, + R
     unsigned long long cnt = 0;
     for (int pt = tid; pt < m / 2; pt += nth) {
       bool outl = false;
       for (int dd = 0; dd < 2; ++dd) {
         const int r = 2 * pt + dd;
-        const double* hr = H + (size_t)r * Pp;
         double q = 0.0;
-        for (int a = 0; a < P; ++a) {
-          double t = 0.0;
-          for (int b = 0; b < P; ++b) t += sP[a * LDP + b] * hr[b];
-          q += hr[a] * t;
-        }
+        for (int b = 0; b < P; ++b) q += G[(size_t)r * Pp + b] * H[(size_t)r * Pp + b];
         const double Srr = q + 1.0 / wr[r];
         if (fabs(res[r]) > 3.0 * sqrt(Srr)) outl = true;
       }
@@ -194,24 +238,25 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     }
     if (cnt) atomicAdd(&s_out, cnt);
     __syncthreads();
-    // aug = [I + A P_xx | A P[x, :] | b]  (rows a < P; padding rows identity)
-    for (int e = tid; e < Pp * (Pp + d.npad); e += nth) {
-      const int a = e / (Pp + d.npad), c = e % (Pp + d.npad);
-      double v = 0.0;
-      if (a < P) {
-        const int cc = c < Pp ? c : c - Pp;
-        const bool live = c < Pp ? cc < P : cc < n;
-        if (live)
-          for (int k = 0; k < P; ++k) v += sA[a * Pp + k] * sP[k * LDP + cc];
-        if (c < Pp && c == a) v += 1.0;
-      } else if (c == a) {
-        v = 1.0;
-      }
-      aug[a * AW + c] = v;
+    EKF_TICK(4);
+    // aug = [I + A P_xx | A P[x, :] | b]: G2 = A P[0:Pp, :] on MFMA (A is zero outside
+    // P x P), then the M block gets the identity and its padding columns are cleared
+    wg_mgemm<false, false>(aug + Pp, AW, sA, Pp, sP, LDP, Pp, d.npad, Pp, 1.0, 0.0);
+    for (int e = tid; e < Pp * d.npad; e += nth) {  // G2 columns >= n must be zero
+      const int a = e / d.npad, c = e % d.npad;
+      if (c >= n) aug[a * AW + Pp + c] = 0.0;
+    }
+    __syncthreads();
+    for (int e = tid; e < Pp * Pp; e += nth) {
+      const int a = e / Pp, c = e % Pp;
+      aug[a * AW + c] = (c < P ? aug[a * AW + Pp + c] : 0.0) + (a == c ? 1.0 : 0.0);
     }
     if (tid >= P && tid < Pp) aug[tid * AW + Pp + d.npad] = 0.0;
     __syncthreads();
-    // Gauss-Jordan with partial pivoting on the P x P block
+    EKF_TICK(5);
+    // Gauss-Jordan with partial pivoting on the P x P block (4 barriers per pivot):
+    // pivot search | row swap | eliminate with the unscaled pivot row (row k and column k
+    // untouched) | scale row k, clear column k
     for (int k = 0; k < P; ++k) {
       if (wave == 0) {
         double best = -1.0;
@@ -243,37 +288,35 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
         }
       __syncthreads();
       const double ip = 1.0 / aug[k * AW + k];
-      __syncthreads();
-      for (int c = tid; c < AW; c += nth) aug[k * AW + c] *= ip;
-      __syncthreads();
-      for (int e = tid; e < P * AW; e += nth) {
-        const int r = e / AW, c = e % AW;
-        if (r == k) continue;
-        const double f = aug[r * AW + k];
-        if (c != k) aug[e] -= f * aug[k * AW + c];
+      for (int c = tid; c < AW; c += nth) {  // one column per thread, rows in a loop
+        if (c == k) continue;
+        const double pkc = aug[k * AW + c] * ip;
+        for (int r = 0; r < P; ++r)
+          if (r != k) aug[r * AW + c] -= aug[r * AW + k] * pkc;
       }
       __syncthreads();
+      for (int c = tid; c < AW; c += nth) aug[k * AW + c] = (c == k) ? 1.0 : aug[k * AW + c] * ip;
       for (int r = tid; r < P; r += nth)
         if (r != k) aug[r * AW + k] = 0.0;
       __syncthreads();
     }
-    // s += P[:, x] Z_b ;  P -= P[:, x] Z_G
+    EKF_TICK(6);
+    // s += P[:, x] Z_b ;  P -= P[:, x] Z_G  (MFMA; sPx / Z are zero outside the live block)
     if (tid < n) {
       double v = 0.0;
       for (int k = 0; k < P; ++k) v += sPx[tid * Pp + k] * aug[k * AW + Pp + d.npad];
       ss[tid] += v;
     }
-    for (int e = tid; e < n * n; e += nth) {
-      const int r = e / n, c = e % n;
-      double v = 0.0;
-      for (int k = 0; k < P; ++k) v += sPx[r * Pp + k] * aug[k * AW + Pp + c];
-      sP[r * LDP + c] -= v;
-    }
-    __syncthreads();
+    wg_mgemm<false, false>(sP, LDP, sPx, Pp, aug + Pp, AW, d.npad, d.npad, Pp, -1.0, 1.0);
+    EKF_TICK(7);
     if (tid < n) xest[fo * n + tid] = ss[tid];
     for (int e = tid; e < n * n; e += nth) Pest[fo * n * n + e] = sP[(e / n) * LDP + e % n];
     __syncthreads();
   }
+#ifdef EKF_PROFILE
+  if (tid == 0 && ekf_prof)
+    for (int k = 0; k < 8; ++k) ekf_prof[seq * 8 + k] = s_prof[k];
+#endif
   if (tid == 0) outliers[seq] = (long long)s_out;
 }
 
@@ -313,7 +356,7 @@ __global__ __launch_bounds__(256) void k_ekf_smooth(EkfDims d, const double* __r
       const int r = e / LD, c = e % LD;
       sInv[e] = (r < n && c < n) ? Pp1[r * n + c] : (r == c ? 1.0 : 0.0);
     }
-    for (int e = tid; e < (int)nn; e += nth) {  // T = P_est F^T ; D = Ps[i+1] - Ppred[i+1]
+    for (int e = tid; e < (keep_P ? (int)nn : 0); e += nth) {  // T = P_est F^T ; D = Ps[i+1] - Ppred[i+1]
       const int r = e / np_, c = e % np_;
       double t = 0.0, dd = 0.0;
       if (r < n && c < n) {
@@ -327,10 +370,32 @@ __global__ __launch_bounds__(256) void k_ekf_smooth(EkfDims d, const double* __r
     }
     __syncthreads();
     wg_gj_inverse<false>(sInv, LD, np_ >> 4, tmp, bad);
-    wg_mgemm<false, false>(A, np_, T, np_, sInv, LD, np_, np_, np_, 1.0, 0.0);  // A = T Pp^-1
     for (int r = tid; r < np_; r += nth)
       sv[r] = r < n ? xs[(base + i + 1) * n + r] - xpred[(base + i + 1) * n + r] : 0.0;
     __syncthreads();
+    if (!keep_P) {
+      // xs[i] = x_est[i] + P_est F^T (P_pred^-1 v): two matrix-vector products, no gain matrix
+      double* sy = tmp;  // np <= 96 < 512
+      for (int r = tid; r < np_; r += nth) {
+        double v = 0.0;
+        for (int c = 0; c < np_; ++c) v += sInv[r * LD + c] * sv[c];
+        sy[r] = v;
+      }
+      __syncthreads();
+      for (int r = tid; r < n; r += nth) {
+        double v = xest[(base + i) * n + r];
+        for (int c = 0; c < n; ++c) {
+          double z = sy[c];  // (F^T y)[c]
+          if (c >= P) z += sT * sy[c - P];
+          if (c >= 2 * P) z += h2 * sy[c - 2 * P];
+          v += Pe[r * n + c] * z;
+        }
+        xs[(base + i) * n + r] = v;
+      }
+      __syncthreads();
+      continue;
+    }
+    wg_mgemm<false, false>(A, np_, T, np_, sInv, LD, np_, np_, np_, 1.0, 0.0);  // A = T Pp^-1
     for (int r = tid; r < n; r += nth) {
       double v = xest[(base + i) * n + r];
       for (int c = 0; c < n; ++c) v += A[(size_t)r * np_ + c] * sv[c];
@@ -343,13 +408,14 @@ __global__ __launch_bounds__(256) void k_ekf_smooth(EkfDims d, const double* __r
     }
     __syncthreads();
     wg_mgemm<false, true>(Pn, np_, E, np_, A, np_, np_, np_, np_, 1.0, 1.0);  // Ps[i] = P_est + E A^T
-    if (keep_P)
-      for (int e = tid; e < (int)nn0; e += nth) Ps[(base + i) * nn0 + e] = Pn[(size_t)(e / n) * np_ + e % n];
+    for (int e = tid; e < (int)nn0; e += nth) Ps[(base + i) * nn0 + e] = Pn[(size_t)(e / n) * np_ + e % n];
     __syncthreads();
   }
 }
 
+unsigned long long* g_ekf_prof = nullptr;
 extern "C" {
+void acs_ekf_prof(unsigned long long* p) { g_ekf_prof = p; }
 
 int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals, int64_t n_reals,
                 const double* cams, int32_t n_cams, const double* meas, const double* likelihood, int32_t n_seq,
@@ -378,6 +444,9 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
   d.npad = ((d.n + 15) / 16) * 16;
   d.Ppad = ((P + 15) / 16) * 16;
   d.m = 2 * n_cams * L;
+  d.mpad = ((d.m + 15) / 16) * 16;
+  d.n_ints = (int)n_ints;
+  d.n_reals = (int)n_reals;
   d.S = n_seq;
   d.sT = 1.0 / fps;
   d.thresh = thresh;
@@ -407,7 +476,7 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
   double* dPs = P_smooth ? ((flags & ACS_DEVICE_PTRS) ? P_smooth
                                                       : (double*)acs_ws(ctx, WS_FTE15, sizeof(double) * NF * n * n))
                          : nullptr;
-  const size_t scr_f = (size_t)n_seq * ((size_t)(P + 1) * d.m + (size_t)d.m * d.Ppad + 2 * d.m);
+  const size_t scr_f = (size_t)n_seq * ((size_t)(P + 1) * d.m + 3 * (size_t)d.mpad * d.Ppad + 2 * d.mpad);
   const size_t scr_s = (size_t)n_seq * 5 * d.npad * d.npad;
   double* scr = (double*)acs_ws(ctx, WS_FTE6, sizeof(double) * std::max(scr_f, scr_s) + 64 * (size_t)n_seq * 8);
   if (!dxp || !dxe || !dxs || !dPe || !dPp || !scr || (P_smooth && !dPs)) return ACS_E_NOMEM;
@@ -416,16 +485,17 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
   ACS_HIP(ctx, hipMemsetAsync(dbad, 0, sizeof(int), s));
   const size_t U = std::max((size_t)EKF_WAVES * sizeof(FkShared) / sizeof(double),
                             (size_t)d.npad * d.Ppad + (size_t)d.Ppad * (d.Ppad + d.npad + 1) + (size_t)d.Ppad * d.Ppad);
-  const size_t lds_f = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + U + d.npad + EKF_WAVES * FK_MAXP);
+  const size_t lds_f = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + U + d.npad + EKF_WAVES * FK_MAXP +
+                                          n_reals + (n_ints + 1) / 2 + 1);
   ACS_CHECK(ctx, lds_f <= 160 * 1024, "ekf: P = %d needs %zu bytes of LDS", P, lds_f);
   if (ref_numerics)
     hipLaunchKernelGGL(k_ekf_filter<true>, dim3(n_seq), dim3(512), lds_f, s, d, (const int*)dI, (const double*)dR,
                        (const double*)dC, (const double*)dM, (const double*)dL, (const double*)dRb, (const double*)dQ,
-                       (const double*)dP0, (const double*)dS0, dxp, dxe, dPp, dPe, scr, dout);
+                       (const double*)dP0, (const double*)dS0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof);
   else
     hipLaunchKernelGGL(k_ekf_filter<false>, dim3(n_seq), dim3(512), lds_f, s, d, (const int*)dI, (const double*)dR,
                        (const double*)dC, (const double*)dM, (const double*)dL, (const double*)dRb, (const double*)dQ,
-                       (const double*)dP0, (const double*)dS0, dxp, dxe, dPp, dPe, scr, dout);
+                       (const double*)dP0, (const double*)dS0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof);
   ACS_HIP(ctx, hipGetLastError());
   const size_t lds_s = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + 512 + d.npad);
   hipLaunchKernelGGL(k_ekf_smooth, dim3(n_seq), dim3(256), lds_s, s, d, dxp, dxe, dPp, dPe, dxs, dPs, scr, dbad,

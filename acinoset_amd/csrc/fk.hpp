@@ -55,6 +55,7 @@ __device__ __forceinline__ SkelView skel_view(const int* I, const double* R) {
 
 struct FkShared {
   double sn[FK_MAXP], cs[FK_MAXP], xp[FK_MAXP];
+  double root[3], world[3];  // head-root translation (x_0, y_0, z_0) and world (lure) position
   double G[FK_MAXJ][9];
   double M[FK_MAXJ][9];
   double pos[FK_MAXN][3];
@@ -102,6 +103,16 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
     } else {
       sincos(v, &sh.sn[p], &sh.cs[p]);
     }
+  }
+  if (tid < 2) {  // translation parameters, summed once per frame instead of once per node chain
+    const int kind = tid == 0 ? PK_TRANS : PK_WORLD;
+    double t[3] = {0.0, 0.0, 0.0};
+    for (int q = 0; q < s.P; ++q)
+      if (s.pk[4 * q] == kind) t[s.pk[4 * q + 1]] += x[q];
+    double* dst = tid == 0 ? sh.root : sh.world;
+    dst[0] = t[0];
+    dst[1] = t[1];
+    dst[2] = t[2];
   }
   __syncthreads();
   for (int j = tid; j < s.J; j += nth) {
@@ -151,25 +162,15 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
       const int* nd = s.nodes + 4 * node;
       const int base = nd[0];
       if (base == -2) {  // world node (lure): params of PK_WORLD kind
-        for (int q = 0; q < s.P; ++q) {
-          if (pk[4 * q] == PK_WORLD) {
-            const int ax = pk[4 * q + 1];
-            if (ax == 0) p0 += sh.xp[q];
-            if (ax == 1) p1 += sh.xp[q];
-            if (ax == 2) p2 += sh.xp[q];
-          }
-        }
+        p0 += sh.world[0];
+        p1 += sh.world[1];
+        p2 += sh.world[2];
         break;
       }
       if (base == -1) {  // head root: (x_0, y_0, z_0)
-        for (int q = 0; q < s.P; ++q) {
-          if (pk[4 * q] == PK_TRANS) {
-            const int ax = pk[4 * q + 1];
-            if (ax == 0) p0 += sh.xp[q];
-            if (ax == 1) p1 += sh.xp[q];
-            if (ax == 2) p2 += sh.xp[q];
-          }
-        }
+        p0 += sh.root[0];
+        p1 += sh.root[1];
+        p2 += sh.root[2];
         break;
       }
       const double* Mf = sh.M[nd[1]];

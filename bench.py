@@ -39,6 +39,9 @@ def parse():
     ap.add_argument('--no-fte', dest='fte', action='store_false')
     ap.add_argument('--window-frames', type=int, default=10000,
                     help='configs[3]: FTE over this many frames, frame windows sharded over the ranks (0 = skip)')
+    ap.add_argument('--ekf-seqs', type=int, default=64, help='EKF + RTS leg: sequences per rank (0 = skip)')
+    ap.add_argument('--ekf-frames', type=int, default=500)
+    ap.add_argument('--ekf-cams', type=int, default=12)
     ap.add_argument('--exchange', default='nccl', choices=('nccl', 'gloo'),
                     help='backend of the FTE window all-reduces (nccl = RCCL over xGMI)')
     ap.add_argument('--scale-frames', type=int, default=20000,
@@ -157,6 +160,8 @@ def main():
 
     if args.fte and world == 1:
         out['fte'] = bench_fte(ctx, torch, stream, n_frames=args.fte_frames)
+    if args.ekf_seqs > 0:
+        out['ekf'] = bench_ekf(ctx, torch, args.ekf_seqs, args.ekf_frames, args.ekf_cams, world, rank)
     if args.window_frames > 0:
         out['fte_window'] = bench_fte_window(ctx, torch, stream, args.window_frames, world, rank, args.exchange)
     if args.scale_frames > 0 and world == 1:
@@ -293,6 +298,48 @@ def _fte_problem(ctx, n_frames, seed=77):
                             'z': xyz[ok, 2]})
     X0 = cfte.initial_state(nose_df, 'default_nolure', 0, N - 1)
     return seq, cams, meas, w, X0, build_table('default_nolure'), cfte.model_weights('default_nolure')
+
+
+def bench_ekf(ctx, torch, n_seq, n_frames, n_cams, world, rank, steps=2):
+    """EKF + RTS smoother (the EKF half of configs[4]): `n_seq`
+    independent synthetic sequences per rank (replicas: the filter is sequential in time),
+    12-camera ring, default skeleton (29 pose parameters, 21 markers), reference numerics."""
+    import importlib
+    import torch.distributed as tdist
+    from acinoset_amd import _native, synth
+    from acinoset_amd.kinematics import build_table
+    cekf = importlib.import_module('acinoset_amd.core.ekf')
+    scene = synth.load_scene_file() if n_cams == 6 else synth.ring_scene(n_cams)
+    seqs = [synth.make_sequence(n_frames, scene, mode='default', seed=500 + 97 * rank + k) for k in range(n_seq)]
+    table = build_table('default')
+    P = table.P
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    meas = np.stack([q.uv for q in seqs])
+    lik = np.stack([q.likelihood for q in seqs])
+    s0 = np.zeros((n_seq, 3 * P))   # first frame's pose and velocity (throughput leg, not an init study)
+    for k, q in enumerate(seqs):
+        s0[k, :P] = q.x[0]
+        s0[k, P:2 * P] = (q.x[1] - q.x[0]) / q.Ts
+    covs = (cekf.CAL_COVS * ((n_cams + 5) // 6))[:n_cams]
+    args = (90.0, 0.5, float(scene.res[0]), cekf.measurement_std(n_cams, covs), cekf.process_covariance(P, 1 / 90.0),
+            cekf.initial_covariance('default'))
+    out = ctx.ekf_run(table, cams, meas, lik, *args, s0)                 # warm-up
+    if world > 1:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.ekf_run(table, cams, meas, lik, *args, s0)
+    dt = (time.perf_counter() - t0) / steps
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    return {'workload': f'ekf+rts C={n_cams} default (P=29, L=21) {n_seq} seqs x {n_frames} frames/rank',
+            'frames_per_s': world * n_seq * n_frames / dt, 'ms_per_call': dt * 1e3,
+            'us_per_frame_per_seq': dt / n_frames * 1e6, 'scaling': 'weak (replicas)',
+            'outliers_mean': float(np.mean(out['outliers'])),
+            'numerics': 'reference (float32 state rounding); the reference default-mode filter itself drifts on '
+                        'long sequences (oracle/ekf.py reproduces it), so no accuracy figure is quoted here'}
 
 
 def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl', steps=3):
