@@ -192,8 +192,8 @@ def pmc_per_launch(kernel, grid):
     r = d['per_launch'].get(f'{kernel}@{grid}')
     if r is None:
         return None, None
-    return r.get('hbm_bytes'), dict(fp64_flops=r.get('fp64_flops'), source=os.path.relpath(files[-1],
-                                                                                           os.path.dirname(files[0])))
+    root = os.path.dirname(os.path.abspath(__file__))
+    return r.get('hbm_bytes'), dict(fp64_flops=r.get('fp64_flops'), source=os.path.relpath(files[-1], root))
 
 
 def _group(C):
