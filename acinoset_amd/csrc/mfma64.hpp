@@ -59,34 +59,44 @@ __device__ void wg_gj_inverse(double* A, int lda, int nb, double* tmp, int* bad)
   const int li = lane & 15, lk = lane >> 4;
   for (int k = 0; k < nb; ++k) {
     double* Akk = A + (size_t)(k << 4) * lda + (k << 4);
-    // 1. 16x16 diagonal block: unblocked Gauss-Jordan, one entry per thread, double buffer
-    const int i = tid >> 4, j = tid & 15;
-    if (tid < 256) tmp[tid] = Akk[i * lda + j];
-    __syncthreads();
-    for (int s = 0; s < 16; ++s) {
-      const double* cur = tmp + ((s & 1) << 8);
-      double* nxt = tmp + (((s + 1) & 1) << 8);
-      if (tid < 256) {
-        double p = cur[s * 16 + s];
+    // 1. 16x16 diagonal block: unblocked Gauss-Jordan by wave 0 in registers (lane l holds
+    //    column l & 15 of rows (l >> 4) + 4q); pivot row / column travel by shuffles, so the
+    //    16 steps need no workgroup barrier. Same arithmetic as an entry-per-thread version.
+    if (wave == 0) {
+      const int r0 = lane >> 4, c = lane & 15;
+      double v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = Akk[(r0 + 4 * q) * lda + c];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int qs = s >> 2, rs = s & 3;
+        double p = __shfl(v[qs], rs * 16 + s);          // A[s][s]
+        const double asc = __shfl(v[qs], rs * 16 + c);  // A[s][c]
+        double ais[4];                                  // A[i][s], i = r0 + 4q
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ais[q] = __shfl(v[q], r0 * 16 + s);
         if (SPD ? !(p > 0.0) : !(fabs(p) > 1e-300)) {
-          if (bad && i == 0 && j == 0) atomicAdd(bad, 1);
+          if (bad && lane == 0) atomicAdd(bad, 1);
           p = 1e-300;
         }
         const double ip = 1.0 / p;
-        double v;
-        if (i == s && j == s)
-          v = ip;
-        else if (i == s)
-          v = cur[s * 16 + j] * ip;
-        else if (j == s)
-          v = -cur[i * 16 + s] * ip;
-        else
-          v = cur[i * 16 + j] - cur[i * 16 + s] * cur[s * 16 + j] * ip;
-        nxt[tid] = v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = r0 + 4 * q;
+          if (i == s && c == s)
+            v[q] = ip;
+          else if (i == s)
+            v[q] = asc * ip;
+          else if (c == s)
+            v[q] = -ais[q] * ip;
+          else
+            v[q] = v[q] - ais[q] * asc * ip;
+        }
       }
-      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Akk[(r0 + 4 * q) * lda + c] = v[q];
     }
-    if (tid < 256) Akk[i * lda + j] = tmp[tid];  // 16 steps: result in buffer 0
+    (void)tmp;
     __syncthreads();
     // 2. row panel A_kJ <- Akk^-1 A_kJ (J != k); each tile read and written by one wave
     for (int J = wave; J < nb; J += nw) {
