@@ -27,6 +27,7 @@ LIB_PATH = os.environ.get('ACINOSET_HIP_LIB', os.path.join(_HERE, 'libacinoset_h
 ACS_DEVICE_PTRS = 1
 ACS_CAM_STRIDE = 20
 STATUS_NAMES = ('running', 'gtol', 'ftol', 'xtol', 'stalled', 'maxiter', 'noobs')
+SD_MODES = {'const': 0, 'variable': 1}        # src/core/fte.py:35 shutter_delay_mode
 
 # exported symbols (checked by tests against include/acinoset_hip.h)
 SYMBOLS = (
@@ -420,44 +421,60 @@ class Context:
         reals = np.ascontiguousarray(table.reals, np.float64)
         return ints, reals, cams, meas, w, qinv, N, Cn
 
+    @staticmethod
+    def _tau_init(tau, N, Cn, sd_mode):
+        """Shutter delays in the layout of sd_mode (0 const: (C,), 1 variable: (N, C)),
+        camera 0 pinned at 0 (src/core/fte.py:304-308)."""
+        shape = (N, Cn) if sd_mode == 1 else (Cn,)
+        t = np.zeros(shape) if tau is None else np.array(np.broadcast_to(_c64(tau), shape), np.float64)
+        t[..., 0] = 0.0
+        return np.ascontiguousarray(t)
+
     def fte_solve(self, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutter_delay=True, intermode=1,
-                  opts=None):
+                  opts=None, sd_mode=0):
+        """sd_mode 0 = 'const' (tau (C,)), 1 = 'variable' (tau (N, C), src/core/fte.py:236-238)."""
         ints, reals, cams, meas, w, qinv, N, Cn = self._fte_args(table, cams, meas, w, Ts, qinv, shutter_delay,
                                                                  intermode)
+        sd_mode = SD_MODES.get(sd_mode, sd_mode)
         X = _c64(X0).reshape(N + 2, table.P).copy()
-        tau = np.zeros(Cn) if tau0 is None else _c64(tau0).copy()
+        tau = self._tau_init(tau0, N, Cn, sd_mode)
         rep = FteReport()
         opts = opts or self.fte_default_opts()
         self.check(self.lib.acs_fte_solve(self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), _ptr(cams), Cn,
-                                          _ptr(meas), _ptr(w), N, int(bool(shutter_delay)), float(Ts), _ptr(qinv), 0,
-                                          int(intermode), _ptr(X), _ptr(tau), C.byref(opts), C.byref(rep), 0),
-                   'acs_fte_solve')
+                                          _ptr(meas), _ptr(w), N, int(bool(shutter_delay)), float(Ts), _ptr(qinv),
+                                          int(sd_mode), int(intermode), _ptr(X), _ptr(tau), C.byref(opts),
+                                          C.byref(rep), 0), 'acs_fte_solve')
         return X, tau, rep.as_dict()
 
     def fte_solve_dev(self, table_ints_p, n_ints, table_reals_p, n_reals, cams_p, n_cams, meas_p, w_p, N,
-                      shutter_delay, Ts, qinv_p, intermode, X_p, tau_p, opts=None):
+                      shutter_delay, Ts, qinv_p, intermode, X_p, tau_p, opts=None, sd_mode=0):
         """Device-pointer variant (all arrays resident in HBM); returns the report."""
+        sd_mode = SD_MODES.get(sd_mode, sd_mode)
         rep = FteReport()
         opts = opts or self.fte_default_opts()
         self.check(self.lib.acs_fte_solve(self.h, C.c_void_p(table_ints_p), n_ints, C.c_void_p(table_reals_p), n_reals,
                                           C.c_void_p(cams_p), n_cams, C.c_void_p(meas_p), C.c_void_p(w_p), N,
-                                          int(bool(shutter_delay)), float(Ts), C.c_void_p(qinv_p), 0, int(intermode),
+                                          int(bool(shutter_delay)), float(Ts), C.c_void_p(qinv_p), int(sd_mode),
+                                          int(intermode),
                                           C.c_void_p(X_p), C.c_void_p(tau_p), C.byref(opts), C.byref(rep),
                                           ACS_DEVICE_PTRS), 'acs_fte_solve')
         return rep.as_dict()
 
-    def fte_eval(self, table, cams, meas, w, Ts, qinv, X, tau=None, shutter_delay=True, intermode=1, hessian=True):
+    def fte_eval(self, table, cams, meas, w, Ts, qinv, X, tau=None, shutter_delay=True, intermode=1, hessian=True,
+                 sd_mode=0):
         ints, reals, cams, meas, w, qinv, N, Cn = self._fte_args(table, cams, meas, w, Ts, qinv, shutter_delay,
                                                                  intermode)
+        sd_mode = SD_MODES.get(sd_mode, sd_mode)
         X = _c64(X).reshape(N + 2, table.P)
-        tau = np.zeros(Cn) if tau is None else _c64(tau)
-        nv = (N + 2) * table.P + (Cn if shutter_delay else 0)
+        tau = np.zeros((N, Cn) if sd_mode == 1 else Cn) if tau is None else _c64(tau)
+        nv = (N + 2) * table.P + ((N * Cn if sd_mode == 1 else Cn) if shutter_delay else 0)
         cost = np.empty(3)
         grad = np.empty(nv)
         H = np.empty((nv, nv)) if hessian else None
         self.check(self.lib.acs_fte_eval(self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), _ptr(cams), Cn,
-                                         _ptr(meas), _ptr(w), N, int(bool(shutter_delay)), float(Ts), _ptr(qinv), 0,
-                                         int(intermode), _ptr(X), _ptr(tau), _ptr(cost), _ptr(grad), _ptr(H), 0),
+                                         _ptr(meas), _ptr(w), N, int(bool(shutter_delay)), float(Ts), _ptr(qinv),
+                                         int(sd_mode), int(intermode), _ptr(X), _ptr(tau), _ptr(cost), _ptr(grad),
+                                         _ptr(H), 0),
                    'acs_fte_eval')
         return cost, grad, H
 

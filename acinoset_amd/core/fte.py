@@ -83,13 +83,18 @@ def states_from_solution(X, tau, Ts, shutter_delay, N):
     ddx = (X[2:] - 2 * X[1:-1] + X[:-2]) / (Ts * Ts)
     states = dict(x=x.tolist(), dx=dx.tolist(), ddx=ddx.tolist())
     if shutter_delay:
-        states['shutter_delay'] = [[float(t)] * N for t in tau]
+        tau = np.asarray(tau, np.float64)
+        if tau.ndim == 2:      # variable mode: tau (N, C) -> [[tau[n, c] for n] for c] (:553-554)
+            states['shutter_delay'] = tau.T.tolist()
+        else:                  # const mode: [[tau[c]] * N for c] (:551-552)
+            states['shutter_delay'] = [[float(t)] * N for t in tau]
     return states
 
 
 def solve(meas, w, camera_params, mode, fps, X0, shutter_delay=True, interpolation_mode='vel', tau0=None,
-          ctx=None, **opts):
-    """Array-level FTE solve. meas (N,C,L,2), w (N,C,L); returns (X (N+2,P), tau (C), report)."""
+          ctx=None, shutter_delay_mode='const', **opts):
+    """Array-level FTE solve. meas (N,C,L,2), w (N,C,L); returns (X (N+2,P), tau, report) with
+    tau (C,) for shutter_delay_mode 'const' and (N, C) for 'variable'."""
     k_arr, d_arr, r_arr, t_arr = camera_params[:4]
     n = len(k_arr)
     cams = _native.pack_cameras(k_arr, np.asarray(d_arr).reshape(n, 4), r_arr, np.asarray(t_arr).reshape(n, 3))
@@ -97,7 +102,7 @@ def solve(meas, w, camera_params, mode, fps, X0, shutter_delay=True, interpolati
     o = ctx.fte_default_opts(**opts)
     im = INTERMODES[interpolation_mode] if shutter_delay else 0
     return ctx.fte_solve(build_table(mode), cams, meas, w, 1.0 / float(fps), model_weights(mode), X0, tau0,
-                         shutter_delay=shutter_delay, intermode=im, opts=o)
+                         shutter_delay=shutter_delay, intermode=im, opts=o, sd_mode=shutter_delay_mode)
 
 
 def fte(OUT_DIR, points_2d_df, mode, camera_params, start_frame, end_frame, dlc_thresh, scene_fpath,
@@ -109,8 +114,6 @@ def fte(OUT_DIR, points_2d_df, mode, camera_params, start_frame, end_frame, dlc_
         assert intermode == 'vel' or intermode == 'acc'
     else:
         assert intermode == 'pos'
-    if sd and sd_mode == 'variable':
-        raise NotImplementedError("shutter_delay_mode='variable' is not implemented on the GPU path yet")
     os.makedirs(OUT_DIR, exist_ok=True)
     app.start_logging(os.path.join(OUT_DIR, 'fte.log'))
     try:
@@ -133,7 +136,7 @@ def fte(OUT_DIR, points_2d_df, mode, camera_params, start_frame, end_frame, dlc_
         print('----- Optimization (GPU LM) -----')
         t0 = time()
         X, tau, rep = solve(meas, w, (k_arr, d_arr, r_arr, t_arr), mode, params['vid_fps'], X0, sd, intermode,
-                            **solver_opts)
+                            shutter_delay_mode=sd_mode, **solver_opts)
         print(f"status {rep['status_name']}, {rep['iters']} iterations, cost {rep['cost_before']:.6e} -> "
               f"{rep['cost_after']:.6e}")
         print('\nOptimization took {0:.2f} seconds\n'.format(time() - t0))

@@ -33,8 +33,13 @@
 #define FTE_CH 32  // observations per LDS chunk (64 Jacobian rows)
 
 
+// Shutter delays: const mode (src/core/fte.py:236) has C unknowns tau_c, the border Cg = C
+// of the normal matrix; variable mode (:238) has N*C unknowns tau[k, c] (NT values, frame
+// major), each touching frame k's measurements only, so they are eliminated per frame
+// (Ct = C tau columns in the local blocks, no border: Cg = 0).
 struct FteDims {
   int N, M, P, L, C, Cg, NZ, im, nblk, BP, GR, nlev;
+  int var, Ct, NT, pad_;
   double Ts, la, lb, lc;
 };
 
@@ -67,6 +72,13 @@ __device__ __forceinline__ ShiftCoef shift_coef(int im, double tc, double Ts) {
     s.prev2 += q;
   }
   return s;
+}
+
+// A shutter delay held out of an LM step (oracle/fte.py solve / active_bounds): camera 0
+// (tau = 0, src/core/fte.py:304-308) and a delay at a bound of [-Ts, Ts] (:310-314) whose
+// descent direction -g points out of the box.
+__device__ __forceinline__ bool tau_held(double t, double g, double Ts, int c) {
+  return c == 0 || (t >= Ts && g < 0.0) || (t <= -Ts && g > 0.0);
 }
 
 __device__ __forceinline__ double loss_curv(double e, const LossOut& l) {
@@ -120,7 +132,7 @@ __global__ __launch_bounds__(256) void k_fte_linearize(FteDims d, const int* __r
   const int P = d.P, C = d.C, L = d.L;
   const int cur = force ? 0 : st->cur;
   const double* X = Xbuf + (size_t)cur * d.M * P;
-  const double* tau = taubuf + cur * C;
+  const double* tau = taubuf + (size_t)cur * d.NT + (d.var ? (size_t)k * C : 0);
   __shared__ FkShared fk;
   __shared__ double s_cam[FTE_MAXC * ACS_CAM_STRIDE];
   __shared__ double s_J[2 * FTE_CH][FTE_NZP + 1];
@@ -137,7 +149,7 @@ __global__ __launch_bounds__(256) void k_fte_linearize(FteDims d, const int* __r
     s_dx[tid] = (x0 - x1) / d.Ts;
     s_ddx[tid] = (x0 - 2.0 * x1 + x2) / (d.Ts * d.Ts);
   }
-  if (tid < C) s_tau[tid] = d.Cg ? tau[tid] : 0.0;
+  if (tid < C) s_tau[tid] = d.Ct ? tau[tid] : 0.0;
   fk_frame(s, X + f * P, fk, tid, blockDim.x);
   __syncthreads();
 
@@ -248,31 +260,56 @@ __global__ __launch_bounds__(256) void k_fte_linearize(FteDims d, const int* __r
 // 2. assembly of the banded normal matrix (row f: blocks (f, f-d), d = 0..3)
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* __restrict__ Xbuf,
+                                                      const double* __restrict__ taubuf,
                                                       const double* __restrict__ qinv,
                                                       const FteState* __restrict__ st, int force, int f0, int lo,
                                                       int hi, const double* __restrict__ Hloc,
                                                       const double* __restrict__ gloc, double* __restrict__ Ab,
                                                       double* __restrict__ gb, double* __restrict__ Bt,
-                                                      double* __restrict__ gmaxp) {
+                                                      double* __restrict__ gmaxp, double* __restrict__ Adiag) {
   // Terms are owned by the lowest X row they touch: frame k (rows k..k+2) iff lo <= k < hi,
   // model stencil m (rows m-3..m) iff lo <= m-3 < hi. The single-GPU solve owns all terms;
   // a frame-window rank owns the terms starting in its window (dist path below).
-  if (!force && (st->status != 0 || !st->relin)) return;
+  // Variable shutter delay (force == 0): the per-frame delays are eliminated here, every
+  // iteration (the damping changes): block (f, f') -= sum_c h_c h_c'^T / T_c and
+  // g_f -= sum_c h_c g_c / T_c over the frames touching row f, T_c = H_cc + lam max(H_cc,
+  // 1e-12) (oracle damping), held delays skipped; Adiag keeps the raw diagonal for k_cr_build.
+  const bool elim = d.var && !force;
+  if (!force && (st->status != 0 || (!st->relin && !elim))) return;
   const int f = blockIdx.x + f0;
   const int tid = threadIdx.x, nth = blockDim.x;
-  const int P = d.P, Cg = d.Cg, N = d.N;
+  const int P = d.P, Cg = d.Cg, N = d.N, C = d.C;
   const int cur = force ? 0 : st->cur;
   const double* X = Xbuf + (size_t)cur * d.M * P;
   double* A = Ab + (size_t)f * 4 * P * P;
   double* g = gb + (size_t)f * P;
   double* B = Bt + (size_t)f * P * Cg;
   __shared__ double s_red[256];
+  __shared__ double s_ti[3][FTE_MAXC], s_tg[3][FTE_MAXC];
   for (int i = tid; i < 4 * P * P; i += nth) A[i] = 0.0;
   for (int i = tid; i < P * Cg; i += nth) B[i] = 0.0;
   for (int i = tid; i < P; i += nth) g[i] = 0.0;
-  __syncthreads();
   const int kown = f - 2, kprev = f - 1, kprev2 = f;
   auto owned = [&](int k) { return k >= 0 && k < N && k >= lo && k < hi; };
+  if (d.var && tid < 3 * C) {
+    // j = 0, 1, 2: frames kown, kprev, kprev2
+    const int j = tid / C, c = tid - j * C, k = f - 2 + j;
+    double ti = 0.0, tg = 0.0;
+    if (owned(k)) {
+      const double* H = Hloc + (size_t)k * FTE_NZP * FTE_NZP;
+      const double t = taubuf[(size_t)cur * d.NT + (size_t)k * C + c];
+      tg = gloc[(size_t)k * FTE_NZP + P + 6 + c];
+      if (tau_held(t, tg, d.Ts, c)) {
+        tg = 0.0;
+      } else if (elim) {
+        const double h = H[(P + 6 + c) * FTE_NZP + P + 6 + c];
+        ti = 1.0 / (h + st->lam * fmax(h, 1e-12));
+      }
+    }
+    s_ti[j][c] = ti;
+    s_tg[j][c] = tg;
+  }
+  __syncthreads();
   if (owned(kown)) {
     const double* H = Hloc + (size_t)kown * FTE_NZP * FTE_NZP;
     for (int i = tid; i < P * P; i += nth) {
@@ -337,8 +374,56 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
   __syncthreads();
   double mx = 0.0;
   for (int i = tid; i < P; i += nth) mx = fmax(mx, fabs(g[i]));
+  if (d.var)
+    for (int c = tid; c < C; c += nth) mx = fmax(mx, fabs(s_tg[0][c]));  // each frame once (kown)
   mx = block_max(mx, s_red);
   if (tid == 0) gmaxp[f] = mx;
+  if (!elim) return;
+  for (int i = tid; i < P; i += nth) Adiag[(size_t)f * P + i] = A[i * P + i];
+  __syncthreads();
+  // Schur terms of the delays of frame k: rows / columns i, j of its local block
+  auto corr = [&](const double* H, int jj, int i, int j) {
+    double v = 0.0;
+    for (int c = 1; c < C; ++c) v += s_ti[jj][c] * H[i * FTE_NZP + P + 6 + c] * H[j * FTE_NZP + P + 6 + c];
+    return v;
+  };
+  auto gcorr = [&](const double* H, int jj, int i) {
+    double v = 0.0;
+    for (int c = 1; c < C; ++c) v += s_ti[jj][c] * H[i * FTE_NZP + P + 6 + c] * s_tg[jj][c];
+    return v;
+  };
+  if (owned(kown)) {
+    const double* H = Hloc + (size_t)kown * FTE_NZP * FTE_NZP;
+    for (int i = tid; i < P * P; i += nth) {
+      const int r = i / P, c = i % P;
+      A[r * P + c] -= corr(H, 0, r, c);
+    }
+    for (int i = tid; i < P * 3; i += nth) {
+      const int r = i / 3, c = i % 3;
+      A[1 * P * P + r * P + c] -= corr(H, 0, r, P + c);
+      A[2 * P * P + r * P + c] -= corr(H, 0, r, P + 3 + c);
+    }
+    for (int i = tid; i < P; i += nth) g[i] -= gcorr(H, 0, i);
+  }
+  __syncthreads();
+  if (owned(kprev)) {
+    const double* H = Hloc + (size_t)kprev * FTE_NZP * FTE_NZP;
+    for (int i = tid; i < 9; i += nth) {
+      const int r = i / 3, c = i % 3;
+      A[r * P + c] -= corr(H, 1, P + r, P + c);
+      A[1 * P * P + r * P + c] -= corr(H, 1, P + r, P + 3 + c);
+    }
+    for (int i = tid; i < 3; i += nth) g[i] -= gcorr(H, 1, P + i);
+  }
+  __syncthreads();
+  if (owned(kprev2)) {
+    const double* H = Hloc + (size_t)kprev2 * FTE_NZP * FTE_NZP;
+    for (int i = tid; i < 9; i += nth) {
+      const int r = i / 3, c = i % 3;
+      A[r * P + c] -= corr(H, 2, P + 3 + r, P + 3 + c);
+    }
+    for (int i = tid; i < 3; i += nth) g[i] -= gcorr(H, 2, P + 3 + i);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -365,7 +450,7 @@ __global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __r
                                                   const double* __restrict__ Ab, const double* __restrict__ gb,
                                                   const double* __restrict__ Bt, double* __restrict__ Dc,
                                                   double* __restrict__ Ec, double* __restrict__ GBc, int b0,
-                                                  int end_l, int end_r) {
+                                                  int end_l, int end_r, const double* __restrict__ Adiag) {
   if (st->status != 0) return;
   const int i = blockIdx.x + b0;
   const bool damp = i != end_l && i != end_r;  // chain ends are damped in the reduced system
@@ -384,7 +469,7 @@ __global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __r
     if (rin && cin) {
       v = (ar >= ac) ? Ab[(size_t)fr * 4 * PP + (ar - ac) * PP + pr * P + pc]
                      : Ab[(size_t)fc * 4 * PP + (ac - ar) * PP + pc * P + pr];
-      if (r == c && damp) v += lam * fmax(v, 1e-12);
+      if (r == c && damp) v += lam * fmax(Adiag ? Adiag[(size_t)fr * P + pr] : v, 1e-12);
     } else if (r == c) {
       v = 1.0;  // padding: identity
     }
@@ -565,8 +650,9 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
 
 __global__ __launch_bounds__(256) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ Dc,
                                                 const double* __restrict__ GBc, const double* __restrict__ part,
-                                                const double* __restrict__ gmaxp, double* __restrict__ dcv,
-                                                double* __restrict__ dtau, int* __restrict__ bad) {
+                                                const double* __restrict__ gmaxp, const double* __restrict__ taubuf,
+                                                double* __restrict__ dcv, double* __restrict__ dtau,
+                                                int* __restrict__ bad) {
   if (st->status != 0) return;
   const int tid = threadIdx.x, nth = blockDim.x;
   const int P = d.P, BP = d.BP, GR = d.GR, Cg = d.Cg;
@@ -580,17 +666,21 @@ __global__ __launch_bounds__(256) void k_cr_top(FteDims d, FteState* __restrict_
   // chunk partials -> sums (fixed order)
   const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
   __shared__ double s_sum[16 * 16 + 16 + 32 * 32];
+  __shared__ int s_held[32];
   for (int e = tid; e < nE; e += nth) {
     double v = 0.0;
     for (int ch = 0; ch < CR_NCHUNK; ++ch) v += part[(size_t)ch * nE + e];
     s_sum[e] = v;
   }
   __syncthreads();
-  // gradient max (frames + tau border)
+  if (tid < 32) s_held[tid] = tid >= Cg || tau_held(taubuf[(size_t)st->cur * d.NT + tid], s_sum[nH + tid], d.Ts, tid);
+  __syncthreads();
+  // gradient max (frames + free tau border)
   {
     double mx = 0.0;
     for (int f = tid; f < d.M; f += nth) mx = fmax(mx, gmaxp[f]);
-    for (int c = 1 + tid; c < Cg; c += nth) mx = fmax(mx, fabs(s_sum[nH + c]));
+    for (int c = tid; c < Cg; c += nth)
+      if (!s_held[c]) mx = fmax(mx, fabs(s_sum[nH + c]));
     mx = block_max(mx, s_red);
     if (tid == 0) st->gmax = mx;
   }
@@ -617,19 +707,19 @@ __global__ __launch_bounds__(256) void k_cr_top(FteDims d, FteState* __restrict_
       }
     }
     __syncthreads();
-    if (tid < GR) sr[tid] = (tid > 0 && tid < Cg) ? sS[tid * GR + Cg] : 0.0;
+    if (tid < GR) sr[tid] = (tid < Cg && !s_held[tid]) ? sS[tid * GR + Cg] : 0.0;
     __syncthreads();
-    // pin tau_0 and the padding (identity rows / columns)
+    // pin tau_0, the held delays and the padding (identity rows / columns)
     for (int e = tid; e < GR * GR; e += nth) {
       const int r = e / GR, c = e % GR;
-      if (r >= Cg || c >= Cg || r == 0 || c == 0) sS[e] = (r == c) ? 1.0 : 0.0;
+      if (r >= Cg || c >= Cg || s_held[r] || s_held[c]) sS[e] = (r == c) ? 1.0 : 0.0;
     }
     __syncthreads();
     wg_spd_inverse(sS, GR, GR >> 4, tmp, bad);
     if (tid < GR) {
       double v = 0.0;
       for (int c = 0; c < GR; ++c) v += sS[tid * GR + c] * sr[c];
-      dtau[tid] = (tid < Cg && tid > 0) ? v : 0.0;
+      dtau[tid] = (tid < Cg && !s_held[tid]) ? v : 0.0;
     }
     __syncthreads();
   }
@@ -667,9 +757,12 @@ __global__ __launch_bounds__(256) void k_cr_back(FteDims d, int s, int a0, int b
   }
 }
 
-// trial state X + delta, tau + dtau (clipped), norm partials per super-block
+// trial state X + delta, tau + dtau (clipped), norm partials per super-block. Variable
+// shutter delay: block i back-substitutes the delays of frames 3i-2..3i (X rows 3i..3i+2),
+// dtau[k, c] = -(g_c + h_c^T dx_k) / T_c over the local unknowns of frame k.
 __global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __restrict__ st,
                                                   const double* __restrict__ dcv, const double* __restrict__ dtau,
+                                                  const double* __restrict__ Hloc, const double* __restrict__ gloc,
                                                   double* __restrict__ Xbuf, double* __restrict__ taubuf,
                                                   double* __restrict__ normp) {
   if (st->status != 0) return;
@@ -690,13 +783,40 @@ __global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __r
     xn += x * x;
   }
   if (i == 0 && d.Cg) {
-    const double* tau = taubuf + cur * d.C;
-    double* taun = taubuf + (cur ^ 1) * d.C;
+    const double* tau = taubuf + cur * d.NT;
+    double* taun = taubuf + (cur ^ 1) * d.NT;
     for (int c = threadIdx.x; c < d.C; c += blockDim.x) {
       const double dv = (c == 0) ? 0.0 : dtau[c];
       taun[c] = (c == 0) ? 0.0 : fmin(fmax(tau[c] + dv, -d.Ts), d.Ts);
       dn += dv * dv;
       xn += tau[c] * tau[c];
+    }
+  }
+  if (d.var) {
+    const int C = d.C;
+    const double* tau = taubuf + (size_t)cur * d.NT;
+    double* taun = taubuf + (size_t)(cur ^ 1) * d.NT;
+    const double lam = st->lam;
+    for (int e = threadIdx.x; e < 3 * C; e += blockDim.x) {
+      const int k = 3 * i - 2 + e / C, c = e % C;
+      if (k < 0 || k >= d.N) continue;
+      const double* H = Hloc + (size_t)k * FTE_NZP * FTE_NZP + (size_t)(P + 6 + c) * FTE_NZP;
+      const double t = tau[(size_t)k * C + c], gc = gloc[(size_t)k * FTE_NZP + P + 6 + c];
+      double dv = 0.0;
+      if (!tau_held(t, gc, d.Ts, c)) {
+        const int f = k + 2;
+        double v = gc;
+        for (int j = 0; j < P + 6; ++j) {
+          const int row = j < P ? f : (j < P + 3 ? f - 1 : f - 2);
+          const int p = j < P ? j : (j < P + 3 ? j - P : j - P - 3);
+          v += H[j] * dcv[(size_t)(row / 3) * BP + (row % 3) * P + p];
+        }
+        const double h = H[P + 6 + c];
+        dv = -v / (h + lam * fmax(h, 1e-12));
+      }
+      taun[(size_t)k * C + c] = (c == 0) ? 0.0 : fmin(fmax(t + dv, -d.Ts), d.Ts);
+      dn += dv * dv;
+      xn += t * t;
     }
   }
   dn = block_sum(dn, s_red);
@@ -726,7 +846,7 @@ __global__ __launch_bounds__(64) void k_fte_cost(FteDims d, const int* __restric
   const int P = d.P, C = d.C, L = d.L;
   const int buf = which == 1 ? (st->cur ^ 1) : st->cur;
   const double* X = Xbuf + (size_t)buf * d.M * P;
-  const double* tau = taubuf + buf * C;
+  const double* tau = taubuf + (size_t)buf * d.NT + (d.var ? (size_t)k * C : 0);
   __shared__ FkShared fk;
   __shared__ double s_red[64];
   __shared__ double s_dx[3], s_ddx[3];
@@ -743,7 +863,7 @@ __global__ __launch_bounds__(64) void k_fte_cost(FteDims d, const int* __restric
   for (int o = own_meas ? tid : C * L; o < C * L; o += blockDim.x) {
     const int c = o / L, l = o - (o / L) * L;
     const int node = s.outn[l];
-    const double tc = d.Cg ? tau[c] : 0.0;
+    const double tc = d.Ct ? tau[c] : 0.0;
     double p[3];
     for (int i = 0; i < 3; ++i) {
       p[i] = fk.pos[node][i];
@@ -841,6 +961,7 @@ struct FteBuffers {
   int* I;
   double *Rl, *cams, *meas, *w, *qinv, *X, *tau;
   double *Hloc, *gloc, *Floc, *Ab, *gb, *Bt, *gmaxp, *Dc, *Ec, *GBc, *Wc, *Tau, *dcv, *dtau, *normp, *Fm, *Fq, *part;
+  double* Adiag;
   int* bad;
   FteState* st;
 };
@@ -856,8 +977,9 @@ struct FteSetup {
 // several of which may share a context).
 static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
                      int64_t n_reals, const double* cams, int32_t n_cams, const double* meas, const double* w,
-                     int32_t N, int32_t sd, double Ts, const double* qinv, int32_t intermode, const double* X,
-                     const double* tau, double la, double lb, double lc, uint32_t flags, void** owned = nullptr) {
+                     int32_t N, int32_t sd, double Ts, const double* qinv, int32_t sd_mode, int32_t intermode,
+                     const double* X, const double* tau, double la, double lb, double lc, uint32_t flags,
+                     void** owned = nullptr) {
   int hdr[FK_HDR];
   if (flags & ACS_DEVICE_PTRS)
     ACS_HIP(ctx, hipMemcpy(hdr, skel_ints, sizeof(hdr), hipMemcpyDeviceToHost));
@@ -871,14 +993,19 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   ACS_CHECK(ctx, intermode >= 0 && intermode <= 2 && (sd ? intermode >= 1 : intermode == 0),
             "fte: shutter_delay=%d needs intermode %s (got %d), as src/core/fte.py:44-48", sd,
             sd ? "vel/acc" : "pos", intermode);
+  ACS_CHECK(ctx, sd_mode == 0 || sd_mode == 1, "fte: shutter_delay_mode %d (0 const, 1 variable)", sd_mode);
   FteDims& d = S.d;
   d.N = N;
   d.M = N + 2;
   d.P = P;
   d.L = L;
   d.C = n_cams;
-  d.Cg = sd ? n_cams : 0;
-  d.NZ = P + 6 + d.Cg;
+  d.var = sd && sd_mode == 1;
+  d.Ct = sd ? n_cams : 0;
+  d.Cg = sd && !d.var ? n_cams : 0;
+  d.NT = d.var ? N * n_cams : n_cams;
+  d.pad_ = 0;
+  d.NZ = P + 6 + d.Ct;
   ACS_CHECK(ctx, d.NZ <= FTE_NZP, "fte: P + 6 + C = %d exceeds %d", d.NZ, FTE_NZP);
   d.im = intermode;
   d.Ts = Ts;
@@ -900,7 +1027,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
     return o;
   };
   const size_t Cg1 = d.Cg ? d.Cg : 1;
-  const size_t oX = take((size_t)2 * M * P), oT = take(2 * C), oH = take((size_t)N * FTE_NZP * FTE_NZP),
+  const size_t oX = take((size_t)2 * M * P), oT = take(2 * (size_t)d.NT), oAd = take((size_t)M * P), oH = take((size_t)N * FTE_NZP * FTE_NZP),
                og = take((size_t)N * FTE_NZP), oF = take(N), oAb = take((size_t)M * 4 * P * P),
                ogb = take((size_t)M * P), oBt = take((size_t)M * P * Cg1), ogm = take(M),
                oD = take((size_t)n * BP * BP), oE = take((size_t)n * BP * BP), oG = take((size_t)n * BP * GR),
@@ -951,6 +1078,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   }
   b.X = arena + oX;
   b.tau = arena + oT;
+  b.Adiag = arena + oAd;
   b.Hloc = arena + oH;
   b.gloc = arena + og;
   b.Floc = arena + oF;
@@ -973,10 +1101,10 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.bad = (int*)(arena + oint);
   ACS_HIP(ctx, hipMemcpyAsync(b.X, X, sizeof(double) * M * P, kin, s));
   if (tau)
-    ACS_HIP(ctx, hipMemcpyAsync(b.tau, tau, sizeof(double) * C, kin, s));
+    ACS_HIP(ctx, hipMemcpyAsync(b.tau, tau, sizeof(double) * d.NT, kin, s));
   else
-    ACS_HIP(ctx, hipMemsetAsync(b.tau, 0, sizeof(double) * C, s));
-  ACS_HIP(ctx, hipMemsetAsync(b.tau + C, 0, sizeof(double) * C, s));
+    ACS_HIP(ctx, hipMemsetAsync(b.tau, 0, sizeof(double) * d.NT, s));
+  ACS_HIP(ctx, hipMemsetAsync(b.tau + d.NT, 0, sizeof(double) * d.NT, s));
   ACS_HIP(ctx, hipMemcpyAsync(b.X + (size_t)M * P, b.X, sizeof(double) * M * P, hipMemcpyDeviceToDevice, s));
   ACS_HIP(ctx, hipMemsetAsync(b.bad, 0, sizeof(int), s));
   ACS_HIP(ctx, hipMemsetAsync(b.dtau, 0, sizeof(double) * GR, s));
@@ -988,8 +1116,8 @@ static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
   FteBuffers& b = S.b;
   hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
                      b.st, force, 0, b.Hloc, b.gloc, b.Floc);
-  hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.qinv, b.st, force, 0, 0, INT_MAX, b.Hloc,
-                     b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp);
+  hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, force, 0, 0, INT_MAX,
+                     b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag);
 }
 
 // one LM iteration: linearise (if the last step was accepted), cyclic-reduction solve,
@@ -1001,7 +1129,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   const size_t lds_elim = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1) + 512);
   const size_t lds_upd = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1));
   hipLaunchKernelGGL(k_cr_build, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, 0, -1,
-                     -1);
+                     -1, d.var ? b.Adiag : nullptr);
   const int bend = d.nblk - 1;
   for (int lv = 0, st = 1; lv < d.nlev; ++lv, st <<= 1) {
     const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
@@ -1012,14 +1140,15 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   }
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
                      d.N, 1, d.nblk);
-  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, d, b.st, b.Dc, b.GBc, b.part, b.gmaxp, b.dcv, b.dtau,
+  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, d, b.st, b.Dc, b.GBc, b.part, b.gmaxp, b.tau, b.dcv, b.dtau,
                      b.bad);
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
     hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(256), 0, s, d, st, 0, bend, b.st, b.Wc, b.dtau, b.dcv);
   }
-  hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.X, b.tau, b.normp);
+  hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
+                     b.normp);
   hipLaunchKernelGGL(k_fte_cost, dim3(d.N), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau, b.qinv,
                      b.st, 1, 0, 0, INT_MAX, b.Fm, b.Fq);
   hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 0, b.Fm, b.Fq, b.normp);
@@ -1302,12 +1431,11 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   acs_fte_opts op;
   acs_fte_default_opts(&op);
   if (opts) op = *opts;
-  ACS_CHECK(ctx, sd_mode == 0, "fte: only shutter_delay_mode='const' (0) is implemented");
   ACS_CHECK(ctx, op.max_iters >= 0, "fte: max_iters < 0");
   FteSetup S;
   int rc;
   if ((rc = fte_setup(ctx, S, skel_ints, n_ints, skel_reals, n_reals, cams, n_cams, meas, w, n_frames, shutter_delay,
-                      Ts, qinv, intermode, X, tau, op.redesc_a, op.redesc_b, op.redesc_c, flags)))
+                      Ts, qinv, sd_mode, intermode, X, tau, op.redesc_a, op.redesc_b, op.redesc_c, flags)))
     return rc;
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
@@ -1363,7 +1491,7 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   }
   const hipMemcpyKind kout = (flags & ACS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
   ACS_HIP(ctx, hipMemcpyAsync(X, b.X + (size_t)hs.cur * d.M * d.P, sizeof(double) * d.M * d.P, kout, s));
-  if (tau) ACS_HIP(ctx, hipMemcpyAsync(tau, b.tau + hs.cur * d.C, sizeof(double) * d.C, kout, s));
+  if (tau) ACS_HIP(ctx, hipMemcpyAsync(tau, b.tau + (size_t)hs.cur * d.NT, sizeof(double) * d.NT, kout, s));
   int nbad = 0;
   ACS_HIP(ctx, hipMemcpyAsync(&nbad, b.bad, sizeof(int), hipMemcpyDeviceToHost, s));
   ACS_HIP(ctx, hipStreamSynchronize(s));
@@ -1388,12 +1516,11 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
                  const double* cams, int32_t n_cams, const double* meas, const double* w, int32_t n_frames,
                  int32_t shutter_delay, double Ts, const double* qinv, int32_t sd_mode, int32_t intermode,
                  const double* X, const double* tau, double* cost3, double* grad, double* H, uint32_t flags) {
-  ACS_CHECK(ctx, sd_mode == 0, "fte: only shutter_delay_mode='const' (0) is implemented");
   ACS_CHECK(ctx, !(flags & ACS_DEVICE_PTRS), "acs_fte_eval takes host pointers");
   FteSetup S;
   int rc;
   if ((rc = fte_setup(ctx, S, skel_ints, n_ints, skel_reals, n_reals, cams, n_cams, meas, w, n_frames, shutter_delay,
-                      Ts, qinv, intermode, X, tau, 3.0, 10.0, 20.0, 0)))
+                      Ts, qinv, sd_mode, intermode, X, tau, 3.0, 10.0, 20.0, 0)))
     return rc;
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
@@ -1417,7 +1544,7 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
   ACS_HIP(ctx, hipMemcpyAsync(Fm.data(), b.Fm, sizeof(double) * N, hipMemcpyDeviceToHost, s));
   ACS_HIP(ctx, hipMemcpyAsync(Fq.data(), b.Fq, sizeof(double) * N, hipMemcpyDeviceToHost, s));
   ACS_HIP(ctx, hipStreamSynchronize(s));
-  const int nv = M * P + Cg;
+  const int C = d.C, nv = M * P + (d.var ? N * C : Cg);
   double fm = 0.0, fq = 0.0;
   for (int k = 0; k < N; ++k) {
     fm += Fm[k];
@@ -1435,6 +1562,9 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
       for (int k = 0; k < N; ++k) v += gl[(size_t)k * FTE_NZP + P + 6 + c];
       grad[M * P + c] = v;
     }
+    if (d.var)
+      for (int k = 0; k < N; ++k)
+        for (int c = 0; c < C; ++c) grad[M * P + k * C + c] = gl[(size_t)k * FTE_NZP + P + 6 + c];
   }
   if (H) {
     std::memset(H, 0, sizeof(double) * (size_t)nv * nv);
@@ -1459,6 +1589,24 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
         for (int k = 0; k < N; ++k) v += Hl[(size_t)k * FTE_NZP * FTE_NZP + (P + 6 + r) * FTE_NZP + P + 6 + c];
         H[(size_t)(M * P + r) * nv + M * P + c] = v;
       }
+    if (d.var) {
+      // frame k's delays couple with its local unknowns: X_{k+2} (all), X_{k+1}, X_k (xyz)
+      for (int k = 0; k < N; ++k) {
+        const double* Hk = Hl.data() + (size_t)k * FTE_NZP * FTE_NZP;
+        for (int c = 0; c < C; ++c) {
+          const size_t tc = (size_t)M * P + (size_t)k * C + c;
+          for (int j = 0; j < P + 6; ++j) {
+            const int row = j < P ? k + 2 : (j < P + 3 ? k + 1 : k);
+            const int p = j < P ? j : (j < P + 3 ? j - P : j - P - 3);
+            const double v = Hk[j * FTE_NZP + P + 6 + c];
+            H[(size_t)(row * P + p) * nv + tc] += v;
+            H[tc * nv + row * P + p] += v;
+          }
+          for (int c2 = 0; c2 < C; ++c2)
+            H[tc * nv + M * P + (size_t)k * C + c2] = Hk[(P + 6 + c) * FTE_NZP + P + 6 + c2];
+        }
+      }
+    }
   }
   return ACS_OK;
 }
@@ -1478,14 +1626,15 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
   acs_fte_opts op;
   acs_fte_default_opts(&op);
   if (opts) op = *opts;
-  ACS_CHECK(ctx, sd_mode == 0, "fte: only shutter_delay_mode='const' (0) is implemented");
+  ACS_CHECK(ctx, sd_mode == 0 || !shutter_delay,
+            "fte_dist: shutter_delay_mode='variable' runs on one GPU (acs_fte_solve)");
   ACS_CHECK(ctx, op.max_iters >= 0, "fte: max_iters < 0");
   ACS_CHECK(ctx, world >= 1 && world <= 1024 && rank >= 0 && rank < world, "fte_dist: rank %d / world %d", rank,
             world);
   acs_fte_dist* h = new acs_fte_dist();
   h->ctx = ctx;
   int rc = fte_setup(ctx, h->S, skel_ints, n_ints, skel_reals, n_reals, cams, n_cams, meas, w, n_frames,
-                     shutter_delay, Ts, qinv, intermode, X, tau, op.redesc_a, op.redesc_b, op.redesc_c, flags, &h->own);
+                     shutter_delay, Ts, qinv, sd_mode, intermode, X, tau, op.redesc_a, op.redesc_b, op.redesc_c, flags, &h->own);
   if (rc) {
     if (h->own) (void)hipFree(h->own);
     delete h;
@@ -1597,11 +1746,11 @@ int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
     if (h->k_hi > h->k_lo)
       hipLaunchKernelGGL(k_fte_linearize, dim3(h->k_hi - h->k_lo), dim3(256), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w,
                          b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc);
-    hipLaunchKernelGGL(k_fte_assemble, dim3(h->f_hi - h->f_lo), dim3(256), 0, s, d, b.X, b.qinv, b.st, 0, h->f_lo,
-                       h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp);
+    hipLaunchKernelGGL(k_fte_assemble, dim3(h->f_hi - h->f_lo), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, 0,
+                       h->f_lo, h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag);
     const int top = std::min(h->bend, d.nblk - 1);
     hipLaunchKernelGGL(k_cr_build, dim3(top - h->a0 + 1), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec,
-                       b.GBc, h->a0, h->a0, h->bend);
+                       b.GBc, h->a0, h->a0, h->bend, nullptr);
     dist_local_cr(h);
     hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part,
                        h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk));
@@ -1638,7 +1787,8 @@ int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
                      0, 1, dr.nblk);
   const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
   hipLaunchKernelGGL(k_red_part, dim3(1), dim3(256), 0, s, nE, h->Lo, b.st, p1, r.part);
-  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, dr, b.st, r.Dc, r.GBc, r.part, r.gmaxp, r.dcv, b.dtau, b.bad);
+  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, dr, b.st, r.Dc, r.GBc, r.part, r.gmaxp, b.tau, r.dcv, b.dtau,
+                     b.bad);
   for (int lv = dr.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (dr.nblk - st + 2 * st - 1) / (2 * st);
@@ -1666,7 +1816,8 @@ int acs_fte_dist_phase3(acs_fte_dist* h, const double* p2, double* p3) {
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
   hipStream_t s = ctx->stream;
-  hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, p2, b.dtau, b.X, b.tau, b.normp);
+  hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, p2, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
+                     b.normp);
   if (h->c_hi > h->c_lo)
     hipLaunchKernelGGL(k_fte_cost, dim3(h->c_hi - h->c_lo), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
                        b.tau, b.qinv, b.st, 1, h->c_lo, h->own_lo, h->own_hi, b.Fm, b.Fq);
@@ -1699,7 +1850,7 @@ int acs_fte_dist_result(acs_fte_dist* h, double* X, double* tau, acs_fte_report*
   ACS_HIP(ctx, hipStreamSynchronize(s));
   const hipMemcpyKind kout = (flags & ACS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
   if (X) ACS_HIP(ctx, hipMemcpyAsync(X, b.X + (size_t)hs.cur * d.M * d.P, sizeof(double) * d.M * d.P, kout, s));
-  if (tau) ACS_HIP(ctx, hipMemcpyAsync(tau, b.tau + hs.cur * d.C, sizeof(double) * d.C, kout, s));
+  if (tau) ACS_HIP(ctx, hipMemcpyAsync(tau, b.tau + (size_t)hs.cur * d.NT, sizeof(double) * d.NT, kout, s));
   int nbad = 0;
   ACS_HIP(ctx, hipMemcpyAsync(&nbad, b.bad, sizeof(int), hipMemcpyDeviceToHost, s));
   ACS_HIP(ctx, hipStreamSynchronize(s));

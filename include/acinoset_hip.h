@@ -141,12 +141,14 @@ int acs_fk(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double*
 
 /* ---- a10-a13: FTE trajectory solve (src/core/fte.py:176-555) ------------------------
  * Unknowns: X ((n_frames + 2) x P, row f = frame f - 2; rows 0, 1 are the virtual frames
- * carrying the reference's free dx[1], ddx[1]) and tau (n_cams; tau[0] pinned to 0,
- * |tau| <= Ts, only when shutter_delay). meas (n_frames, n_cams, L, 2) pixels,
+ * carrying the reference's free dx[1], ddx[1]) and tau, only when shutter_delay:
+ * sd_mode 0 = 'const' (fte.py:236): tau (n_cams), tau[0] pinned to 0; sd_mode 1 =
+ * 'variable' (fte.py:238): tau (n_frames x n_cams, frame major), tau[n][0] pinned to 0;
+ * |tau| <= Ts (fte.py:304-318; a delay on the bound whose descent direction points out is
+ * held for that step). meas (n_frames, n_cams, L, 2) pixels,
  * w (n_frames, n_cams, L) = 1/R where likelihood > thresh else 0 (fte.py:210-215),
  * qinv (P) = 1/Q_p = 1/_Q[p]^2 (fte.py:113-144, 217-218). intermode 0 pos / 1 vel / 2 acc
- * (shutter_delay requires vel/acc, fte.py:44-48); sd_mode 0 = 'const' (1 'variable' is
- * not implemented yet and returns ACS_E_INVALID). X and tau are in/out.                */
+ * (shutter_delay requires vel/acc, fte.py:44-48). X and tau are in/out.                 */
 typedef struct {
   int32_t max_iters;  /* LM iterations; default 200 */
   int32_t window;     /* reserved (0) */
@@ -172,8 +174,8 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
                   const double* w, int32_t n_frames, int32_t shutter_delay, double Ts,
                   const double* qinv, int32_t sd_mode, int32_t intermode, double* X, double* tau,
                   const acs_fte_opts* opts, acs_fte_report* report, uint32_t flags);
-/* objective (cost3 = [total, measurement, model]), gradient (nv = (n_frames+2)*P + C if
- * shutter_delay) and the dense undamped GN normal matrix (nv x nv, may be NULL) at
+/* objective (cost3 = [total, measurement, model]), gradient (nv = (n_frames+2)*P + the
+ * number of delays: C const / n_frames*C variable, if shutter_delay) and the dense undamped GN normal matrix (nv x nv, may be NULL) at
  * (X, tau): the linearisation acs_fte_solve uses, exported for parity tests. Host ptrs. */
 int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
                  int64_t n_reals, const double* cams, int32_t n_cams, const double* meas,
@@ -193,7 +195,8 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
  * ~ (world+1) (2 BP^2 + BP GR) doubles; p2: the step, n_blocks x BP; p3: 2 costs). Every
  * rank runs the same reduced solve on the summed p1 and takes the same decisions; the
  * result equals acs_fte_solve up to summation order. Phases are asynchronous on the
- * context stream except phase4, which returns the LM status (0 = running).            */
+ * context stream except phase4, which returns the LM status (0 = running).
+ * shutter_delay with sd_mode 1 ('variable') is single-GPU only (ACS_E_INVALID here).   */
 typedef struct acs_fte_dist acs_fte_dist;
 int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
                         int64_t n_reals, const double* cams, int32_t n_cams, const double* meas,

@@ -16,17 +16,21 @@ Reference NLP (src/core/fte.py), frames n = 1..N, cameras c, markers l, pose par
   min  sum_{n,p} slack_model^2 / Q_p  +  sum redescending_loss(w_ncl * slack_meas, 3, 10, 20)
        Q_p = _Q[p]^2 (:113-144), w = 1/R = 1/3 if likelihood > thresh else 0 (:210-215)
   tau_1 = 0, -Ts <= tau_c <= Ts (const shutter-delay mode, :304-318)
+  variable mode (:237-238, :307-314, :449-450): tau[n, c] per frame, tau[n, 1] = 0,
+       -Ts <= tau[n, c] <= Ts, frame n's shift uses tau[n, c]
 
 Exact elimination (no penalty, no approximation): with two virtual frames x[-1], x[0]
 in front of the sequence, dx[n] = (x[n]-x[n-1])/Ts and ddx[n] = (dx[n]-dx[n-1])/Ts hold
 for every n (the free dx[1], ddx[1] of the reference map one-to-one onto the virtual
 frames), slack_model[n] = (x[n] - 3x[n-1] + 3x[n-2] - x[n-3]) / Ts^2 for n >= 2, and
-slack_model[1] (free, unconstrained) is 0 at any optimum. Unknowns: X (N+2, P) + tau (C).
+slack_model[1] (free, unconstrained) is 0 at any optimum. Unknowns: X (N+2, P) + tau (C)
+(const) or tau (N, C) (variable; flattened frame-major after X).
 
 LM spec (shared with the GPU):
   H = sum_meas max(rho''(e), rho'(e)/e, 0) w^2 dproj^T dproj + 2 D^T diag(qinv) D (model, exact)
   g = sum_meas rho'(e) w dproj + 2 D^T diag(qinv) D X
-  A = H + lam * diag(max(H_ii, 1e-12)); solve A d = -g (tau_0 pinned)
+  A = H + lam * diag(max(H_ii, 1e-12)); solve A d = -g (tau of camera 0 pinned, and every
+      tau held at a bound whose -g points outward: active set, g zeroed there)
   trial: X + d_X, tau clipped to [-Ts, Ts]; accept iff F_new < F
   accept: lam = max(lam / 10, 1e-15); reject: lam *= 10
   stop: |g|_inf <= gtol | accept & (F - F_new <= ftol*|F| or |d| <= xtol*(xtol+|X|))
@@ -55,7 +59,7 @@ def qinv_for(mode):
 
 class Problem:
     def __init__(self, mode, meas, w, K, D, R, t, Ts, sd=True, intermode='vel', a=3.0, b=10.0, c=20.0,
-                 qinv=None):
+                 qinv=None, sd_mode='const'):
         self.mode = mode
         self.meas = np.nan_to_num(np.asarray(meas, np.float64))       # (N, C, L, 2)
         self.w = np.asarray(w, np.float64)                            # (N, C, L)
@@ -69,7 +73,22 @@ class Problem:
         self.P = len(okin.POSE[mode])
         self.M = self.N + 2
         self.qinv = qinv_for(mode) if qinv is None else np.asarray(qinv, np.float64)
-        self.nv = self.M * self.P + (self.C if self.sd else 0)
+        assert sd_mode in ('const', 'variable'), sd_mode
+        self.var = sd_mode == 'variable' and self.sd
+        self.tau_shape = (self.N, self.C) if self.var else (self.C,)
+        self.nv = self.M * self.P + (int(np.prod(self.tau_shape)) if self.sd else 0)
+
+    def tau_frames(self, tau):
+        """(N, C) shutter delay of every frame (const mode: broadcast)."""
+        tau = np.asarray(tau, np.float64)
+        return tau if tau.ndim == 2 else np.broadcast_to(tau[None, :], (self.N, self.C))
+
+    def pinned(self):
+        """Indices of the unknowns fixed at 0: tau of camera 0 (src/core/fte.py:304-308)."""
+        if not self.sd:
+            return np.zeros(0, int)
+        base = self.M * self.P
+        return base + np.arange(self.N) * self.C if self.var else np.array([base])
 
     # ---- helpers --------------------------------------------------------------------
     def derivs(self, X):
@@ -84,9 +103,10 @@ class Problem:
         if self.im == 0:
             return np.zeros((self.N, self.C, 3))
         _, dx, ddx = self.derivs(X)
-        s = dx[:, None, :3] * tau[None, :, None]
+        tf = self.tau_frames(tau)
+        s = dx[:, None, :3] * tf[:, :, None]
         if self.im == 2:
-            s = s + ddx[:, None, :3] * (tau ** 2)[None, :, None]
+            s = s + ddx[:, None, :3] * (tf ** 2)[:, :, None]
         return s
 
     def model_slack(self, X):
@@ -128,6 +148,7 @@ class Problem:
         pos = okin.marker_positions(self.mode, x)                      # (N, L, 3)
         Jfk = okin.marker_jacobian(self.mode, x)                       # (N, L, 3, P)
         shift = self.shift(X, tau)
+        tf = self.tau_frames(tau) if self.sd else np.zeros((N, C))
         rows, cols, vals = [], [], []
         grad = np.zeros(self.nv)
         F_meas = 0.0
@@ -146,7 +167,7 @@ class Problem:
             gs = d1 * wl                                                 # scale of gradient rows
             # d proj / d x_k (own frame)
             Jown = np.einsum('nldk,nlkp->nldp', Jp, Jfk)                 # (N, L, 2, P)
-            tc = tau[c] if self.sd else 0.0
+            tc = tf[:, c, None, None, None]                              # (N, 1, 1, 1)
             a_own = a_prev = a_prev2 = 0.0
             if self.im >= 1:
                 a_own += tc / Ts
@@ -174,13 +195,14 @@ class Problem:
                 vals.append((Jb * sq[..., None]).ravel())
                 np.add.at(grad, colids.ravel(), (Jb * gs[..., None]).ravel())
             if self.sd and c > 0:
-                dtau = dx[:, None, :3] + (2 * tc * ddx[:, None, :3] if self.im == 2 else 0.0)  # (N, 1, 3)
-                Jt = np.einsum('nldk,nk->nld', Jp, dtau[:, 0])           # (N, L, 2)
-                colid = M * P + c
+                dtau = dx[:, :3] + (2 * tf[:, c, None] * ddx[:, :3] if self.im == 2 else 0.0)  # (N, 3)
+                Jt = np.einsum('nldk,nk->nld', Jp, dtau)                 # (N, L, 2)
+                colid = M * P + (np.arange(N) * C + c if self.var else np.full(N, c))
+                colid = np.broadcast_to(colid[:, None, None], ridx.shape)
                 rows.append(ridx.ravel())
-                cols.append(np.full(ridx.size, colid))
+                cols.append(colid.ravel())
                 vals.append((Jt * sq).ravel())
-                grad[colid] += (Jt * gs).sum()
+                np.add.at(grad, colid.ravel(), (Jt * gs).ravel())
         Jm = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
                            shape=(2 * N * C * L, self.nv))
         H = (Jm.T @ Jm).tocsr()
@@ -204,11 +226,11 @@ class Problem:
         return F_meas + F_model, H.tocsr(), grad
 
     def pack(self, X, tau):
-        return np.concatenate([X.ravel(), tau]) if self.sd else X.ravel()
+        return np.concatenate([X.ravel(), np.ravel(tau)]) if self.sd else X.ravel()
 
     def unpack(self, v):
         X = v[:self.M * self.P].reshape(self.M, self.P)
-        tau = v[self.M * self.P:] if self.sd else np.zeros(self.C)
+        tau = v[self.M * self.P:].reshape(self.tau_shape) if self.sd else np.zeros(self.tau_shape)
         return X, tau
 
 
@@ -249,18 +271,29 @@ def _project_jac_fte(X, K, D, R, t):
     return np.stack([u, v], -1), np.stack([Ju, Jv], -2)
 
 
+def active_bounds(prob, tau, g):
+    """Shutter delays held at a bound of -Ts <= tau <= Ts whose descent direction -g
+    points out of the box: pinned for this step (projected gradient / active set)."""
+    t = np.ravel(tau)
+    gt = g[prob.M * prob.P:]
+    act = ((t >= prob.Ts) & (gt < 0)) | ((t <= -prob.Ts) & (gt > 0))
+    return prob.M * prob.P + np.flatnonzero(act)
+
+
 def solve(prob, X0, tau0=None, max_iters=200, ftol=1e-12, xtol=1e-12, gtol=1e-8, lam0=1e-3, verbose=False):
     """LM of the module docstring. Returns (X, tau, info)."""
     X = np.array(X0, np.float64).reshape(prob.M, prob.P)
-    tau = np.zeros(prob.C) if tau0 is None else np.array(tau0, np.float64)
-    tau[0] = 0.0
+    tau = np.zeros(prob.tau_shape) if tau0 is None else np.array(tau0, np.float64).reshape(prob.tau_shape)
+    tau[..., 0] = 0.0
     F, H, g = prob.linearize(X, tau)
     F0 = F
     lam = lam0
     status, iters, n_acc = 'maxiter', 0, 0
-    pin = prob.M * prob.P if prob.sd else None
+    pin0 = prob.pinned() if prob.sd else None
+    pin = pin0
     while iters < max_iters:
-        if pin is not None:
+        if pin0 is not None:
+            pin = np.concatenate([pin0, active_bounds(prob, tau, g)])
             g[pin] = 0.0
         gmax = float(np.abs(g).max())
         if gmax <= gtol:
@@ -277,7 +310,7 @@ def solve(prob, X0, tau0=None, max_iters=200, ftol=1e-12, xtol=1e-12, gtol=1e-8,
         Xn = X + dX
         taun = np.clip(tau + dtau, -prob.Ts, prob.Ts) if prob.sd else tau
         if prob.sd:
-            taun[0] = 0.0
+            taun[..., 0] = 0.0
         Fn = prob.cost(Xn, taun)[0]
         iters += 1
         xn = np.linalg.norm(prob.pack(X, tau))

@@ -113,12 +113,19 @@ class OracleFteRank:
         graw = p1[nS * nS + 2 * nS:nS * nS + 3 * nS].copy()
         S[np.diag_indices_from(S)] += lam * np.maximum(rdiag, 1e-12)
         if self.ntau:
-            t0 = nS - self.ntau                       # tau_0 pinned (src/core/fte.py:304-318)
-            S[t0, :] = 0.0
-            S[:, t0] = 0.0
-            S[t0, t0] = 1.0
-            rhs[t0] = 0.0
-            graw[t0] = 0.0
+            # tau_0 pinned (src/core/fte.py:304-318) and the delays held at a bound
+            # (oracle/fte.py active_bounds), on the summed tau gradient
+            t0 = nS - self.ntau
+            gt = graw[t0:]
+            held = np.zeros(self.ntau, bool)
+            held[0] = True
+            held |= ((self.tau >= p.Ts) & (gt < 0)) | ((self.tau <= -p.Ts) & (gt > 0))
+            for h in t0 + np.flatnonzero(held):
+                S[h, :] = 0.0
+                S[:, h] = 0.0
+                S[h, h] = 1.0
+                rhs[h] = 0.0
+                graw[h] = 0.0
         self.gmax = max(np.abs(graw).max(), p1[nS * nS + 3 * nS:].max())
         dS = np.linalg.solve(S, rhs)
         d = np.zeros(p.nv)

@@ -110,15 +110,15 @@ def test_core_sba_end_to_end(tmp_path):
     assert os.path.exists(os.path.join(tmp_path, 'sba', 'sba.mat'))
 
 
-@pytest.mark.parametrize('mode', ['head', 'default_nolure'])
-def test_core_fte_end_to_end_matches_oracle(mode, tmp_path):
+@pytest.mark.parametrize('mode,sd_mode', [('head', 'const'), ('default_nolure', 'const'), ('head', 'variable')])
+def test_core_fte_end_to_end_matches_oracle(mode, sd_mode, tmp_path):
     scene = synth.load_scene_file()
     N = 40
     seq = synth.make_sequence(N, scene, mode=mode, seed=13, tau_max=0.003)
     df = seq.to_df()
     cp = scene.camera_params()
     out = core.fte(str(tmp_path / 'fte'), df, mode, cp, 0, N - 1, 0.5, 'scene.json', params={'vid_fps': 90.0},
-                   shutter_delay=True, shutter_delay_mode='const', interpolation_mode='vel', video=False)
+                   shutter_delay=True, shutter_delay_mode=sd_mode, interpolation_mode='vel', video=False)
     with open(out, 'rb') as f:
         st = pickle.load(f)
     assert set(['x', 'dx', 'ddx', 'shutter_delay', 'reprj_errors', 'start_frame', 'positions']) <= set(st)
@@ -126,7 +126,7 @@ def test_core_fte_end_to_end_matches_oracle(mode, tmp_path):
     # oracle from the same (reference) initialisation
     w = np.where(seq.likelihood > 0.5, 1 / 3, 0.0)
     prob = ofte.Problem(mode, np.nan_to_num(seq.uv), w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=True,
-                        intermode='vel')
+                        intermode='vel', sd_mode=sd_mode)
     tri = utils.get_pairwise_3d_points_from_df(df.query('likelihood > 0.5'), scene.K, scene.D.reshape(-1, 4),
                                                scene.R, scene.t, verbose=False)
     nose = tri[tri['marker'] == 'nose']
@@ -135,6 +135,8 @@ def test_core_fte_end_to_end_matches_oracle(mode, tmp_path):
     from oracle import kinematics as okin
     d = okin.marker_positions(mode, X) - okin.marker_positions(mode, Xo[2:])
     assert float(np.sqrt(np.mean(np.sum(d ** 2, -1)))) < 1e-6
-    np.testing.assert_allclose([s[0] for s in st['shutter_delay']], to, atol=1e-6)
+    sd_state = np.asarray(st['shutter_delay'])                     # (C, N), src/core/fte.py:551-554
+    np.testing.assert_allclose(sd_state, np.broadcast_to(to.T if to.ndim == 2 else to[:, None], sd_state.shape),
+                               atol=1e-6)
     rms = metric.reprojection_rms(st['reprj_errors'])
     assert rms < 10.0  # includes the 1 % +-30 px outliers and dropouts, as the reference metric does

@@ -1,5 +1,6 @@
 """GPU parity of the FTE trajectory solve (acs_fte_eval / acs_fte_solve) against the
-oracle restatement of src/core/fte.py (parity unpinned vs IPOPT: see oracle/fte.py).
+oracle restatement of src/core/fte.py (parity unpinned vs IPOPT: see oracle/fte.py),
+both shutter-delay modes (const: tau (C,), variable: tau (N, C), src/core/fte.py:236-238).
 
 Tolerances (float64):
   * objective: 1e-10 relative; gradient / GN normal matrix: 1e-8 relative to their max
@@ -16,11 +17,12 @@ from acinoset_amd import _native, kinematics as pkin, synth
 pytestmark = pytest.mark.gpu
 
 
-def _problem(N, mode='default_nolure', sd=True, inter='vel', seed=2, tau_max=0.004):
+def _problem(N, mode='default_nolure', sd=True, inter='vel', seed=2, tau_max=0.004, sd_mode='const'):
     scene = synth.load_scene_file()
     seq = synth.make_sequence(N, scene, mode=mode, seed=seed, tau_max=tau_max if sd else 0.0)
     w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
-    prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter)
+    prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter,
+                        sd_mode=sd_mode)
     cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
     return seq, prob, cams
 
@@ -107,3 +109,68 @@ def test_fte_rejects_bad_modes(ctx):
     X0 = np.zeros((prob.M, prob.P))
     with pytest.raises(RuntimeError):   # shutter delay with intermode 'pos' (fte.py:44-46)
         ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, shutter_delay=True, intermode=0)
+
+
+# ---- shutter_delay_mode='variable' (per-frame delays eliminated frame by frame) ---------
+@pytest.mark.parametrize('inter', ['vel', 'acc'])
+def test_fte_eval_variable_matches_oracle(ctx, inter):
+    seq, prob, cams = _problem(10, sd_mode='variable', inter=inter)
+    rng = np.random.default_rng(5)
+    X = np.concatenate([seq.x[:1], seq.x[:1], seq.x], 0) + rng.normal(0, 0.01, (prob.M, prob.P))
+    tau = rng.uniform(-0.004, 0.004, (prob.N, prob.C))
+    tau[:, 0] = 0.0
+    table = pkin.build_table(prob.mode)
+    cost, g, H = ctx.fte_eval(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X, tau, intermode=prob.im,
+                              sd_mode='variable')
+    np.testing.assert_allclose(cost, prob.cost(X, tau), rtol=1e-10)
+    Fo, Ho, go = prob.linearize(X, tau)
+    np.testing.assert_allclose(g, go, rtol=0, atol=1e-8 * np.abs(go).max())
+    Hd = Ho.toarray()
+    np.testing.assert_allclose(H, Hd, rtol=0, atol=1e-8 * np.abs(Hd).max())
+
+
+@pytest.mark.parametrize('N,iters', [(7, 1), (31, 1), (64, 1), (31, 5)])
+def test_fte_variable_lm_steps_match_oracle(ctx, N, iters):
+    """The first LM steps: per-frame delay elimination + cyclic reduction + delay
+    back-substitution = the oracle's sparse solve of the full damped system."""
+    seq, prob, cams = _problem(N, sd_mode='variable')
+    X0 = ofte.initial_state(prob, np.arange(N), seq.pos3d[:, 0, 0])
+    table = pkin.build_table(prob.mode)
+    X, tau, rep = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
+                                opts=ctx.fte_default_opts(max_iters=iters), sd_mode='variable')
+    Xo, to, info = ofte.solve(prob, X0, max_iters=iters)
+    assert tau.shape == (N, prob.C)
+    assert rep['n_bad_pivots'] == 0 and rep['iters'] == info['iters'] and rep['n_accepted'] == info['n_accepted']
+    np.testing.assert_allclose(X, Xo, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(tau, to, rtol=0, atol=1e-11)
+
+
+@pytest.mark.parametrize('mode,inter,N', [('default_nolure', 'vel', 30), ('head', 'acc', 40)])
+def test_fte_variable_solve_matches_oracle(ctx, mode, inter, N):
+    seq, prob, cams = _problem(N, mode=mode, inter=inter, sd_mode='variable')
+    X0 = ofte.initial_state(prob, np.arange(N), seq.pos3d[:, 0, 0])
+    Xo, to, info = ofte.solve(prob, X0)
+    table = pkin.build_table(mode)
+    X, tau, rep = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, intermode=prob.im,
+                                sd_mode='variable')
+    assert rep['status_name'] in ('ftol', 'xtol', 'gtol'), rep
+    assert info['status'] in ('ftol', 'xtol', 'gtol'), info
+    pg = okin.marker_positions(mode, X[2:])
+    po = okin.marker_positions(mode, Xo[2:])
+    assert float(np.sqrt(np.mean(np.sum((pg - po) ** 2, -1)))) < 1e-6
+    np.testing.assert_allclose(tau, to, atol=1e-6)
+    np.testing.assert_allclose(rep['cost_after'], info['cost_after'], rtol=1e-9, atol=1e-9)
+    assert np.all(np.abs(tau) <= prob.Ts) and np.all(tau[:, 0] == 0.0)
+
+
+def test_fte_const_delay_at_bound_matches_oracle(ctx):
+    """True delays beyond Ts: the const-mode delays end on the bound (active set)."""
+    seq, prob, cams = _problem(30, tau_max=0.03)
+    X0 = ofte.initial_state(prob, np.arange(30), seq.pos3d[:, 0, 0])
+    Xo, to, info = ofte.solve(prob, X0)
+    table = pkin.build_table(prob.mode)
+    X, tau, rep = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0)
+    assert np.any(np.abs(to) == prob.Ts)
+    assert rep['iters'] == info['iters'] and rep['status_name'] == info['status'], (rep, info)
+    np.testing.assert_allclose(X, Xo, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(tau, to, rtol=0, atol=1e-9)

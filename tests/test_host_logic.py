@@ -98,3 +98,11 @@ def test_ekf_dense_observations_pivot():
     ok = ~np.isnan(lik)
     np.testing.assert_array_equal(lik[ok], seq.likelihood[ok])
     np.testing.assert_array_equal(meas[ok], seq.uv[ok])
+
+
+def test_states_variable_shutter_delay_layout():
+    """variable mode: sd_state = [[tau[n, c] for n] for c] (src/core/fte.py:553-554)."""
+    X = np.zeros((7, 6))
+    tau = np.arange(15.0).reshape(5, 3) * 1e-4
+    st = cfte.states_from_solution(X, tau, 1 / 90, True, 5)
+    assert np.array_equal(np.asarray(st['shutter_delay']), tau.T)

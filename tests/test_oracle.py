@@ -228,3 +228,68 @@ def test_oracle_ekf_matches_reference_default_early_frames():
                    float(g['res'][0]))
     np.testing.assert_allclose(out['x_est'][:, :29], g['out_x'][:10], atol=1e-3, rtol=0)
     np.testing.assert_allclose(out['x_est'][:2, :29], g['out_x'][:2], atol=1e-8, rtol=0)
+
+
+# ---- FTE objective (parity unpinned vs IPOPT, oracle/fte.py): exact gradient and the
+# shutter-delay modes (src/core/fte.py:236-238, :304-318, :447-450)
+def _fte_small(sd_mode, inter, N=6, tau_max=0.004):
+    from oracle import fte as ofte
+    from acinoset_amd import synth
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(N, scene, mode='head', seed=2, tau_max=tau_max)
+    w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
+    prob = ofte.Problem('head', seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=True, intermode=inter,
+                        sd_mode=sd_mode)
+    return seq, prob
+
+
+@pytest.mark.parametrize('sd_mode', ['const', 'variable'])
+@pytest.mark.parametrize('inter', ['vel', 'acc'])
+def test_oracle_fte_gradient_fd(sd_mode, inter):
+    seq, prob = _fte_small(sd_mode, inter)
+    rng = np.random.default_rng(1)
+    X = np.concatenate([seq.x[:1], seq.x[:1], seq.x], 0) + rng.normal(0, 0.01, (prob.M, prob.P))
+    tau = rng.uniform(-0.003, 0.003, prob.tau_shape)
+    tau[..., 0] = 0.0
+    F, H, g = prob.linearize(X, tau)
+    assert F == prob.cost(X, tau)[0]
+    v = prob.pack(X, tau)
+    fd = np.zeros_like(v)
+    for i in range(v.size):
+        h = 1e-6 if i < prob.M * prob.P else 1e-8
+        vp, vm = v.copy(), v.copy()
+        vp[i] += h
+        vm[i] -= h
+        fd[i] = (prob.cost(*prob.unpack(vp))[0] - prob.cost(*prob.unpack(vm))[0]) / (2 * h)
+    fd[prob.pinned()] = 0.0          # camera 0's delay is not an unknown
+    np.testing.assert_allclose(g, fd, rtol=0, atol=1e-8 * np.abs(g).max())
+    assert H.shape == (prob.nv, prob.nv)
+
+
+def test_oracle_fte_variable_generalises_const():
+    """tau[n, c] = tau_c for every n gives the const-mode objective; the variable optimum
+    is at most the const one (a superset of the unknowns) and respects |tau| <= Ts."""
+    from oracle import fte as ofte
+    seq, pc = _fte_small('const', 'vel')
+    _, pv = _fte_small('variable', 'vel')
+    rng = np.random.default_rng(3)
+    X = np.concatenate([seq.x[:1], seq.x[:1], seq.x], 0) + rng.normal(0, 0.01, (pc.M, pc.P))
+    tc = np.array([0.0, 0.002, -0.001, 0.003, 0.0, -0.002])
+    assert pv.cost(X, np.tile(tc, (pv.N, 1)))[0] == pytest.approx(pc.cost(X, tc)[0], rel=1e-14)
+    X0 = ofte.initial_state(pc, np.arange(pc.N), seq.pos3d[:, 0, 0])
+    _, tc_, ic = ofte.solve(pc, X0)
+    _, tv_, iv = ofte.solve(pv, X0)
+    assert iv['status'] in ('ftol', 'xtol', 'gtol') and ic['status'] in ('ftol', 'xtol', 'gtol')
+    assert iv['cost_after'] <= ic['cost_after']
+    assert np.all(np.abs(tv_) <= pv.Ts) and np.all(tv_[:, 0] == 0.0)
+
+
+def test_oracle_fte_const_delay_at_bound():
+    """A true delay beyond Ts drives tau_c to the bound; the active-set step keeps the
+    solve converging there (held delays leave the gradient test)."""
+    from oracle import fte as ofte
+    seq, prob = _fte_small('const', 'vel', N=8, tau_max=0.03)
+    X0 = ofte.initial_state(prob, np.arange(prob.N), seq.pos3d[:, 0, 0])
+    _, tau, info = ofte.solve(prob, X0)
+    assert info['status'] in ('ftol', 'xtol', 'gtol'), info
+    assert np.any(np.abs(tau) == prob.Ts)
