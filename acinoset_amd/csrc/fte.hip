@@ -16,8 +16,9 @@
 //   k_fte_assemble   [M blocks]  block-banded (bandwidth 3) normal matrix + tau border
 //                                + exact model term (third differences)
 //   k_cr_build       [n blocks]  3-frame super-blocks (block tridiagonal) + LM damping
-//   k_cr_elim/update [log2 n levels]  block cyclic reduction: SPD block inverse by blocked
-//                                Gauss-Jordan and Schur updates, all on f64 MFMA tiles
+//   k_cr_level       [log2 n levels]  block cyclic reduction, one launch per level:
+//                                register-tiled Gauss-Jordan on [D | couplings | rhs] and the
+//                                neighbours' Schur terms, all on f64 MFMA tiles
 //   k_cr_top         [1 block ]  last block + tau border
 //   k_cr_back        [log2 n levels]  back substitution
 //   k_cr_trial       [n blocks]  trial state X + delta, tau clipped to [-Ts, Ts]
@@ -433,18 +434,46 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
 // multiple of 16; padding rows are identity). With bandwidth 3 the normal matrix is block
 // tridiagonal in super-blocks: D_i (diagonal) and E_i = T(i, i-1), plus the tau border
 // G_i and rhs b_i = -g_i packed as GB_i = [G_i | b_i] (BP x GR). Level s (= 1, 2, 4, ..)
-// eliminates the active blocks i = s(2m+1) in parallel:
-//   W_i = D_i^-1 [E_i | E_{i+s}^T | GB_i]      (blocked Gauss-Jordan + MFMA GEMMs)
-// and every survivor j = 2sm gathers the Schur updates of its eliminated neighbours
+// eliminates the active blocks i = s(2m+1) in parallel (k_cr_level):
+//   W_i = D_i^-1 [E_i | E_{i+s}^T | GB_i]      (register-tiled Gauss-Jordan, MFMA)
+// and every survivor j = 2sm receives the Schur terms of its eliminated neighbours
 // a = j - s and c = j + s:
 //   D_j -= E_j W_r(a) + E_c^T W_l(c),  GB_j -= E_j W_gb(a) + E_c^T W_gb(c),
 //   E_j <- -E_j W_l(a)   (new coupling to the next active block on the left)
-// until only block 0 is left; k_cr_top solves block 0 with the tau border (tau Schur sum
+// (formed by the eliminating workgroups, applied when j is next loaded) until only block 0
+// is left; k_cr_top solves block 0 with the tau border (tau Schur sum
 // over every eliminated block, fixed order), and k_cr_back substitutes the levels back:
 //   delta_i = W_b(i) - W_l(i) delta_{i-s} - W_r(i) delta_{i+s} - W_g(i) delta_tau.
 // All sums are in a fixed order, so the solve is deterministic run to run.
 // ---------------------------------------------------------------------------------------
 #define CR_MAXBP 96
+
+#ifdef FTE_PROFILE  // per-phase wall-clock ticks (100 MHz) of block 0 (tools/prof_fte_phases.py)
+__device__ unsigned long long g_fte_prof[32];
+#define PROF_T0 unsigned long long t_prof = wall_clock64();
+#define PROF(slot)                                                          \
+  do {                                                                      \
+    __syncthreads();                                                        \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                              \
+      const unsigned long long t_now = wall_clock64();                      \
+      atomicAdd(&g_fte_prof[slot], t_now - t_prof);                         \
+      t_prof = t_now;                                                       \
+    }                                                                       \
+  } while (0)
+// no barrier: lane 0 of wave w of block 0 (time since its own previous mark)
+#define PROFW(slot, w)                                                      \
+  do {                                                                      \
+    if (blockIdx.x == 0 && threadIdx.x == 64 * (w)) {                       \
+      const unsigned long long t_now = wall_clock64();                      \
+      atomicAdd(&g_fte_prof[slot], t_now - t_prof);                         \
+      t_prof = t_now;                                                       \
+    }                                                                       \
+  } while (0)
+#else
+#define PROF_T0
+#define PROF(slot)
+#define PROFW(slot, w)
+#endif
 
 __global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __restrict__ st,
                                                   const double* __restrict__ Ab, const double* __restrict__ gb,
@@ -496,121 +525,288 @@ __global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __r
   }
 }
 
-// LDS budget (BP <= 96): sD + one staged panel, both (BP x BP+1) doubles
-__global__ __launch_bounds__(1024) void k_cr_elim(FteDims d, int s, int a0, int bend,
-                                                  const FteState* __restrict__ st,
-                                                  const double* __restrict__ Dc, const double* __restrict__ Ec,
-                                                  const double* __restrict__ GBc, double* __restrict__ Wc,
-                                                  double* __restrict__ Tau, int* __restrict__ bad) {
-  // chain [a0, bend]: a0 is a multiple of 2s, so i is an odd multiple of s as in a
-  // whole-sequence reduction; the chain end bend survives every level of the chain
+// One reduction level: workgroups [0, ne * nsplit) eliminate the blocks i = a0 + s(2m+1)
+// (< iend), workgroups after them apply the pending Schur terms of level s/2 to the survivors
+// j = a0 + astep m (<= top). 1024 threads = 16 waves, register-tiled (16x16 f64 MFMA tiles):
+//   waves 0 .. NB-1  hold the row-blocks of D_i,
+//   waves NB ..      hold one column-block each of [E_i | E_r^T | GB_i] (r = i + s);
+// Gauss-Jordan elimination on that augmented matrix leaves W_i = D_i^-1 [E_i | E_r^T | GB_i]
+// in the column waves' registers after NB steps, one barrier per step (the pivot inverse,
+// the new pivot row and the old pivot column travel through double-buffered LDS).
+// `nsplit` workgroups share one block: each repeats the (cheap) D part and owns the
+// column-blocks J = part mod nsplit, which spreads the MFMA work of the few blocks of the
+// deep levels over more CUs (and is required when 2NB + GR/16 > 16 - NB).
+// The column waves then form this block's Schur terms for its neighbours (MFMA, A operand
+// from LDS copies of the coupling blocks, B operand = the W tiles in registers); every
+// output column depends on one W column only:
+//   dL_i = E_i^T [W_l | W_gb]  (-> left survivor l = i - s),
+//   dR_i = E_r   [W_r | W_gb]  (-> right survivor r),   E_r <- -E_r W_l  (next level's E),
+//   Tau_i = GB_i^T W_gb.
+// Survivors accumulate them lazily: a block applies dR_{j-s/2} + dL_{j+s/2} when it is
+// loaded at the next level (or by an apply workgroup), so a level is one launch.
+template <int NB>
+__global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int iend, int top, int ne, int astep,
+                                                   int nsplit, const FteState* __restrict__ st,
+                                                   double* __restrict__ Dc, const double* __restrict__ Ein,
+                                                   double* __restrict__ Eout, double* __restrict__ GBc,
+                                                   double* __restrict__ Wc, double* __restrict__ Tau,
+                                                   double* __restrict__ dL, double* __restrict__ dR,
+                                                   int* __restrict__ bad) {
   if (st->status != 0) return;
-  const int i = a0 + s * (2 * blockIdx.x + 1);
-  const int r = (i + s <= bend && i + s < d.nblk) ? i + s : -1;
-  const int BP = d.BP, GR = d.GR, WL = 2 * BP + GR, LD = BP + 1;
-  extern __shared__ double lds[];
-  double* sD = lds;                 // BP x LD
-  double* sB = lds + BP * LD;       // BP x LD (panel)
-  double* tmp = sB + BP * LD;       // 512
-  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
-  lds_stage<false>(sD, Dc + (size_t)i * BP * BP, BP, BP, BP);
-  __syncthreads();
-  wg_spd_inverse(sD, LD, BP >> 4, tmp, bad);
-  double* W = Wc + (size_t)i * BP * WL;
-  // W_l = D^-1 E_i ; W_r = D^-1 E_r^T ; W_gb = D^-1 GB_i
-  for (int part = 0; part < 3; ++part) {
-    const int cols = part < 2 ? BP : GR;
-    const int ldb = lds_ld(cols);
-    if (part == 0) lds_stage<false>(sB, Ec + (size_t)i * BP * BP, BP, BP, BP);
-    if (part == 1) {
-      if (r >= 0)
-        lds_stage<true>(sB, Ec + (size_t)r * BP * BP, BP, BP, BP);
+  // pivot tiles in LDS with row stride 17 doubles: the 16 rows an A fragment reads land on
+  // distinct banks
+  constexpr int BP = 16 * NB, TS = 17, BUF = 16 * TS + 16 * BP + BP * TS;
+  constexpr bool ER_LDS = NB <= 5;  // room for both coupling copies (BP <= 80)
+  const int GR = d.GR, GRB = GR >> 4, WL = 2 * BP + GR, LDD = BP + GR, NBB = 2 * NB + GRB;
+  const int hs = s >> 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
+  if ((int)blockIdx.x >= ne * nsplit) {
+    // survivor: D_j -= dR_{j-hs} + dL_{j+hs},  GB_j likewise
+    if (!hs) return;
+    const int j = a0 + astep * ((int)blockIdx.x - ne * nsplit);
+    const double* pr = (j - hs >= a0) ? dR + (size_t)(j - hs) * BP * LDD : nullptr;
+    const double* pl = (j + hs < iend) ? dL + (size_t)(j + hs) * BP * LDD : nullptr;
+    double* D = Dc + (size_t)j * BP * BP;
+    double* G = GBc + (size_t)j * BP * GR;
+    for (int e = tid; e < BP * LDD; e += blockDim.x) {
+      const int r = e / LDD, c = e - r * LDD;
+      double v = 0.0;
+      if (pr) v += pr[e];
+      if (pl) v += pl[e];
+      if (c < BP)
+        D[r * BP + c] -= v;
       else
-        for (int e = threadIdx.x; e < BP * ldb; e += blockDim.x) sB[e] = 0.0;
+        G[r * GR + c - BP] -= v;
     }
-    if (part == 2) lds_stage<false>(sB, GBc + (size_t)i * BP * GR, GR, BP, GR);
-    __syncthreads();
-    double* Wp = W + part * BP;
-    lds_gemm(sD, LD, sB, ldb, BP, cols, BP, [&](int i0, int j0, dbl4 acc) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Wp[(size_t)(i0 + lk + 4 * q) * WL + j0 + li] = acc[q];
-    });
-    __syncthreads();
+    return;
   }
-  // tau Schur contribution Tau_i = GB_i^T (D^-1 GB_i): A = GB_i^T (staged transposed into sD)
-  lds_stage<true>(sD, GBc + (size_t)i * BP * GR, GR, GR, BP);          // GR x BP
-  lds_stage<false>(sB, W + 2 * BP, WL, BP, GR);                        // BP x GR
-  __syncthreads();
-  double* T = Tau + (size_t)i * GR * GR;
-  lds_gemm(sD, BP + 1, sB, GR + 1, GR, GR, BP, [&](int i0, int j0, dbl4 acc) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) T[(i0 + lk + 4 * q) * GR + j0 + li] = acc[q];
-  });
-}
-
-__global__ __launch_bounds__(1024) void k_cr_update(FteDims d, int s, int a0, int bend,
-                                                    const FteState* __restrict__ st,
-                                                    double* __restrict__ Dc, double* __restrict__ Ec,
-                                                    double* __restrict__ GBc, const double* __restrict__ Wc) {
-  if (st->status != 0) return;
-  const int j = a0 + 2 * s * blockIdx.x;
-  const int a = j - s >= a0 ? j - s : -1;
-  const int c = (j + s <= bend && j + s < d.nblk) ? j + s : -1;
-  const int BP = d.BP, GR = d.GR, WL = 2 * BP + GR, LD = BP + 1;
+  const int part = (int)blockIdx.x % nsplit;
+  const int i = a0 + s * (2 * ((int)blockIdx.x / nsplit) + 1);
+  const int r = (i + s <= top) ? i + s : -1;
+  const double* qR = hs ? dR + (size_t)(i - hs) * BP * LDD : nullptr;  // pending of level hs
+  const double* qL = (hs && i + hs < iend) ? dL + (size_t)(i + hs) * BP * LDD : nullptr;
+  const double* Ei = Ein + (size_t)i * BP * BP;
+  const double* Er = r >= 0 ? Ein + (size_t)r * BP * BP : nullptr;
   extern __shared__ double lds[];
-  double* sA = lds;             // BP x LD
-  double* sB = lds + BP * LD;   // BP x LD
-  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
-  double* D = Dc + (size_t)j * BP * BP;
-  double* E = Ec + (size_t)j * BP * BP;
-  double* G = GBc + (size_t)j * BP * GR;
-  dbl4 keep[3];
-  int nkeep = 0;
-  auto sub_D = [&](int i0, int j0, dbl4 acc) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) D[(size_t)(i0 + lk + 4 * q) * BP + j0 + li] -= acc[q];
-  };
-  auto sub_G = [&](int i0, int j0, dbl4 acc) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) G[(size_t)(i0 + lk + 4 * q) * GR + j0 + li] -= acc[q];
-  };
-  if (a >= 0) {
-    const double* Wa = Wc + (size_t)a * BP * WL;
-    lds_stage<false>(sA, E, BP, BP, BP);
-    lds_stage<false>(sB, Wa + BP, WL, BP, BP);          // W_r(a)
-    __syncthreads();
-    lds_gemm(sA, LD, sB, LD, BP, BP, BP, sub_D);
-    __syncthreads();
-    lds_stage<false>(sB, Wa + 2 * BP, WL, BP, GR);      // W_gb(a)
-    __syncthreads();
-    lds_gemm(sA, LD, sB, GR + 1, BP, GR, BP, sub_G);
-    __syncthreads();
-    lds_stage<false>(sB, Wa, WL, BP, BP);               // W_l(a)
-    __syncthreads();
-    lds_gemm(sA, LD, sB, LD, BP, BP, BP, [&](int i0, int j0, dbl4 acc) { keep[nkeep++] = acc; });
-    __syncthreads();
+  double* G0 = lds + 2 * BUF;  // GB_i (pending applied), BP x GR, for Tau
+  // LDS copies of the coupling blocks (A operands of the Schur terms): E_i (row major BP x
+  // BP) and E_r (row stride BP + 1: the 16 rows of a fragment spread over the banks); E_r is
+  // read from global memory when BP = 96 leaves no room
+  double* sEi = G0 + BP * GR;
+  double* sEr = ER_LDS && Er ? sEi + BP * BP : nullptr;
+  const bool dwave = wave < NB;
+  // this wave's column-block J (0..NB-1 E_i, NB..2NB-1 E_r^T, 2NB.. GB_i): the p-th of the
+  // column-blocks J = part (mod nsplit)
+  int J = -1;
+  if (!dwave) {
+    const int jj = part + nsplit * (wave - NB);
+    if (jj < NBB) J = jj;
   }
-  if (c >= 0) {
-    const double* Wcc = Wc + (size_t)c * BP * WL;
-    lds_stage<true>(sA, Ec + (size_t)c * BP * BP, BP, BP, BP);  // E_c^T
-    lds_stage<false>(sB, Wcc, WL, BP, BP);                      // W_l(c)
-    __syncthreads();
-    lds_gemm(sA, LD, sB, LD, BP, BP, BP, sub_D);
-    __syncthreads();
-    lds_stage<false>(sB, Wcc + 2 * BP, WL, BP, GR);             // W_gb(c)
-    __syncthreads();
-    lds_gemm(sA, LD, sB, GR + 1, BP, GR, BP, sub_G);
+  PROF_T0
+  for (int e = tid; e < BP * BP; e += blockDim.x) {
+    sEi[e] = Ei[e];
+    if (sEr) sEr[(e / BP) * (BP + 1) + e % BP] = Er[e];
   }
-  if (a >= 0) {
-    // E_j <- -E_j W_l(a): tiles were assigned to waves in lds_gemm order
-    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6, tn = BP >> 4, nt = tn * tn;
-    int q = 0;
-    for (int t = wave; t < nt; t += nw, ++q) {
-      const int i0 = (t / tn) << 4, j0 = (t % tn) << 4;
+  dbl4 t[NB];
+  // loads: one branch-free unrolled batch per source so that they all issue back to back
+  auto load_rows = [&](const double* src, int ld, int r0) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) E[(size_t)(i0 + lk + 4 * r) * BP + j0 + li] = -keep[q][r];
+    for (int K = 0; K < NB; ++K)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[K][q] = src[(r0 + lk + 4 * q) * ld + K * 16 + li];
+  };
+  auto sub_rows = [&](const double* src, int ld, int r0) {
+    double v[NB][4];
+#pragma unroll
+    for (int K = 0; K < NB; ++K)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[K][q] = src[(r0 + lk + 4 * q) * ld + K * 16 + li];
+#pragma unroll
+    for (int K = 0; K < NB; ++K)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[K][q] -= v[K][q];
+  };
+  // column-block loads: element (K*16 + lk + 4q, c0 + li) of a row-major source
+  auto load_cols = [&](const double* src, int ld, int c0) {
+#pragma unroll
+    for (int K = 0; K < NB; ++K)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[K][q] = src[(K * 16 + lk + 4 * q) * ld + c0 + li];
+  };
+  auto sub_cols = [&](const double* src, int ld, int c0) {
+    double v[NB][4];
+#pragma unroll
+    for (int K = 0; K < NB; ++K)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[K][q] = src[(K * 16 + lk + 4 * q) * ld + c0 + li];
+#pragma unroll
+    for (int K = 0; K < NB; ++K)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[K][q] -= v[K][q];
+  };
+  if (dwave) {
+    load_rows(Dc + (size_t)i * BP * BP, BP, wave * 16);
+    if (qR) sub_rows(qR, LDD, wave * 16);
+    if (qL) sub_rows(qL, LDD, wave * 16);
+  } else if (J >= 0 && J < NB) {
+    load_cols(Ei, BP, J * 16);
+  } else if (J >= NB && J < 2 * NB) {
+    if (Er) {
+      // E_r^T: element (K*16 + lk + 4q, li) = E_r[(J-NB)*16 + li][K*16 + lk + 4q]
+      const double* src = Er + (size_t)((J - NB) * 16 + li) * BP;
+#pragma unroll
+      for (int K = 0; K < NB; ++K)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[K][q] = src[K * 16 + lk + 4 * q];
+    } else {
+#pragma unroll
+      for (int K = 0; K < NB; ++K) t[K] = dbl4{0.0, 0.0, 0.0, 0.0};
+    }
+  } else if (J >= 2 * NB) {
+    const int c0 = (J - 2 * NB) * 16;
+    load_cols(GBc + (size_t)i * BP * GR, GR, c0);
+    if (qR) sub_cols(qR + BP, LDD, c0);
+    if (qL) sub_cols(qL + BP, LDD, c0);
+#pragma unroll
+    for (int K = 0; K < NB; ++K)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) G0[(K * 16 + lk + 4 * q) * GR + c0 + li] = t[K][q];
+  }
+  PROF(0);
+  // Gauss-Jordan elimination, pivot block k
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    double* Pk = lds + (k & 1) * BUF;  // D_kk^-1, 16 x 16 (stride TS)
+    double* Rk = Pk + 16 * TS;         // new pivot row-block of D, 16 x BP
+    double* Ck = Rk + 16 * BP;         // old pivot column-block of D, BP x 16 (stride TS)
+    if (dwave) {
+      if (wave == k) {
+        double v[4] = {t[k][0], t[k][1], t[k][2], t[k][3]};
+        tile16_gj_inverse<true>(v, lane, part ? nullptr : bad);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          t[k][q] = v[q];
+          Pk[(lk + 4 * q) * TS + li] = v[q];
+        }
+#pragma unroll
+        for (int K = k + 1; K < NB; ++K) {
+          dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) acc = mfma64(Pk[li * TS + 4 * ks + lk], t[K][ks], acc);
+          t[K] = acc;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Rk[(lk + 4 * q) * BP + K * 16 + li] = acc[q];
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Ck[(wave * 16 + lk + 4 * q) * TS + li] = t[k][q];
+      }
+    }
+    __syncthreads();
+    if (dwave) {
+      if (wave != k) {
+#pragma unroll
+        for (int K = k + 1; K < NB; ++K) {
+          dbl4 acc = t[K];
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks)
+            acc = mfma64(-Ck[(wave * 16 + li) * TS + 4 * ks + lk], Rk[(4 * ks + lk) * BP + K * 16 + li], acc);
+          t[K] = acc;
+        }
+      }
+    } else if (J >= 0) {
+      dbl4 nk = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) nk = mfma64(Pk[li * TS + 4 * ks + lk], t[k][ks], nk);
+      t[k] = nk;
+#pragma unroll
+      for (int I = 0; I < NB; ++I) {
+        if (I == k) continue;
+        dbl4 acc = t[I];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc = mfma64(-Ck[(I * 16 + li) * TS + 4 * ks + lk], nk[ks], acc);
+        t[I] = acc;
+      }
     }
   }
+  PROF(1);
+  if (dwave || J < 0) return;
+  // W_i (back substitution), Schur terms for the neighbours, Tau_i
+  double* W = Wc + (size_t)i * BP * WL;
+  double* oL = dL + (size_t)i * BP * LDD;
+  double* oR = dR + (size_t)i * BP * LDD;
+  double* Er_out = r >= 0 ? Eout + (size_t)r * BP * BP : nullptr;
+  const int wcol = J < NB ? J * 16 : (J < 2 * NB ? BP + (J - NB) * 16 : 2 * BP + (J - 2 * NB) * 16);
+#pragma unroll
+  for (int K = 0; K < NB; ++K)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) W[(size_t)(K * 16 + lk + 4 * q) * WL + wcol + li] = t[K][q];
+  const int ocol = J < NB ? J * 16 : (J < 2 * NB ? (J - NB) * 16 : BP + (J - 2 * NB) * 16);
+  // out tile I = sum_K A(I, K) W(K): two independent MFMA chains (even / odd K)
+  auto term = [&](auto aop, auto store) {
+#pragma unroll 1
+    for (int I = 0; I < NB; ++I) {
+      dbl4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int K = 0; K < NB; K += 2) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          a0 = mfma64(aop(I, K, ks), t[K][ks], a0);
+          if (K + 1 < NB) a1 = mfma64(aop(I, K + 1, ks), t[K + 1][ks], a1);
+        }
+      }
+      store(I, a0 + a1);
+    }
+  };
+  // A operands (lane: row li, column 4 ks + lk of tile (I, K))
+  auto aEiT = [&](int I, int K, int ks) { return sEi[(K * 16 + 4 * ks + lk) * BP + I * 16 + li]; };
+  auto aEr_lds = [&](int I, int K, int ks) { return sEr[(I * 16 + li) * (BP + 1) + K * 16 + 4 * ks + lk]; };
+  auto aEr_glb = [&](int I, int K, int ks) { return Er[(I * 16 + li) * BP + K * 16 + 4 * ks + lk]; };
+  auto put_L = [&](int I, dbl4 acc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) oL[(size_t)(I * 16 + lk + 4 * q) * LDD + ocol + li] = acc[q];
+  };
+  auto put_R = [&](int I, dbl4 acc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) oR[(size_t)(I * 16 + lk + 4 * q) * LDD + ocol + li] = acc[q];
+  };
+  auto put_E = [&](int I, dbl4 acc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Er_out[(size_t)(I * 16 + lk + 4 * q) * BP + J * 16 + li] = -acc[q];
+  };
+  // left term E_i^T W (columns W_l and W_gb)
+  if (J < NB || J >= 2 * NB) term(aEiT, put_L);
+  PROFW(3, NB);
+  PROFW(3 + 8, 15);
+  // right term E_r W (columns W_r and W_gb) and the new coupling -E_r W_l
+  if (Er) {
+    if (J < NB) {
+      if (sEr)
+        term(aEr_lds, put_E);
+      else
+        term(aEr_glb, put_E);
+    } else {
+      if (sEr)
+        term(aEr_lds, put_R);
+      else
+        term(aEr_glb, put_R);
+    }
+  }
+  PROFW(4, NB);
+  PROFW(4 + 8, 15);
+  if (J >= 2 * NB) {
+    const int g = J - 2 * NB;
+    for (int g2 = 0; g2 < GRB; ++g2) {
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int K = 0; K < NB; ++K)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc = mfma64(G0[(K * 16 + 4 * ks + lk) * GR + g2 * 16 + li], t[K][ks], acc);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Tau[(size_t)i * GR * GR + (g2 * 16 + lk + 4 * q) * GR + g * 16 + li] = acc[q];
+    }
+  }
+  PROFW(5 + 8, 15);
 }
 
 // Fixed-order partial sums feeding the tau border (parallel over chunks, summed in chunk
@@ -962,6 +1158,7 @@ struct FteBuffers {
   double *Rl, *cams, *meas, *w, *qinv, *X, *tau;
   double *Hloc, *gloc, *Floc, *Ab, *gb, *Bt, *gmaxp, *Dc, *Ec, *GBc, *Wc, *Tau, *dcv, *dtau, *normp, *Fm, *Fq, *part;
   double* Adiag;
+  double *Ec2, *dL, *dR;  // second coupling buffer (levels alternate), pending Schur terms
   int* bad;
   FteState* st;
 };
@@ -1032,6 +1229,8 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
                ogb = take((size_t)M * P), oBt = take((size_t)M * P * Cg1), ogm = take(M),
                oD = take((size_t)n * BP * BP), oE = take((size_t)n * BP * BP), oG = take((size_t)n * BP * GR),
                oW = take((size_t)n * BP * (2 * BP + GR)), oTau = take((size_t)n * GR * GR),
+               oE2 = take((size_t)n * BP * BP), odL = take((size_t)n * BP * (BP + GR)),
+               odR = take((size_t)n * BP * (BP + GR)),
                odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)),
                onp = take(2 * (size_t)n), oFm = take(N), oFq = take(N), ost = take(16), oint = take(8);
   // staged inputs (owned mode only)
@@ -1091,6 +1290,9 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.GBc = arena + oG;
   b.Wc = arena + oW;
   b.Tau = arena + oTau;
+  b.Ec2 = arena + oE2;
+  b.dL = arena + odL;
+  b.dR = arena + odR;
   b.dcv = arena + odc;
   b.part = arena + opart;
   b.dtau = arena + odt;
@@ -1111,6 +1313,59 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   return ACS_OK;
 }
 
+// one k_cr_level launch (template on the tile count NB = BP/16)
+static void cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int iend, int top, int ne, int ns,
+                            int astep, const FteState* st, FteBuffers& b, const double* Ein, double* Eout, int* bad) {
+  if (ne + ns == 0) return;
+  const int NB = d.BP >> 4, NBB = 2 * NB + d.GR / 16;
+  // workgroups per eliminated block: enough column waves (16 - NB per workgroup), and more
+  // of them when few blocks are left (the deep levels are latency-bound)
+  const int need = (NBB + 16 - NB - 1) / (16 - NB);
+  const int want = ne <= 32 ? 4 : (ne <= 96 ? 2 : 1);
+  const int nsplit = std::min(std::max(need, want), NBB);
+  const int nwg = ne * nsplit + ns;
+  const size_t lds = sizeof(double) * (2 * (16 * 17 + 16 * (size_t)d.BP + 17 * (size_t)d.BP) + (size_t)d.BP * d.GR +
+                                       (NB <= 5 ? 2 * (size_t)d.BP + 1 : (size_t)d.BP) * d.BP);
+#define CR_LEVEL(nb)                                                                                               \
+  hipLaunchKernelGGL((k_cr_level<nb>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, top, ne, astep, nsplit, st, \
+                     b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
+  switch (NB) {
+    case 1: CR_LEVEL(1); break;
+    case 2: CR_LEVEL(2); break;
+    case 3: CR_LEVEL(3); break;
+    case 4: CR_LEVEL(4); break;
+    case 5: CR_LEVEL(5); break;
+    default: CR_LEVEL(6); break;
+  }
+#undef CR_LEVEL
+}
+
+// Block cyclic reduction of super-blocks [a0, top] (blocks < iend may be eliminated; a
+// chain end at iend survives), nlev levels, then the last level's pending Schur terms are
+// applied to the survivors. Returns the buffer holding the final couplings E.
+static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* st, FteBuffers& b, int a0, int iend,
+                               int top, int nlev, int* bad) {
+  const double* Ein = b.Ec;
+  double* Eout = b.Ec2;
+  int sl = 1;
+  for (int lv = 0; lv < nlev; ++lv, sl <<= 1) {
+    int ne = 0, ns = 0;
+    for (int i = a0 + sl; i < iend; i += 2 * sl) ++ne;
+    if (sl > 1)
+      for (int j = a0; j <= top; j += 2 * sl) ++ns;
+    cr_launch_level(d, s, sl, a0, iend, top, ne, ns, 2 * sl, st, b, Ein, Eout, bad);
+    double* t = const_cast<double*>(Ein);
+    Ein = Eout;
+    Eout = t;
+  }
+  if (nlev > 0) {
+    int ns = 0;
+    for (int j = a0; j <= top; j += sl) ++ns;
+    cr_launch_level(d, s, sl, a0, iend, top, 0, ns, sl, st, b, Ein, Eout, bad);
+  }
+  return Ein;
+}
+
 static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
@@ -1126,18 +1381,10 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
   fte_enqueue_linearize(S, s, 0);
-  const size_t lds_elim = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1) + 512);
-  const size_t lds_upd = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1));
   hipLaunchKernelGGL(k_cr_build, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, 0, -1,
                      -1, d.var ? b.Adiag : nullptr);
   const int bend = d.nblk - 1;
-  for (int lv = 0, st = 1; lv < d.nlev; ++lv, st <<= 1) {
-    const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
-    const int ns = (d.nblk + 2 * st - 1) / (2 * st);
-    hipLaunchKernelGGL(k_cr_elim, dim3(ne), dim3(1024), lds_elim, s, d, st, 0, bend, b.st, b.Dc, b.Ec, b.GBc, b.Wc,
-                       b.Tau, b.bad);
-    hipLaunchKernelGGL(k_cr_update, dim3(ns), dim3(1024), lds_upd, s, d, st, 0, bend, b.st, b.Dc, b.Ec, b.GBc, b.Wc);
-  }
+  cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
                      d.N, 1, d.nblk);
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, d, b.st, b.Dc, b.GBc, b.part, b.gmaxp, b.tau, b.dcv, b.dtau,
@@ -1392,22 +1639,11 @@ struct acs_fte_dist {
   int k_lo, k_hi, f_lo, f_hi, b_hi_build, c_lo, c_hi, own_lo, own_hi, out_lo, out_hi;
 };
 
-static void dist_local_cr(acs_fte_dist* h) {
+static const double* dist_local_cr(acs_fte_dist* h) {
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
-  hipStream_t s = h->ctx->stream;
-  const size_t lds_elim = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1) + 512);
-  const size_t lds_upd = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1));
   const int top = std::min(h->bend, d.nblk - 1);  // last existing block of the chain
-  for (int lv = 0, st = 1; lv < h->klev; ++lv, st <<= 1) {
-    int ne = 0, ns = 0;
-    for (int i = h->a0 + st; i < std::min(h->bend, d.nblk); i += 2 * st) ++ne;
-    for (int j = h->a0; j <= top; j += 2 * st) ++ns;
-    if (ne) hipLaunchKernelGGL(k_cr_elim, dim3(ne), dim3(1024), lds_elim, s, d, st, h->a0, h->bend, b.st, b.Dc, b.Ec,
-                               b.GBc, b.Wc, b.Tau, b.bad);
-    if (ns) hipLaunchKernelGGL(k_cr_update, dim3(ns), dim3(1024), lds_upd, s, d, st, h->a0, h->bend, b.st, b.Dc,
-                               b.Ec, b.GBc, b.Wc);
-  }
+  return cr_reduce(d, h->ctx->stream, b.st, b, h->a0, std::min(h->bend, d.nblk), top, h->klev, b.bad);
 }
 
 extern "C" {
@@ -1611,6 +1847,11 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
   return ACS_OK;
 }
 
+#ifdef FTE_PROFILE
+void acs_fte_prof_read(unsigned long long* out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fte_prof), sizeof(g_fte_prof));
+}
+#endif
 }  // extern "C"
 
 // ---------------------------------------------------------------------------------------
@@ -1680,6 +1921,7 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
   };
   const size_t oD = take(nb * BP * BP), oE = take(nb * BP * BP), oG = take(nb * BP * GR),
                oW = take(nb * BP * (2 * BP + GR)), oT = take(nb * GR * GR), odc = take(nb * BP),
+               oE2 = take(nb * BP * BP), odL = take(nb * BP * (BP + GR)), odR = take(nb * BP * (BP + GR)),
                op_ = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)), ogm = take(4);
   void* p = nullptr;
   if (hipMalloc(&p, off * sizeof(double)) != hipSuccess) {
@@ -1695,6 +1937,9 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
   h->r.GBc = a + oG;
   h->r.Wc = a + oW;
   h->r.Tau = a + oT;
+  h->r.Ec2 = a + oE2;
+  h->r.dL = a + odL;
+  h->r.dR = a + odR;
   h->r.dcv = a + odc;
   h->r.part = a + op_;
   h->r.gmaxp = a + ogm;
@@ -1751,10 +1996,10 @@ int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
     const int top = std::min(h->bend, d.nblk - 1);
     hipLaunchKernelGGL(k_cr_build, dim3(top - h->a0 + 1), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec,
                        b.GBc, h->a0, h->a0, h->bend, nullptr);
-    dist_local_cr(h);
+    const double* Efin = dist_local_cr(h);
     hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part,
                        h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk));
-    hipLaunchKernelGGL(k_dist_pack, dim3(32, 2), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.Dc, b.Ec,
+    hipLaunchKernelGGL(k_dist_pack, dim3(32, 2), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.Dc, Efin,
                        b.GBc, b.Ab, b.gb, p1);
     hipLaunchKernelGGL(k_dist_pack_small, dim3(1), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.part,
                        b.gmaxp, p1);
@@ -1770,19 +2015,11 @@ int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
   FteBuffers& b = h->S.b;
   FteBuffers& r = h->r;
   hipStream_t s = ctx->stream;
-  const size_t lds_elim = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1) + 512);
-  const size_t lds_upd = sizeof(double) * (2 * (size_t)d.BP * (d.BP + 1));
   // reduced system (identical on every rank)
   hipLaunchKernelGGL(k_red_build, dim3(dr.nblk), dim3(256), 0, s, d, b.st, h->Lo, h->R, h->span, p1, r.Dc, r.Ec,
                      r.GBc, r.gmaxp);
   const int rb = dr.nblk - 1;
-  for (int lv = 0, st = 1; lv < dr.nlev; ++lv, st <<= 1) {
-    const int ne = (dr.nblk - st + 2 * st - 1) / (2 * st);
-    const int ns = (dr.nblk + 2 * st - 1) / (2 * st);
-    hipLaunchKernelGGL(k_cr_elim, dim3(ne), dim3(1024), lds_elim, s, dr, st, 0, rb, b.st, r.Dc, r.Ec, r.GBc, r.Wc,
-                       r.Tau, b.bad);
-    hipLaunchKernelGGL(k_cr_update, dim3(ns), dim3(1024), lds_upd, s, dr, st, 0, rb, b.st, r.Dc, r.Ec, r.GBc, r.Wc);
-  }
+  cr_reduce(dr, s, b.st, r, 0, dr.nblk, rb, dr.nlev, b.bad);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, dr, b.st, r.Hloc, r.gloc, r.Tau, r.part, 0,
                      0, 1, dr.nblk);
   const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;

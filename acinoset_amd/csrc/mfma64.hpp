@@ -41,6 +41,41 @@ __device__ void wg_mgemm(double* C, int ldc, const double* A, int lda, const dou
   __syncthreads();
 }
 
+// In-register Gauss-Jordan inverse of one 16x16 tile held by a wave in accumulator layout
+// (lane l: column l & 15 of rows (l >> 4) + 4q). Pivot row / column travel by shuffles:
+// 16 steps, no barrier. SPD: pivots must be positive; otherwise |p| > 1e-300. A failed
+// pivot is replaced by 1e-300 and counted in *bad.
+template <bool SPD>
+__device__ __forceinline__ void tile16_gj_inverse(double* v, int lane, int* bad) {
+  const int r0 = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int qs = s >> 2, rs = s & 3;
+    double p = __shfl(v[qs], rs * 16 + s);          // A[s][s]
+    const double asc = __shfl(v[qs], rs * 16 + c);  // A[s][c]
+    double ais[4];                                  // A[i][s], i = r0 + 4q
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ais[q] = __shfl(v[q], r0 * 16 + s);
+    if (SPD ? !(p > 0.0) : !(fabs(p) > 1e-300)) {
+      if (bad && lane == 0) atomicAdd(bad, 1);
+      p = 1e-300;
+    }
+    const double ip = 1.0 / p;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = r0 + 4 * q;
+      if (i == s && c == s)
+        v[q] = ip;
+      else if (i == s)
+        v[q] = asc * ip;
+      else if (c == s)
+        v[q] = -ais[q] * ip;
+      else
+        v[q] = v[q] - ais[q] * asc * ip;
+    }
+  }
+}
+
 // In-place inverse of an SPD matrix (n = 16*nb, LDS or global, ld) by blocked
 // Gauss-Jordan without pivoting (SPD + LM damping: every pivot block is SPD).
 // tmp: 512 doubles of LDS. Non-positive pivots are counted in *bad.
@@ -67,32 +102,7 @@ __device__ void wg_gj_inverse(double* A, int lda, int nb, double* tmp, int* bad)
       double v[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = Akk[(r0 + 4 * q) * lda + c];
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int qs = s >> 2, rs = s & 3;
-        double p = __shfl(v[qs], rs * 16 + s);          // A[s][s]
-        const double asc = __shfl(v[qs], rs * 16 + c);  // A[s][c]
-        double ais[4];                                  // A[i][s], i = r0 + 4q
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ais[q] = __shfl(v[q], r0 * 16 + s);
-        if (SPD ? !(p > 0.0) : !(fabs(p) > 1e-300)) {
-          if (bad && lane == 0) atomicAdd(bad, 1);
-          p = 1e-300;
-        }
-        const double ip = 1.0 / p;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = r0 + 4 * q;
-          if (i == s && c == s)
-            v[q] = ip;
-          else if (i == s)
-            v[q] = asc * ip;
-          else if (c == s)
-            v[q] = -ais[q] * ip;
-          else
-            v[q] = v[q] - ais[q] * asc * ip;
-        }
-      }
+      tile16_gj_inverse<SPD>(v, lane, bad);
 #pragma unroll
       for (int q = 0; q < 4; ++q) Akk[(r0 + 4 * q) * lda + c] = v[q];
     }

@@ -441,10 +441,18 @@ def bench_fte(ctx, torch, stream, n_frames=1000, steps=5):
                    for c in range(C)], 1)
     m = w > 0
     rms = float(np.sqrt(np.mean(np.sum((uv - meas)[m] ** 2, -1))))
+    # algorithmic flops per frame per GN step = 2 (2CL) P^2 (J^T J) + ~80 kflop
+    # (FK + Jacobian) + 6 P^3 (banded Cholesky-equivalent solve)
+    P = table.P
+    flop_frame = 2 * (2 * C * L) * P * P + 80e3 + 6 * P ** 3
+    tfs = N * rep['iters'] * flop_frame / dt / 1e12
     return {'workload': f'fte C={C} frames={N} L={L} P={table.P} sd=const intermode=vel (configs[2])',
             'frames_per_s': N / dt, 'ms_per_solve': dt * 1e3, 'status': rep['status_name'], 'iters': rep['iters'],
             'accepted': rep['n_accepted'], 'cost_before': rep['cost_before'], 'cost_after': rep['cost_after'],
             'reproj_rms_px': rms, 'pos_rms_vs_truth_m': pos_rms, 'tau_err_max_s': float(np.abs(tau - seq.tau).max()),
+            'roofline': {'bound': 'fp64', 'achieved': tfs, 'peak': FP64_PEAK_TFS, 'unit': 'TFLOP/s',
+                         'frac': tfs / FP64_PEAK_TFS, 'flop_per_frame_step': flop_frame,
+                         'note': 'whole solve (all kernels), algorithmic flops of SURVEY.md 8(d)'},
             }
 
 
