@@ -108,7 +108,12 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
     const int kind = tid == 0 ? PK_TRANS : PK_WORLD;
     double t[3] = {0.0, 0.0, 0.0};
     for (int q = 0; q < s.P; ++q)
-      if (s.pk[4 * q] == kind) t[s.pk[4 * q + 1]] += x[q];
+      if (s.pk[4 * q] == kind) {
+        const int a = s.pk[4 * q + 1];
+        t[0] += a == 0 ? x[q] : 0.0;
+        t[1] += a == 1 ? x[q] : 0.0;
+        t[2] += a == 2 ? x[q] : 0.0;
+      }
     double* dst = tid == 0 ? sh.root : sh.world;
     dst[0] = t[0];
     dst[1] = t[1];
@@ -193,8 +198,8 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
     const int j = pk[4 * q + 1], r = pk[4 * q + 2];
     const int* jt = s.joints + 8 * j;
     const int nrot = jt[1];
-    double v[3] = {0.0, 0.0, 0.0};
-    v[jt[2 + r]] = 1.0;
+    const int ax = jt[2 + r];
+    double v[3] = {ax == 0 ? 1.0 : 0.0, ax == 1 ? 1.0 : 0.0, ax == 2 ? 1.0 : 0.0};
     for (int rr = r + 1; rr < nrot; ++rr) {
       double w[3];
       const int p = jt[5 + rr];
@@ -224,8 +229,10 @@ __device__ __forceinline__ void fk_dpos(const SkelView& s, const FkShared& sh, i
   const int* pk = s.pk + 4 * q;
   switch (pk[0]) {
     case PK_TRANS:
-    case PK_WORLD:
-      d[pk[1]] = 1.0;
+    case PK_WORLD:  // unit vector along axis pk[1] (selects, no indexed private store)
+      d[0] = pk[1] == 0 ? 1.0 : 0.0;
+      d[1] = pk[1] == 1 ? 1.0 : 0.0;
+      d[2] = pk[1] == 2 ? 1.0 : 0.0;
       break;
     case PK_LEN: {
       const int owner = pk[1];

@@ -116,8 +116,72 @@ __device__ double block_max(double v, double* s_red) {
 
 // ---------------------------------------------------------------------------------------
 // 1. per-frame linearisation
+//
+// Observation o = (camera c, marker l) has the 2 x NZ Jacobian Jp_o (2x3, the fisheye
+// projection derivative scaled by the weight) times D_o (3 x NZ, the derivative of the
+// shifted marker position), and D_o = D_l + S_c splits into the camera-independent FK part
+// D_l (columns < P, fk_dpos) and the shutter-delay part S_c = [own_c I (x_0..z_0) | prev_c I
+// | prev2_c I | v_c (tau column of camera c)] that is the same for every marker. With the
+// 3x3 curvature blocks Z_o = Jp_o^T diag(curv) Jp_o and gradient vectors r_o = Jp_o^T rho',
+//   H = sum_o D_o^T Z_o D_o
+//     = sum_l [D_l ; Q_l]^T [Z_l D_l + Q_l ; D_l]  +  sum_c S_c^T Z_c S_c,
+//   g = sum_l D_l^T r_l + sum_c S_c^T r_c,
+// with Z_l = sum_c Z_o, Q_l = sum_c Z_o S_c, Z_c = sum_l Z_o (and r likewise). The first
+// term is one MFMA product with K = 6L rows instead of the 2CL rows of the stacked
+// Jacobian (C times fewer FK derivatives, 2C/2 = C times fewer MFMA K-steps); the second
+// touches only the 9 + C shift / delay columns and is added when H is stored.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_fte_linearize(FteDims d, const int* __restrict__ I,
+#define LIN_OCH 256  // observations per aggregation chunk (= blockDim)
+#define LIN_MC 4     // markers per MFMA chunk (3 * LIN_MC operand rows)
+
+struct LinLds {
+  int cam, am, qt, ac, cf, uni, total;
+};
+// dynamic LDS of k_fte_linearize (doubles)
+__host__ __device__ __forceinline__ LinLds lin_lds(int C, int L, int NZP) {
+  LinLds o;
+  int p = 0;
+  o.cam = p;
+  p += C * ACS_CAM_STRIDE;
+  o.am = p;  // per marker: Z_l, sum own Z, sum prev Z, sum prev2 Z (6 each), r_l (3)
+  p += 27 * L;
+  o.qt = p;  // per (marker, camera): Z_o v_c (tau column of Q_l)
+  p += 3 * C * L;
+  o.ac = p;  // per camera: Z_c (6), r_c (3)
+  p += 9 * C;
+  o.cf = p;  // per camera: own, prev, prev2, v_c (3), tau_c
+  p += 7 * C;
+  o.uni = p;  // observation chunk (9 per obs) | operand rows (3 x 3 LIN_MC x (NZP + 1))
+  const int a = 9 * LIN_OCH, b = 9 * LIN_MC * (NZP + 1);
+  p += a > b ? a : b;
+  o.total = p;
+  return o;
+}
+
+__device__ __forceinline__ int sym3(int i, int j) {
+  // [xx xy xz yy yz zz]
+  return i <= j ? (i == 0 ? j : (i == 1 ? 2 + j : 5)) : (j == 0 ? i : (j == 1 ? 2 + i : 5));
+}
+
+// shift / delay column class: 0..2 = own (x_0..z_0), prev, prev2 with component *i;
+// 3 = tau column of camera *i; -1 = FK-only column
+__device__ __forceinline__ int lin_tcol(int x, int P, int NZ, int* i) {
+  if (x < 3) {
+    *i = x;
+    return 0;
+  }
+  if (x >= P && x < P + 6) {
+    *i = (x - P) % 3;
+    return 1 + (x - P) / 3;
+  }
+  if (x >= P + 6 && x < NZ) {
+    *i = x - P - 6;
+    return 3;
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* __restrict__ I,
                                                        const double* __restrict__ Rl,
                                                        const double* __restrict__ cams,
                                                        const double* __restrict__ meas,
@@ -129,132 +193,247 @@ __global__ __launch_bounds__(256) void k_fte_linearize(FteDims d, const int* __r
                                                        double* __restrict__ Floc) {
   if (!force && (st->status != 0 || !st->relin)) return;
   const int k = blockIdx.x + k0;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int P = d.P, C = d.C, L = d.L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
+  const int P = d.P, C = d.C, L = d.L, NZ = d.NZ;
+  const int NZP = (NZ + 15) & ~15, LD = NZP + 1, NT = NZP >> 4;
   const int cur = force ? 0 : st->cur;
   const double* X = Xbuf + (size_t)cur * d.M * P;
   const double* tau = taubuf + (size_t)cur * d.NT + (d.var ? (size_t)k * C : 0);
+  extern __shared__ double lds[];
+  const LinLds lo = lin_lds(C, L, NZP);
+  double *s_cam = lds + lo.cam, *s_am = lds + lo.am, *s_qt = lds + lo.qt, *s_ac = lds + lo.ac, *s_cf = lds + lo.cf,
+         *s_u = lds + lo.uni;
   __shared__ FkShared fk;
-  __shared__ double s_cam[FTE_MAXC * ACS_CAM_STRIDE];
-  __shared__ double s_J[2 * FTE_CH][FTE_NZP + 1];
-  __shared__ double s_sq[2 * FTE_CH], s_gs[2 * FTE_CH];
-  __shared__ double s_jp[FTE_CH][6];
-  __shared__ int s_node[FTE_CH], s_cid[FTE_CH], s_ok[FTE_CH];
-  __shared__ double s_dx[3], s_ddx[3], s_tau[FTE_MAXC];
+  __shared__ double s_dx[3], s_ddx[3];
   __shared__ double s_red[256];
   const SkelView s = skel_view(I, Rl);
   const int f = k + 2;
   for (int i = tid; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
+  for (int i = lo.am + tid; i < lo.cf; i += blockDim.x) lds[i] = 0.0;
   if (tid < 3) {
     const double x0 = X[f * P + tid], x1 = X[(f - 1) * P + tid], x2 = X[(f - 2) * P + tid];
     s_dx[tid] = (x0 - x1) / d.Ts;
     s_ddx[tid] = (x0 - 2.0 * x1 + x2) / (d.Ts * d.Ts);
   }
-  if (tid < C) s_tau[tid] = d.Ct ? tau[tid] : 0.0;
   fk_frame(s, X + f * P, fk, tid, blockDim.x);
   __syncthreads();
+  if (tid < C) {
+    const double tc = d.Ct ? tau[tid] : 0.0;
+    const ShiftCoef sc = shift_coef(d.im, tc, d.Ts);
+    double* cf = s_cf + 7 * tid;
+    cf[0] = sc.own;
+    cf[1] = sc.prev;
+    cf[2] = sc.prev2;
+    const bool tcol = d.Ct && tid > 0;
+    for (int i = 0; i < 3; ++i) cf[3 + i] = tcol ? s_dx[i] + (d.im == 2 ? 2.0 * tc * s_ddx[i] : 0.0) : 0.0;
+    cf[6] = tc;
+  }
+  __syncthreads();
 
-  // tiles of the symmetric 64x64 product: upper triangle, 10 tiles over 4 waves
-  const int tI[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
-  const int tJ[10] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
+  // (a) one observation per thread: projection, loss, Z_o, r_o; then the fixed-order sums
+  double rho = 0.0;
+  const int nobs = C * L;
+  for (int ch = 0; ch < nobs; ch += LIN_OCH) {
+    const int no = min(LIN_OCH, nobs - ch);
+    if (tid < no) {
+      const int o = ch + tid, c = o / L, l = o - c * L;
+      const double* p = fk.pos[s.outn[l]];
+      const double tc = s_cf[7 * c + 6];
+      double sh[3];
+      for (int i = 0; i < 3; ++i) {
+        sh[i] = 0.0;
+        if (d.im >= 1) sh[i] += s_dx[i] * tc;
+        if (d.im == 2) sh[i] += s_ddx[i] * (tc * tc);
+      }
+      ProjOut po;
+      fisheye_project<true, true>(s_cam + c * ACS_CAM_STRIDE, p[0] + sh[0], p[1] + sh[1], p[2] + sh[2], po);
+      const size_t mi = ((size_t)k * C + c) * L + l;
+      const double wt = wts[mi];
+      const double mu = wt != 0.0 ? meas[2 * mi] : 0.0, mv = wt != 0.0 ? meas[2 * mi + 1] : 0.0;
+      const bool ok = wt != 0.0;
+      double* z = s_u + 9 * tid;
+      for (int i = 0; i < 9; ++i) z[i] = 0.0;
+      // u then v (one loss evaluation live at a time)
+#pragma unroll 1
+      for (int side = 0; side < 2; ++side) {
+        const double e = wt * ((side ? po.v : po.u) - (side ? mv : mu));
+        const LossOut ls = redescending(e, d.la, d.lb, d.lc);
+        rho += ls.f;
+        if (ok) {
+          const double cw = wt * wt * loss_curv(e, ls), gw = wt * ls.d1;
+          const double j0 = po.J[3 * side], j1 = po.J[3 * side + 1], j2 = po.J[3 * side + 2];
+          z[0] += cw * j0 * j0;
+          z[1] += cw * j0 * j1;
+          z[2] += cw * j0 * j2;
+          z[3] += cw * j1 * j1;
+          z[4] += cw * j1 * j2;
+          z[5] += cw * j2 * j2;
+          z[6] += gw * j0;
+          z[7] += gw * j1;
+          z[8] += gw * j2;
+        }
+      }
+    }
+    __syncthreads();
+    // per marker (cameras in order): Z_l, sum_c coef_c Z_o (own, prev, prev2), r_l
+    for (int e = tid; e < 27 * L; e += blockDim.x) {
+      const int l = e / 27, j = e - 27 * l;
+      double v = 0.0;
+      for (int c = 0; c < C; ++c) {
+        const int oo = c * L + l - ch;
+        if (oo < 0 || oo >= no) continue;
+        const double* z = s_u + 9 * oo;
+        if (j < 6)
+          v += z[j];
+        else if (j < 24)
+          v += s_cf[7 * c + (j - 6) / 6] * z[(j - 6) % 6];
+        else
+          v += z[j - 18];
+      }
+      s_am[e] += v;
+    }
+    // per camera (markers in order): Z_c, r_c
+    for (int e = tid; e < 9 * C; e += blockDim.x) {
+      const int c = e / 9, j = e - 9 * c;
+      double v = 0.0;
+      for (int l = 0; l < L; ++l) {
+        const int oo = c * L + l - ch;
+        if (oo >= 0 && oo < no) v += s_u[9 * oo + j];
+      }
+      s_ac[e] += v;
+    }
+    // per observation: Z_o v_c
+    for (int e = tid; e < 3 * no; e += blockDim.x) {
+      const int oo = e / 3, i = e - 3 * oo, o = ch + oo, c = o / L, l = o - c * L;
+      const double* z = s_u + 9 * oo;
+      const double* v = s_cf + 7 * c + 3;
+      s_qt[(l * C + c) * 3 + i] = z[sym3(i, 0)] * v[0] + z[sym3(i, 1)] * v[1] + z[sym3(i, 2)] * v[2];
+    }
+    __syncthreads();
+  }
+
+  // (b) H = sum_l [D_l ; Q_l]^T [Z_l D_l + Q_l ; D_l] on v_mfma_f64_16x16x4f64: upper-triangle
+  //     tiles of NT x NT, tile t on wave t % 4
+  // tile t = wave + 4q (q = 0..2) of the NT (NT + 1) / 2 upper-triangle tiles, row-major
+  const int ntile = NT * (NT + 1) / 2;
+  auto tile_ab = [&](int t, int& a, int& b) {
+    a = 0;
+    while (t >= NT - a) {
+      t -= NT - a;
+      ++a;
+    }
+    b = a + t;
+  };
   dbl4 acc[3];
   for (int q = 0; q < 3; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
-  double gacc = 0.0, rho = 0.0;
-  const int nobs = C * L;
-  for (int ch = 0; ch < nobs; ch += FTE_CH) {
-    if (tid < FTE_CH) {
-      const int o = ch + tid;
-      s_ok[tid] = 0;
-      s_sq[2 * tid] = s_sq[2 * tid + 1] = 0.0;
-      s_gs[2 * tid] = s_gs[2 * tid + 1] = 0.0;
-      if (o < nobs) {
-        const int c = o / L, l = o - (o / L) * L;
-        const int node = s.outn[l];
-        const double tc = s_tau[c];
-        double sh[3];
-        for (int i = 0; i < 3; ++i) {
-          sh[i] = 0.0;
-          if (d.im >= 1) sh[i] += s_dx[i] * tc;
-          if (d.im == 2) sh[i] += s_ddx[i] * (tc * tc);
+  double gacc = 0.0;
+  constexpr int RC = 3 * LIN_MC;
+  double* sD = s_u;            // D_l rows
+  double* sB = s_u + RC * LD;  // Z_l D_l + Q_l rows
+  double* sQ = sB + RC * LD;   // Q_l rows
+  for (int l0 = 0; l0 < L; l0 += LIN_MC) {
+    for (int e = tid; e < LIN_MC * NZP; e += blockDim.x) {
+      const int m = e / NZP, q = e - m * NZP, l = l0 + m;
+      double dp[3] = {0.0, 0.0, 0.0}, qv[3] = {0.0, 0.0, 0.0};
+      const double* am = s_am + 27 * (l < L ? l : 0);
+      if (l < L) {
+        if (q < P) fk_dpos(s, fk, s.outn[l], q, dp);
+        int i0;
+        const int cls = lin_tcol(q, P, NZ, &i0);
+        if (cls >= 0 && cls < 3) {
+          for (int i = 0; i < 3; ++i) qv[i] = am[6 + 6 * cls + sym3(i, i0)];
+        } else if (cls == 3) {
+          for (int i = 0; i < 3; ++i) qv[i] = s_qt[(l * C + i0) * 3 + i];
         }
-        ProjOut po;
-        fisheye_project<true, true>(s_cam + c * ACS_CAM_STRIDE, fk.pos[node][0] + sh[0], fk.pos[node][1] + sh[1],
-                                    fk.pos[node][2] + sh[2], po);
-        const size_t mi = ((size_t)k * C + c) * L + l;
-        const double wt = wts[mi];
-        const double mu = wt != 0.0 ? meas[2 * mi] : 0.0, mv = wt != 0.0 ? meas[2 * mi + 1] : 0.0;
-        const double eu = wt * (po.u - mu), ev = wt * (po.v - mv);
-        const LossOut lu = redescending(eu, d.la, d.lb, d.lc);
-        const LossOut lv = redescending(ev, d.la, d.lb, d.lc);
-        rho += lu.f + lv.f;
-        s_sq[2 * tid] = sqrt(loss_curv(eu, lu));
-        s_sq[2 * tid + 1] = sqrt(loss_curv(ev, lv));
-        s_gs[2 * tid] = lu.d1;
-        s_gs[2 * tid + 1] = lv.d1;
-        for (int i = 0; i < 6; ++i) s_jp[tid][i] = wt * po.J[i];
-        s_node[tid] = node;
-        s_cid[tid] = c;
-        s_ok[tid] = (wt != 0.0);
+      }
+      for (int i = 0; i < 3; ++i) {
+        const int r = (3 * m + i) * LD + q;
+        sD[r] = dp[i];
+        sB[r] = (l < L) ? am[sym3(i, 0)] * dp[0] + am[sym3(i, 1)] * dp[1] + am[sym3(i, 2)] * dp[2] + qv[i] : 0.0;
+        sQ[r] = qv[i];
       }
     }
     __syncthreads();
-    for (int idx = tid; idx < FTE_CH * FTE_NZP; idx += blockDim.x) {
-      const int t = idx / FTE_NZP, q = idx - t * FTE_NZP;
-      double v0 = 0.0, v1 = 0.0;
-      if (s_ok[t] && q < d.NZ) {
-        const int c = s_cid[t];
-        const ShiftCoef sc = shift_coef(d.im, s_tau[c], d.Ts);
-        double dp[3] = {0.0, 0.0, 0.0};
-        if (q < P) {
-          fk_dpos(s, fk, s_node[t], q, dp);
-          if (q < 3) dp[q] += sc.own;
-        } else if (q < P + 3) {
-          dp[q - P] = sc.prev;
-        } else if (q < P + 6) {
-          dp[q - P - 3] = sc.prev2;
-        } else {
-          const int cc = q - P - 6;
-          if (cc == c && c > 0) {
-            for (int i = 0; i < 3; ++i) dp[i] = s_dx[i] + (d.im == 2 ? 2.0 * s_tau[c] * s_ddx[i] : 0.0);
-          }
-        }
-        v0 = s_jp[t][0] * dp[0] + s_jp[t][1] * dp[1] + s_jp[t][2] * dp[2];
-        v1 = s_jp[t][3] * dp[0] + s_jp[t][4] * dp[1] + s_jp[t][5] * dp[2];
-      }
-      s_J[2 * t][q] = v0;
-      s_J[2 * t + 1][q] = v1;
+    if (tid < NZP) {
+      const int nr = 3 * min(LIN_MC, L - l0);
+      for (int r = 0; r < nr; ++r) gacc = fma(sD[r * LD + tid], s_am[27 * (l0 + r / 3) + 24 + r % 3], gacc);
     }
-    __syncthreads();
-    // gradient (one column per thread) and normal blocks (MFMA f64 16x16x4)
-    if (tid < FTE_NZP) {
-      for (int r = 0; r < 2 * FTE_CH; ++r) gacc = fma(s_gs[r], s_J[r][tid], gacc);
-    }
+#pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const int tile = wave + 4 * q;
-      if (tile >= 10) break;
-      const int ci = tI[tile] * 16 + (lane & 15), cj = tJ[tile] * 16 + (lane & 15);
-      for (int r0 = 0; r0 < 2 * FTE_CH; r0 += 4) {
-        const int r = r0 + (lane >> 4);
-        const double sq = s_sq[r];
-        const double a = s_J[r][ci] * sq, b = s_J[r][cj] * sq;
-        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[q], 0, 0, 0);
+      if (wave + 4 * q >= ntile) break;
+      int ta, tb;
+      tile_ab(wave + 4 * q, ta, tb);
+      const int ci = ta * 16 + li, cj = tb * 16 + li;
+#pragma unroll
+      for (int r0 = 0; r0 < RC; r0 += 4) {
+        const int r = (r0 + lk) * LD;
+        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(sD[r + ci], sB[r + cj], acc[q], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r0 = 0; r0 < RC; r0 += 4) {
+        const int r = (r0 + lk) * LD;
+        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(sQ[r + ci], sD[r + cj], acc[q], 0, 0, 0);
       }
     }
     __syncthreads();
   }
+
+  // (c) sum_c S_c^T Z_c S_c and sum_c S_c^T r_c (shift / delay columns), store
+  auto zc_v = [&](int c, int i) {  // (Z_c v_c)[i]
+    const double* z = s_ac + 9 * c;
+    const double* v = s_cf + 7 * c + 3;
+    return z[sym3(i, 0)] * v[0] + z[sym3(i, 1)] * v[1] + z[sym3(i, 2)] * v[2];
+  };
+  auto tpart = [&](int row, int col) {
+    int i, j;
+    const int a = lin_tcol(row, P, NZ, &i), b = lin_tcol(col, P, NZ, &j);
+    if (a < 0 || b < 0) return 0.0;
+    double v = 0.0;
+    if (a < 3 && b < 3) {
+      for (int c = 0; c < C; ++c) v += s_cf[7 * c + a] * s_cf[7 * c + b] * s_ac[9 * c + sym3(i, j)];
+    } else if (a < 3) {
+      v = s_cf[7 * j + a] * zc_v(j, i);
+    } else if (b < 3) {
+      v = s_cf[7 * i + b] * zc_v(i, j);
+    } else if (i == j) {
+      const double* vv = s_cf + 7 * i + 3;
+      v = vv[0] * zc_v(i, 0) + vv[1] * zc_v(i, 1) + vv[2] * zc_v(i, 2);
+    }
+    return v;
+  };
   double* H = Hloc + (size_t)k * FTE_NZP * FTE_NZP;
+#pragma unroll
   for (int q = 0; q < 3; ++q) {
-    const int tile = wave + 4 * q;
-    if (tile >= 10) break;
+    if (wave + 4 * q >= ntile) break;
+    int ta, tb;
+    tile_ab(wave + 4 * q, ta, tb);
+#pragma unroll
     for (int rg = 0; rg < 4; ++rg) {
-      const int row = tI[tile] * 16 + (lane >> 4) + 4 * rg, col = tJ[tile] * 16 + (lane & 15);
-      H[row * FTE_NZP + col] = acc[q][rg];
-      H[col * FTE_NZP + row] = acc[q][rg];
+      const int row = ta * 16 + lk + 4 * rg, col = tb * 16 + li;
+      if (row > col) continue;  // diagonal tiles: the (row <= col) element writes both
+      const double v = acc[q][rg] + tpart(row, col);
+      H[row * FTE_NZP + col] = v;
+      H[col * FTE_NZP + row] = v;
     }
   }
-  if (tid < FTE_NZP) gloc[(size_t)k * FTE_NZP + tid] = gacc;
+  if (tid < NZP) {
+    int i;
+    const int a = lin_tcol(tid, P, NZ, &i);
+    if (a >= 0 && a < 3) {
+      for (int c = 0; c < C; ++c) gacc += s_cf[7 * c + a] * s_ac[9 * c + 6 + i];
+    } else if (a == 3) {
+      const double* v = s_cf + 7 * i + 3;
+      const double* r = s_ac + 9 * i + 6;
+      gacc += v[0] * r[0] + v[1] * r[1] + v[2] * r[2];
+    }
+    gloc[(size_t)k * FTE_NZP + tid] = gacc;
+  }
   const double tot = block_sum(rho, s_red);
   if (tid == 0) Floc[k] = tot;
+}
+
+static size_t lin_lds_bytes(const FteDims& d) {
+  return sizeof(double) * (size_t)lin_lds(d.C, d.L, (d.NZ + 15) & ~15).total;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1369,7 +1548,7 @@ static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* 
 static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
-  hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
+  hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
                      b.st, force, 0, b.Hloc, b.gloc, b.Floc);
   hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, force, 0, 0, INT_MAX,
                      b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag);
@@ -1989,7 +2168,7 @@ int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
   ACS_HIP(ctx, hipMemsetAsync(p1, 0, sizeof(double) * h->Lo.n1, s));
   if (h->a0 < d.nblk) {
     if (h->k_hi > h->k_lo)
-      hipLaunchKernelGGL(k_fte_linearize, dim3(h->k_hi - h->k_lo), dim3(256), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w,
+      hipLaunchKernelGGL(k_fte_linearize, dim3(h->k_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
                          b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc);
     hipLaunchKernelGGL(k_fte_assemble, dim3(h->f_hi - h->f_lo), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, 0,
                        h->f_lo, h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag);

@@ -48,6 +48,9 @@ def parse():
                     help='also time SBA at configs[4] scale on one GPU (0 = skip)')
     ap.add_argument('--scale-cams', type=int, default=12)
     ap.add_argument('--fte-frames', type=int, default=1000)
+    ap.add_argument('--event-every', type=int, default=8,
+                    help='HIP event pairs bracket groups of this many consecutive timed steps '
+                         '(kernel duration for the roofline)')
     return ap.parse_args()
 
 
@@ -88,9 +91,18 @@ def main():
     d_pts = d_pts0.clone()
     opts = _native.Context.sba_opts()
 
-    def step():  # one full solve from the resident initial points (pts_in -> pts_out)
-        ctx.sba_points_dense_dev(d_cams.data_ptr(), C, d_uv.data_ptr(), d_mask.data_ptr(), n_pts,
-                                 d_pts.data_ptr(), opts, pts_in_p=d_pts0.data_ptr())
+    # one step = one full solve from the resident initial points (pts_in -> pts_out): a direct
+    # call of the C ABI entry acs_sba_points_dense_io with pre-marshalled device pointers
+    import ctypes
+    fn = ctx.lib.acs_sba_points_dense_io
+    call = (ctx.h, ctypes.c_void_p(d_cams.data_ptr()), C, ctypes.c_void_p(d_uv.data_ptr()),
+            ctypes.c_void_p(d_mask.data_ptr()), n_pts, ctypes.c_void_p(d_pts0.data_ptr()),
+            ctypes.c_void_p(d_pts.data_ptr()), ctypes.byref(opts), None, _native.ACS_DEVICE_PTRS)
+
+    def step():
+        rc = fn(*call)
+        if rc:
+            ctx.check(rc, 'acs_sba_points_dense_io')
 
     for _ in range(args.warmup):
         step()
@@ -104,17 +116,25 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events on the kernel's stream bracket consecutive groups of `every` steps (a pair
+    # per launch would cost more host time than the launch itself and add its own latency
+    # to the bracket); kernel_ms = bracketed GPU time / launches
+    every = max(1, min(args.event_every, args.steps))
+    ngrp = args.steps // every
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(ngrp)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
+        g, j = divmod(i, every)
+        if g < ngrp and j == 0:
+            ev[g][0].record(stream)
         step()
-        ev[i][1].record(stream)
+        if g < ngrp and j == every - 1:
+            ev[g][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) / every
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -151,7 +171,8 @@ def main():
                    'parallelism': f'frame-shard x{world}'},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                     'kernel': 'k_sba_lm', 'kernel_ms': kern_ms, 'bytes_per_launch': bytes_launch,
+                     'kernel': 'k_sba_lm', 'kernel_ms': kern_ms, 'kernel_ms_launches': ngrp * every,
+                     'bytes_per_launch': bytes_launch,
                      'traffic_source': pmc['source'] if pmc else None},
         'convergence': {'status': rep['status_counts'], 'iters_max': rep['iters_max'],
                         'gn_steps_mean': iters_mean, 'cost_before': rep['cost_before'],
