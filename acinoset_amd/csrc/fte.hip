@@ -1023,7 +1023,7 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
   }
 }
 
-__global__ __launch_bounds__(256) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ Dc,
+__global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ Dc,
                                                 const double* __restrict__ GBc, const double* __restrict__ part,
                                                 const double* __restrict__ gmaxp, const double* __restrict__ taubuf,
                                                 double* __restrict__ dcv, double* __restrict__ dtau,
@@ -1037,14 +1037,21 @@ __global__ __launch_bounds__(256) void k_cr_top(FteDims d, FteState* __restrict_
   __shared__ double sS[32 * 32];
   __shared__ double sr[32];
   __shared__ double tmp[512];
-  __shared__ double s_red[256];
+  __shared__ double s_red[1024];
   // chunk partials -> sums (fixed order)
   const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
   __shared__ double s_sum[16 * 16 + 16 + 32 * 32];
   __shared__ int s_held[32];
   for (int e = tid; e < nE; e += nth) {
+    // 16 loads in flight at a time, summed in chunk order
     double v = 0.0;
-    for (int ch = 0; ch < CR_NCHUNK; ++ch) v += part[(size_t)ch * nE + e];
+    for (int c0 = 0; c0 < CR_NCHUNK; c0 += 16) {
+      double pv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pv[q] = part[(size_t)(c0 + q) * nE + e];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v += pv[q];
+    }
     s_sum[e] = v;
   }
   __syncthreads();
@@ -1121,14 +1128,20 @@ __global__ __launch_bounds__(256) void k_cr_back(FteDims d, int s, int a0, int b
   }
   if (threadIdx.x < 32) st_[threadIdx.x] = threadIdx.x < Cg ? dtau[threadIdx.x] : 0.0;
   __syncthreads();
-  for (int row = threadIdx.x; row < BP; row += blockDim.x) {
-    const double* w = W + (size_t)row * WL;
-    double v = w[2 * BP + Cg];
-    for (int c = 0; c < BP; ++c) v -= w[c] * sl[c];
-    if (r >= 0)
-      for (int c = 0; c < BP; ++c) v -= w[BP + c] * sr_[c];
-    for (int c = 0; c < Cg; ++c) v -= w[2 * BP + c] * st_[c];
-    dcv[(size_t)i * BP + row] = v;
+  // one row per 16-lane row group: coalesced 128-byte reads of W along the row, DPP sum
+  const int li = threadIdx.x & 15, grp = threadIdx.x >> 4, ngrp = blockDim.x >> 4;
+  for (int row0 = 0; row0 < BP; row0 += ngrp) {
+    const int row = row0 + grp;
+    double v = 0.0;
+    if (row < BP) {
+      const double* w = W + (size_t)row * WL;
+      for (int c = li; c < BP; c += 16) v = fma(w[c], sl[c], v);
+      if (r >= 0)
+        for (int c = li; c < BP; c += 16) v = fma(w[BP + c], sr_[c], v);
+      for (int c = li; c < Cg; c += 16) v = fma(w[2 * BP + c], st_[c], v);
+    }
+    v = group_sum<16>(v);
+    if (row < BP && li == 0) dcv[(size_t)i * BP + row] = W[(size_t)row * WL + 2 * BP + Cg] - v;
   }
 }
 
@@ -1566,7 +1579,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
                      d.N, 1, d.nblk);
-  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, d, b.st, b.Dc, b.GBc, b.part, b.gmaxp, b.tau, b.dcv, b.dtau,
+  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, d, b.st, b.Dc, b.GBc, b.part, b.gmaxp, b.tau, b.dcv, b.dtau,
                      b.bad);
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
@@ -2203,7 +2216,7 @@ int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
                      0, 1, dr.nblk);
   const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
   hipLaunchKernelGGL(k_red_part, dim3(1), dim3(256), 0, s, nE, h->Lo, b.st, p1, r.part);
-  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(256), 0, s, dr, b.st, r.Dc, r.GBc, r.part, r.gmaxp, b.tau, r.dcv, b.dtau,
+  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, dr, b.st, r.Dc, r.GBc, r.part, r.gmaxp, b.tau, r.dcv, b.dtau,
                      b.bad);
   for (int lv = dr.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;

@@ -1,4 +1,5 @@
 """Mirror of the SBA / FTE seams of src/lib/app.py: `sba_points_fisheye` (:135-138),
+`sba_board_points_fisheye` (:123-126),
 `save_sba` (:271-295), `save_fte` (:317-332), `start_logging` / `stop_logging` (:337-345).
 Video rendering and plotting (pyqtgraph / OpenCV) are out of scope: the save functions
 write the pickle/.mat outputs and skip the labelled videos."""
@@ -9,11 +10,17 @@ import numpy as np
 
 from . import misc, utils
 from .calib import project_points_fisheye, triangulate_points_fisheye
-from .sba import _sba_points
+from .sba import _sba_board_points, _sba_points
 
 
 def sba_points_fisheye(scene_fpath, points_2d_df):
     return _sba_points(scene_fpath, points_2d_df, triangulate_points_fisheye, project_points_fisheye)
+
+
+def sba_board_points_fisheye(scene_fpath, points_fpaths, out_fpath, manual_points_fpath=None, manual_points_only=False,
+                             camera_indices=None):
+    return _sba_board_points(scene_fpath, points_fpaths, manual_points_fpath, out_fpath, triangulate_points_fisheye,
+                             project_points_fisheye, camera_indices, manual_points_only)
 
 
 def _gaze_targets(head_pos, nose_pos, r_eye_pos, r=3.0):

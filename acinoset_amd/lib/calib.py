@@ -1,9 +1,10 @@
 """Mirror of the fisheye part of src/lib/calib.py used by the SBA / FTE path.
 
 project_points_fisheye (:132-136) and triangulate_points_fisheye (:120-129) run on the
-GPU (acs_project_fisheye, acs_triangulate_pairs). The OpenCV calibration front-end of
-the reference (checkerboard calibration, stereo calibration) is out of scope
-(SURVEY.md §2 row 4).
+GPU (acs_project_fisheye, acs_triangulate_pairs). The board-point bundle adjustment that
+refines a calibrated scene is in `lib.sba._sba_board_points` / `lib.app.sba_board_points_
+fisheye`; OpenCV's checkerboard detection and per-camera / stereo calibration
+(:141-297) stay out of scope (one-off, OpenCV-bound).
 """
 import numpy as np
 

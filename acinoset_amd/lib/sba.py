@@ -7,13 +7,17 @@
 * `_sba_points` (:285-313) keeps the reference's point selection (adjacent-pair
   triangulation + inner merge on (frame, marker)) and index semantics.
 * `bundle_adjust_points_and_extrinsics` (:158-178) -> acs_sba_extrinsics (Schur LM).
+* Calibration-board front end (:37-137, :196-282): `prepare_calib_board_data_for_bundle_
+  adjustment`, `prepare_manual_points_for_bundle_adjustment`, `bundle_adjust_board_points_only`
+  and `_sba_board_points`, with every image's first-two-camera triangulation batched into one
+  GPU call (acs_triangulate_pairs) and the joint points + extrinsics solve on the GPU.
 """
 from time import time
 
 import numpy as np
 
 from .. import _native
-from .utils import get_pairwise_3d_points_from_df, load_scene
+from .utils import get_pairwise_3d_points_from_df, load_manual_points, load_points, load_scene, save_scene
 
 
 def create_bundle_adjustment_jacobian_sparsity_matrix(n_cams, n_params_per_camera, camera_indices, n_points,
@@ -160,3 +164,144 @@ def bundle_adjust_points_and_extrinsics(points_2d, points_3d, point_3d_indices, 
     r_out = cams[:, 8:17].reshape(n, 3, 3).copy()
     t_out = cams[:, 17:20].reshape(n, 3, 1).copy()
     return pts, r_out, t_out, dict(before=rb, after=ra)
+
+
+# ---- calibration-board front end (src/lib/sba.py:37-137, :196-282) -----------------------
+
+def _triangulate_batch(jobs, k_arr, d_arr, r_arr, t_arr, triangulate_func):
+    """jobs: [(uv_a (n,2), uv_b (n,2), cam_a, cam_b)] -> list of (n, 3). The fisheye model
+    (triangulate_func None or calib.triangulate_points_fisheye) runs as ONE GPU batch;
+    any other triangulate_func is called per job, as the reference does."""
+    from .calib import triangulate_points_fisheye
+    if not jobs:
+        return []
+    if triangulate_func is not None and triangulate_func is not triangulate_points_fisheye:
+        return [np.asarray(triangulate_func(a, b, k_arr[ca], d_arr[ca], r_arr[ca], t_arr[ca],
+                                            k_arr[cb], d_arr[cb], r_arr[cb], t_arr[cb])).reshape(-1, 3)
+                for a, b, ca, cb in jobs]
+    cams = _native.pack_cameras(k_arr, np.asarray(d_arr).reshape(-1, 4), r_arr, t_arr)
+    uva = np.concatenate([np.asarray(a, np.float64).reshape(-1, 2) for a, _, _, _ in jobs])
+    uvb = np.concatenate([np.asarray(b, np.float64).reshape(-1, 2) for _, b, _, _ in jobs])
+    cia = np.concatenate([np.full(len(np.asarray(a).reshape(-1, 2)), ca, np.int32) for a, _, ca, _ in jobs])
+    cib = np.concatenate([np.full(len(np.asarray(a).reshape(-1, 2)), cb, np.int32) for a, _, _, cb in jobs])
+    xyz = _native.default_context().triangulate_pairs(cams, uva, uvb, cia, cib)
+    out, o = [], 0
+    for a, _, _, _ in jobs:
+        n = len(np.asarray(a).reshape(-1, 2))
+        out.append(xyz[o:o + n])
+        o += n
+    return out
+
+
+def prepare_calib_board_data_for_bundle_adjustment(img_pts_arr, fnames_arr, board_shape, k_arr, d_arr, r_arr,
+                                                   t_arr, triangulate_func=None):
+    """`src/lib/sba.py:37-92`: every image name seen by at least two cameras contributes its
+    board corners once per camera that saw it (u,v), one 3-D point per corner, initialised
+    by triangulating the first two of those cameras. Returns (points_2d (n_obs,2) float32,
+    points_3d (n_pts,3) float32, point_3d_indices, camera_indices).
+
+    The reference walks the image names in the iteration order of a Python `set` of
+    strings, which depends on PYTHONHASHSEED; here the order is sorted, so it is
+    reproducible. Any order gives the same problem up to a permutation of the points."""
+    n_cam = len(img_pts_arr)
+    lists = [list(f) for f in fnames_arr]
+    seen = {}
+    for fnames in lists:
+        for fn in set(fnames):
+            seen[fn] = seen.get(fn, 0) + 1
+    ppi = board_shape[0] * board_shape[1]
+    points_2d, point_3d_indices, camera_indices, jobs = [], [], [], []
+    counter = 0
+    for fn in sorted(k for k, v in seen.items() if v >= 2):
+        tri = []
+        for cam in range(n_cam):
+            if fn in lists[cam]:
+                f_idx = lists[cam].index(fn)
+                tri.append((cam, f_idx))
+                points_2d.append(np.asarray(img_pts_arr[cam][f_idx]).reshape(ppi, 2))
+                point_3d_indices.append(np.arange(counter, counter + ppi))
+                camera_indices.append(np.full(ppi, cam))
+        (a, a_pt), (b, b_pt) = tri[0], tri[1]
+        jobs.append((img_pts_arr[a][a_pt], img_pts_arr[b][b_pt], a, b))
+        counter += ppi
+    points_3d = _triangulate_batch(jobs, k_arr, d_arr, r_arr, t_arr, triangulate_func)
+    if not jobs:
+        return (np.zeros((0, 2), np.float32), np.zeros((0, 3), np.float32), np.zeros(0, np.int64),
+                np.zeros(0, np.int64))
+    return (np.concatenate(points_2d).astype(np.float32), np.concatenate(points_3d).astype(np.float32),
+            np.concatenate(point_3d_indices).astype(np.int64), np.concatenate(camera_indices).astype(np.int64))
+
+
+def prepare_manual_points_for_bundle_adjustment(img_pts_arr, k_arr, d_arr, r_arr, t_arr, triangulate_func=None):
+    """`src/lib/sba.py:95-137`: img_pts_arr (n_points, n_cams, 2) with NaN where a camera did
+    not label the point; a point seen by >= 2 cameras becomes one 3-D point initialised
+    from its first two cameras. Returns the four arrays of the board variant."""
+    pts = np.asarray(img_pts_arr).swapaxes(0, 1)  # (n_cams, n_points, 2)
+    n_cam, n_pts = pts.shape[0], pts.shape[1]
+    points_2d, point_3d_indices, camera_indices, jobs = [], [], [], []
+    idx = 0
+    for i in range(n_pts):
+        cams = [c for c in range(n_cam) if not np.isnan(pts[c, i]).any()]
+        if len(cams) > 1:
+            points_2d.extend(pts[c, i] for c in cams)
+            camera_indices.extend(cams)
+            point_3d_indices.extend([idx] * len(cams))
+            jobs.append((pts[cams[0], i], pts[cams[1], i], cams[0], cams[1]))
+            idx += 1
+    points_3d = _triangulate_batch(jobs, k_arr, d_arr, r_arr, t_arr, triangulate_func)
+    return (np.array(points_2d, np.float32).reshape(-1, 2),
+            (np.concatenate(points_3d) if points_3d else np.zeros((0, 3))).astype(np.float32),
+            np.array(point_3d_indices, np.int64), np.array(camera_indices, np.int64))
+
+
+def bundle_adjust_board_points_only(img_pts_arr, fnames_arr, board_shape, k_arr, d_arr, r_arr, t_arr,
+                                    triangulate_func=None, project_func=None):
+    """`src/lib/sba.py:196-204`."""
+    p2, p3, pi, ci = prepare_calib_board_data_for_bundle_adjustment(img_pts_arr, fnames_arr, board_shape, k_arr,
+                                                                    d_arr, r_arr, t_arr, triangulate_func)
+    return bundle_adjust_points_only(p2, p3, pi, ci, k_arr, d_arr, r_arr, t_arr, project_func)
+
+
+def _sba_board_points(scene_fpath, points_fpaths, manual_points_fpath, out_fpath, triangulate_func=None,
+                      project_func=None, camera_indices=None, manual_points_only=False):
+    """`src/lib/sba.py:209-282`: board corners (+ optional hand-labelled points) -> joint
+    points + extrinsics SBA -> refined scene JSON at out_fpath. Returns the residuals.
+
+    Kept as the reference has it: manual point indices are offset by the LAST board point
+    index (`manual + board.max()`, :249), so the first manual point shares its index with
+    the last board corner and the final initial 3-D point is unused."""
+    img_pts_arr, fnames_arr, board_shape = [], [], None
+    if camera_indices is None:
+        camera_indices = range(len(points_fpaths))
+    for i in camera_indices:
+        points, fnames, board_shape, *_ = load_points(points_fpaths[i])
+        img_pts_arr.append(points)
+        fnames_arr.append(fnames)
+    k_arr, d_arr, r_arr, t_arr, cam_res = load_scene(scene_fpath)
+    assert len(k_arr) == len(img_pts_arr)
+    if manual_points_fpath is not None:
+        manual_points, _, *_ = load_manual_points(manual_points_fpath)
+        m2, m3, mi, mc = prepare_manual_points_for_bundle_adjustment(manual_points, k_arr, d_arr, r_arr, t_arr,
+                                                                     triangulate_func)
+        if manual_points_only:
+            print('bundle_adjust_board_points_and_extrinsics (with manual points only)')
+            p2, p3, pi, ci = m2, m3, mi, mc
+        else:
+            print('bundle_adjust_board_points_and_extrinsics (with manual points)')
+            p2, p3, pi, ci = prepare_calib_board_data_for_bundle_adjustment(img_pts_arr, fnames_arr, board_shape,
+                                                                            k_arr, d_arr, r_arr, t_arr,
+                                                                            triangulate_func)
+            p2 = np.append(p2, m2, axis=0)
+            p3 = np.append(p3, m3, axis=0)
+            pi = np.append(pi, mi + pi.max(), axis=0)
+            ci = np.append(ci, mc, axis=0)
+    else:
+        print('bundle_adjust_board_points_and_extrinsics')
+        p2, p3, pi, ci = prepare_calib_board_data_for_bundle_adjustment(img_pts_arr, fnames_arr, board_shape, k_arr,
+                                                                        d_arr, r_arr, t_arr, triangulate_func)
+    obj_pts, r_arr, t_arr, res = bundle_adjust_points_and_extrinsics(p2, p3, pi, ci, k_arr, d_arr, r_arr, t_arr,
+                                                                     project_func)
+    print(f"\nBefore: mean: {np.mean(res['before'])}, std: {np.std(res['before'])}")
+    print(f"After: mean: {np.mean(res['after'])}, std: {np.std(res['after'])}\n")
+    save_scene(out_fpath, k_arr, d_arr, r_arr, t_arr, cam_res)
+    return res

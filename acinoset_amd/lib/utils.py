@@ -18,6 +18,66 @@ import pandas as pd
 from .. import _native
 
 
+def load_points(fpath, verbose=False):
+    """`src/lib/utils.py:18-28`: checkerboard corners JSON -> (points (n_img, n_corner, 1, 2)
+    float32, fnames, board_shape, board_square_len, cam_res)."""
+    with open(fpath) as f:
+        data = json.load(f)
+    fnames = list(data['points'].keys())
+    points = np.array(list(data['points'].values()), dtype=np.float32)
+    board_shape = tuple(data['board_shape'])
+    board_square_len = data['board_square_len']
+    cam_res = tuple(data['camera_resolution'])
+    if verbose:
+        print(f'Loaded checkerboard points from {fpath}\n')
+    return points, fnames, board_shape, board_square_len, cam_res
+
+
+def load_manual_points(fpath, verbose=True):
+    """`src/lib/utils.py:31-41`: hand-labelled points JSON -> (points (n_pts, n_cams, 2),
+    fnames 'imgNNNNN.jpg', cam_res)."""
+    with open(fpath) as f:
+        data = json.load(f)
+    points = np.array(data['points'])
+    fnames = [f'img{str(i).zfill(5)}.jpg' for i in data['frame_idx']]
+    cam_res = tuple(data['camera_resolution'])
+    if verbose:
+        print(f'Loaded manual points from {fpath}\n')
+    return points, fnames, cam_res
+
+
+def load_camera(fpath, verbose=False):
+    """`src/lib/utils.py:44-52`: intrinsics JSON -> (k (3,3), d (4,1), cam_res)."""
+    with open(fpath) as f:
+        data = json.load(f)
+    cam_res = tuple(data['camera_resolution'])
+    k = np.array(data['k'], dtype=np.float64)
+    d = np.array(data['d'], dtype=np.float64)
+    if verbose:
+        print(f'Loaded intrinsics from {fpath}\n')
+    return k, d, cam_res
+
+
+def save_points(out_fpath, img_points, img_fnames, board_shape, board_square_len, cam_res):
+    """`src/lib/utils.py:156-170`."""
+    if isinstance(img_points, np.ndarray):
+        img_points = img_points.tolist()
+    data = {'timestamp': str(datetime.now()), 'board_shape': board_shape, 'board_square_len': board_square_len,
+            'camera_resolution': cam_res, 'points': dict(zip(img_fnames, img_points))}
+    with open(out_fpath, 'w') as f:
+        json.dump(data, f)
+    print(f'Saved points to {out_fpath}\n')
+
+
+def save_camera(out_fpath, cam_res, k, d):
+    """`src/lib/utils.py:173-183`."""
+    data = {'timestamp': str(datetime.now()), 'camera_resolution': cam_res, 'k': np.asarray(k).tolist(),
+            'd': np.asarray(d).tolist()}
+    with open(out_fpath, 'w') as f:
+        json.dump(data, f)
+    print(f'Saved intrinsics to {out_fpath}\n')
+
+
 def load_scene(fpath, verbose=True):
     """`src/lib/utils.py:55-74` -> (k_arr (C,3,3), d_arr (C,4,1), r_arr, t_arr (C,3,1), cam_res)."""
     with open(fpath) as f:

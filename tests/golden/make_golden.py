@@ -237,6 +237,95 @@ def ekf_fixture(mode='default', n_frames=30, seed=31):
     print(f'ekf {mode}: {n_frames} frames, ref {dt:.1f}s, keys {sorted(captured)}')
 
 
+def board_fixture(n_img=8, cams=(0, 1, 2), board_shape=(9, 6), square=0.088, seed=11):
+    """Calibration-board bundle adjustment (src/lib/sba.py:37-137, :209-282): synthetic
+    checkerboard corners seen by 1-3 cameras per image + hand-labelled points with NaNs,
+    the reference's data preparation and its full _sba_board_points run."""
+    import json
+    rng = np.random.default_rng(seed)
+    scene = synth.load_scene_file().subset(list(cams))
+    C = scene.n_cams
+    obj = ref_utils.create_board_object_pts(board_shape, square).astype(np.float64)
+    obj -= obj.mean(0)
+    vis_pattern = [(0, 1, 2), (0, 1), (1, 2), (0, 2), (0,), (0, 1, 2), (2,), (0, 1, 2)]
+    pts_per_cam = [dict() for _ in range(C)]
+    truth = {}
+    for i in range(n_img):
+        fn = f'img{i:05d}.jpg'
+        rv = np.array([np.pi / 2, 0.0, 0.0]) + rng.normal(0, 0.25, 3)
+        Rb = _cv2shim._rodrigues(rv)[0]
+        ctr = np.array([1.9, 6.4, 0.6]) + rng.normal(0, 0.4, 3)
+        X = obj @ Rb.T + ctr
+        truth[fn] = X
+        for c in vis_pattern[i % len(vis_pattern)]:
+            uv = synth.project_numpy(X, scene.K[c], scene.D[c], scene.R[c], scene.t[c])
+            uv = uv + rng.normal(0, 0.3, uv.shape)
+            pts_per_cam[c][fn] = uv.reshape(-1, 1, 2).tolist()
+    # hand-labelled points: (n_points, n_cams, 2) with NaN where a camera has no label
+    n_man = 6
+    Xm = np.array([1.9, 6.4, 0.5]) + rng.normal(0, 0.5, (n_man, 3))
+    man = np.full((n_man, C, 2), np.nan)
+    for j in range(n_man):
+        for c in range(C):
+            if (j + c) % 4 != 3:
+                man[j, c] = synth.project_numpy(Xm[j:j + 1], scene.K[c], scene.D[c], scene.R[c], scene.t[c])[0]
+    man[0, 1:] = np.nan  # seen by one camera only: dropped
+    # perturbed starting extrinsics
+    R0, t0 = scene.R.copy(), scene.t.copy()
+    for c in range(1, C):
+        R0[c] = _cv2shim._rodrigues(_cv2shim._rodrigues(R0[c])[0].ravel() + rng.normal(0, 2e-3, 3))[0]
+        t0[c] = t0[c] + rng.normal(0, 5e-3, (3, 1))
+    tmp = '/tmp/golden_board'
+    os.makedirs(tmp, exist_ok=True)
+    scene_path = os.path.join(tmp, 'scene.json')
+    ref_utils.save_scene(scene_path, scene.K, scene.D, R0, t0, tuple(scene.res))
+    pfs = []
+    for c in range(C):
+        fnames = sorted(pts_per_cam[c])
+        pf = os.path.join(tmp, f'points_cam{c}.json')
+        ref_utils.save_points(pf, [pts_per_cam[c][f] for f in fnames], fnames, board_shape, square, tuple(scene.res))
+        pfs.append(pf)
+    mf = os.path.join(tmp, 'manual_points.json')
+    with open(mf, 'w') as f:
+        json.dump({'points': man.tolist(), 'frame_idx': list(range(n_man)),
+                   'camera_resolution': list(scene.res)}, f)
+    man_loaded = ref_utils.load_manual_points(mf)[0].astype(np.float64)
+    img_pts_arr, fnames_arr = [], []
+    for pf in pfs:
+        p, fn, *_ = ref_utils.load_points(pf)
+        img_pts_arr.append(p)
+        fnames_arr.append(fn)
+    b2, b3, bi, bc = ref_sba.prepare_calib_board_data_for_bundle_adjustment(
+        img_pts_arr, fnames_arr, board_shape, scene.K, scene.D, R0, t0, ref_calib.triangulate_points_fisheye)
+    # image name of every 3-D point block (the reference walks a set: hash-seed order)
+    ppi = board_shape[0] * board_shape[1]
+    order = []
+    for blk in range(len(b3) // ppi):
+        rows = np.flatnonzero(bi == blk * ppi)[0]
+        c = int(bc[rows])
+        uv = b2[rows:rows + ppi]
+        hit = [fn for fn, v in zip(fnames_arr[c], img_pts_arr[c]) if np.array_equal(v.reshape(-1, 2), uv)]
+        order.append(hit[0])
+    m2, m3, mi, mc = ref_sba.prepare_manual_points_for_bundle_adjustment(
+        man_loaded, scene.K, scene.D, R0, t0, ref_calib.triangulate_points_fisheye)
+    out_path = os.path.join(tmp, 'scene_sba.json')
+    t_start = time.time()
+    res = ref_sba._sba_board_points(scene_path, pfs, mf, out_path, ref_calib.triangulate_points_fisheye,
+                                    ref_calib.project_points_fisheye)
+    dt = time.time() - t_start
+    _, _, R1, t1, _ = ref_utils.load_scene(out_path, verbose=False)
+    files = {f'points_cam{c}': open(pfs[c]).read() for c in range(C)}
+    np.savez_compressed(os.path.join(HERE, 'board.npz'), K=scene.K, D=scene.D, R_true=scene.R, t_true=scene.t,
+                        R0=R0, t0=t0, res=np.array(scene.res), board_shape=np.array(board_shape), square=square,
+                        manual_points_json=open(mf).read(), manual=man_loaded,
+                        board_points_2d=b2, board_points_3d=b3, board_point_indices=bi, board_camera_indices=bc,
+                        board_fname_order=np.array(order), manual_points_2d=m2, manual_points_3d=m3,
+                        manual_point_indices=mi, manual_camera_indices=mc, R_out=R1, t_out=t1,
+                        resid_before=np.asarray(res['before']), resid_after=np.asarray(res['after']),
+                        ref_seconds=dt, **files)
+    print(f'board: {len(b2)} board obs + {len(m2)} manual obs, ref {dt:.1f}s')
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['loss', 'fk', 'tri', 'cfg1', 'cfg2', 'ext']
     if 'loss' in which:
@@ -251,6 +340,8 @@ if __name__ == '__main__':
         sba_fixture('sba_cfg2', 100, list(range(6)))
     if 'ext' in which:
         extrinsics_fixture()
+    if 'board' in which:
+        board_fixture()
     if 'ekf' in which:
         ekf_fixture('default', 30)
         ekf_fixture('head', 40)
