@@ -654,45 +654,64 @@ __device__ unsigned long long g_fte_prof[32];
 #define PROFW(slot, w)
 #endif
 
-__global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __restrict__ st,
-                                                  const double* __restrict__ Ab, const double* __restrict__ gb,
-                                                  const double* __restrict__ Bt, double* __restrict__ Dc,
-                                                  double* __restrict__ Ec, double* __restrict__ GBc, int b0,
-                                                  int end_l, int end_r, const double* __restrict__ Adiag) {
+template <int NB>
+__global__ __launch_bounds__(1024) void k_cr_build(FteDims d, const FteState* __restrict__ st,
+                                                   const double* __restrict__ Ab, const double* __restrict__ gb,
+                                                   const double* __restrict__ Bt, double* __restrict__ Dc,
+                                                   double* __restrict__ Ec, double* __restrict__ GBc, int b0,
+                                                   int end_l, int end_r, const double* __restrict__ Adiag) {
   if (st->status != 0) return;
-  const int i = blockIdx.x + b0;
+  constexpr int BP = 16 * NB, NE = (BP * BP + 1023) / 1024;
+  const int i = blockIdx.x + b0, tid = threadIdx.x;
   const bool damp = i != end_l && i != end_r;  // chain ends are damped in the reduced system
-  const int tid = threadIdx.x, nth = blockDim.x;
-  const int P = d.P, PP = P * P, BP = d.BP, GR = d.GR, Cg = d.Cg;
+  const int P = d.P, PP = P * P, GR = d.GR, Cg = d.Cg;
   const double lam = st->lam;
   double* D = Dc + (size_t)i * BP * BP;
   double* E = Ec + (size_t)i * BP * BP;
   double* G = GBc + (size_t)i * BP * GR;
-  for (int e = tid; e < BP * BP; e += nth) {
-    const int r = e / BP, c = e % BP;
-    const int ar = r / P, pr = r % P, ac = c / P, pc = c % P;
+  __shared__ int s_a[BP], s_p[BP];  // super-block row/col -> (frame in block, parameter)
+  if (tid < BP) {
+    s_a[tid] = tid / P;
+    s_p[tid] = tid - (tid / P) * P;
+  }
+  __syncthreads();
+  double dv[NE], ev[NE];
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int e = tid + 1024 * q;
+    const int r = e / BP, c = e - (e / BP) * BP;
+    dv[q] = 0.0;
+    ev[q] = 0.0;
+    if (e >= BP * BP) continue;
+    const int ar = s_a[r], pr = s_p[r], ac = s_a[c], pc = s_p[c];
     const int fr = 3 * i + ar, fc = 3 * i + ac;
-    double v = 0.0, w = 0.0;
     const bool rin = r < 3 * P && fr < d.M, cin = c < 3 * P && fc < d.M;
     if (rin && cin) {
-      v = (ar >= ac) ? Ab[(size_t)fr * 4 * PP + (ar - ac) * PP + pr * P + pc]
-                     : Ab[(size_t)fc * 4 * PP + (ac - ar) * PP + pc * P + pr];
+      double v = (ar >= ac) ? Ab[(size_t)fr * 4 * PP + (ar - ac) * PP + pr * P + pc]
+                            : Ab[(size_t)fc * 4 * PP + (ac - ar) * PP + pc * P + pr];
       if (r == c && damp) v += lam * fmax(Adiag ? Adiag[(size_t)fr * P + pr] : v, 1e-12);
+      dv[q] = v;
     } else if (r == c) {
-      v = 1.0;  // padding: identity
+      dv[q] = 1.0;  // padding: identity
     }
-    D[e] = v;
     // E_i = T(block i, block i-1): frames 3i+ar vs 3(i-1)+ac, distance 3 + ar - ac <= 3
     const int fe = 3 * (i - 1) + ac;
     if (i > 0 && rin && c < 3 * P && fe < d.M) {
       const int dist = 3 + ar - ac;
-      if (dist <= 3) w = Ab[(size_t)fr * 4 * PP + dist * PP + pr * P + pc];
+      if (dist <= 3) ev[q] = Ab[(size_t)fr * 4 * PP + dist * PP + pr * P + pc];
     }
-    E[e] = w;
   }
-  for (int e = tid; e < BP * GR; e += nth) {
-    const int r = e / GR, c = e % GR;
-    const int ar = r / P, pr = r % P, fr = 3 * i + ar;
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int e = tid + 1024 * q;
+    if (e < BP * BP) {
+      D[e] = dv[q];
+      E[e] = ev[q];
+    }
+  }
+  for (int e = tid; e < BP * GR; e += blockDim.x) {
+    const int r = e / GR, c = e - (e / GR) * GR;
+    const int pr = s_p[r], fr = 3 * i + s_a[r];
     double v = 0.0;
     if (r < 3 * P && fr < d.M) {
       if (c < Cg)
@@ -702,6 +721,24 @@ __global__ __launch_bounds__(256) void k_cr_build(FteDims d, const FteState* __r
     }
     G[e] = v;
   }
+}
+
+static void cr_launch_build(const FteDims& d, hipStream_t s, int nblk, const FteState* st, const double* Ab,
+                            const double* gb, const double* Bt, double* Dc, double* Ec, double* GBc, int b0,
+                            int end_l, int end_r, const double* Adiag) {
+  if (nblk <= 0) return;
+#define CR_BUILD(nb)                                                                                          \
+  hipLaunchKernelGGL((k_cr_build<nb>), dim3(nblk), dim3(1024), 0, s, d, st, Ab, gb, Bt, Dc, Ec, GBc, b0, end_l, \
+                     end_r, Adiag)
+  switch (d.BP >> 4) {
+    case 1: CR_BUILD(1); break;
+    case 2: CR_BUILD(2); break;
+    case 3: CR_BUILD(3); break;
+    case 4: CR_BUILD(4); break;
+    case 5: CR_BUILD(5); break;
+    default: CR_BUILD(6); break;
+  }
+#undef CR_BUILD
 }
 
 // One reduction level: workgroups [0, ne * nsplit) eliminate the blocks i = a0 + s(2m+1)
@@ -782,9 +819,24 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     if (jj < NBB) J = jj;
   }
   PROF_T0
-  for (int e = tid; e < BP * BP; e += blockDim.x) {
-    sEi[e] = Ei[e];
-    if (sEr) sEr[(e / BP) * (BP + 1) + e % BP] = Er[e];
+  {
+    // every load in flight before the LDS stores (blockDim = 1024)
+    constexpr int NCP = (BP * BP + 1023) / 1024;
+    double ve[NCP], vr[NCP];
+#pragma unroll
+    for (int q = 0; q < NCP; ++q) {
+      const int e = tid + 1024 * q;
+      ve[q] = e < BP * BP ? Ei[e] : 0.0;
+      vr[q] = (sEr && e < BP * BP) ? Er[e] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < NCP; ++q) {
+      const int e = tid + 1024 * q;
+      if (e < BP * BP) {
+        sEi[e] = ve[q];
+        if (sEr) sEr[(e / BP) * (BP + 1) + e % BP] = vr[q];
+      }
+    }
   }
   dbl4 t[NB];
   // loads: one branch-free unrolled batch per source so that they all issue back to back
@@ -1112,37 +1164,55 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
   }
 }
 
-__global__ __launch_bounds__(256) void k_cr_back(FteDims d, int s, int a0, int bend,
-                                                 const FteState* __restrict__ st,
-                                                 const double* __restrict__ Wc, const double* __restrict__ dtau,
-                                                 double* __restrict__ dcv) {
+__global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int bend,
+                                                  const FteState* __restrict__ st,
+                                                  const double* __restrict__ Wc, const double* __restrict__ dtau,
+                                                  double* __restrict__ dcv) {
   if (st->status != 0) return;
   const int i = a0 + s * (2 * blockIdx.x + 1);
   const int l = i - s, r = (i + s <= bend && i + s < d.nblk) ? i + s : -1;
   const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
   const double* W = Wc + (size_t)i * BP * WL;
   __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32];
-  for (int e = threadIdx.x; e < BP; e += blockDim.x) {
-    sl[e] = dcv[(size_t)l * BP + e];
-    sr_[e] = r >= 0 ? dcv[(size_t)r * BP + e] : 0.0;
+  const int tid = threadIdx.x;
+  if (tid < BP) {
+    sl[tid] = dcv[(size_t)l * BP + tid];
+    sr_[tid] = r >= 0 ? dcv[(size_t)r * BP + tid] : 0.0;
   }
-  if (threadIdx.x < 32) st_[threadIdx.x] = threadIdx.x < Cg ? dtau[threadIdx.x] : 0.0;
+  if (tid < 32) st_[tid] = tid < Cg ? dtau[tid] : 0.0;
+  // one row per aligned group of 8 lanes (BP <= 96 < 128 groups): the W loads of every
+  // row are issued together, then an FMA chain per lane and a 3-step DPP sum
+  constexpr int NQ = CR_MAXBP / 8;
+  const int row = tid >> 3, j = tid & 7;
+  const bool live = row < BP;
+  const double* w = W + (size_t)(live ? row : 0) * WL;
+  double a[NQ], b[NQ], t[4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int c = j + 8 * q;
+    a[q] = (live && c < BP) ? w[c] : 0.0;
+    b[q] = (live && r >= 0 && c < BP) ? w[BP + c] : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = j + 8 * q;
+    t[q] = (live && c < Cg) ? w[2 * BP + c] : 0.0;
+  }
+  const double rhs = live ? w[2 * BP + Cg] : 0.0;
   __syncthreads();
-  // one row per 16-lane row group: coalesced 128-byte reads of W along the row, DPP sum
-  const int li = threadIdx.x & 15, grp = threadIdx.x >> 4, ngrp = blockDim.x >> 4;
-  for (int row0 = 0; row0 < BP; row0 += ngrp) {
-    const int row = row0 + grp;
-    double v = 0.0;
-    if (row < BP) {
-      const double* w = W + (size_t)row * WL;
-      for (int c = li; c < BP; c += 16) v = fma(w[c], sl[c], v);
-      if (r >= 0)
-        for (int c = li; c < BP; c += 16) v = fma(w[BP + c], sr_[c], v);
-      for (int c = li; c < Cg; c += 16) v = fma(w[2 * BP + c], st_[c], v);
-    }
-    v = group_sum<16>(v);
-    if (row < BP && li == 0) dcv[(size_t)i * BP + row] = W[(size_t)row * WL + 2 * BP + Cg] - v;
+  double v = 0.0;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int c = j + 8 * q;
+    if (c < BP) v = fma(a[q], sl[c], fma(b[q], sr_[c], v));
   }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = j + 8 * q;
+    if (c < 32) v = fma(t[q], st_[c], v);
+  }
+  v = group_sum<8>(v);
+  if (live && j == 0) dcv[(size_t)i * BP + row] = rhs - v;
 }
 
 // trial state X + delta, tau + dtau (clipped), norm partials per super-block. Variable
@@ -1573,8 +1643,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
   fte_enqueue_linearize(S, s, 0);
-  hipLaunchKernelGGL(k_cr_build, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, 0, -1,
-                     -1, d.var ? b.Adiag : nullptr);
+  cr_launch_build(d, s, d.nblk, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, 0, -1, -1, d.var ? b.Adiag : nullptr);
   const int bend = d.nblk - 1;
   cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
@@ -1584,7 +1653,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
-    hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(256), 0, s, d, st, 0, bend, b.st, b.Wc, b.dtau, b.dcv);
+    hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, d, st, 0, bend, b.st, b.Wc, b.dtau, b.dcv);
   }
   hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
                      b.normp);
@@ -2186,8 +2255,7 @@ int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
     hipLaunchKernelGGL(k_fte_assemble, dim3(h->f_hi - h->f_lo), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, 0,
                        h->f_lo, h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag);
     const int top = std::min(h->bend, d.nblk - 1);
-    hipLaunchKernelGGL(k_cr_build, dim3(top - h->a0 + 1), dim3(256), 0, s, d, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec,
-                       b.GBc, h->a0, h->a0, h->bend, nullptr);
+    cr_launch_build(d, s, top - h->a0 + 1, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, h->a0, h->a0, h->bend, nullptr);
     const double* Efin = dist_local_cr(h);
     hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part,
                        h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk));
@@ -2221,7 +2289,7 @@ int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
   for (int lv = dr.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (dr.nblk - st + 2 * st - 1) / (2 * st);
-    hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(256), 0, s, dr, st, 0, rb, b.st, r.Wc, b.dtau, r.dcv);
+    hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, dr, st, 0, rb, b.st, r.Wc, b.dtau, r.dcv);
   }
   // this chain: ends from the reduced solve, interior by back substitution
   ACS_HIP(ctx, hipMemsetAsync(p2, 0, sizeof(double) * h->Lo.n2, s));
@@ -2231,7 +2299,7 @@ int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
       const int st = 1 << lv;
       int ne = 0;
       for (int i = h->a0 + st; i < std::min(h->bend, d.nblk); i += 2 * st) ++ne;
-      if (ne) hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(256), 0, s, d, st, h->a0, h->bend, b.st, b.Wc, b.dtau, b.dcv);
+      if (ne) hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, d, st, h->a0, h->bend, b.st, b.Wc, b.dtau, b.dcv);
     }
     if (h->out_hi > h->out_lo)
       hipLaunchKernelGGL(k_dist_delta_out, dim3(64), dim3(256), 0, s, d, b.st, h->out_lo, h->out_hi, b.dcv, p2);

