@@ -628,8 +628,15 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
 #define CR_MAXBP 96
 
 #ifdef FTE_PROFILE  // per-phase wall-clock ticks (100 MHz) of block 0 (tools/prof_fte_phases.py)
-__device__ unsigned long long g_fte_prof[32];
-#define PROF_T0 unsigned long long t_prof = wall_clock64();
+__device__ unsigned long long g_fte_prof[64];
+#define PROF_T0 unsigned long long t_prof = wall_clock64(); const unsigned long long t_start = t_prof; \
+  const bool prof_on = ne * nsplit + (int)gridDim.x * 0 <= 12 && ne > 0;
+// timeline event: wave w of block 0 at time since the kernel start (deep levels only)
+#define PROFA(slot, w)                                                      \
+  do {                                                                      \
+    if (prof_on && blockIdx.x == 0 && threadIdx.x == 64 * (w))              \
+      atomicAdd(&g_fte_prof[slot], wall_clock64() - t_start);               \
+  } while (0)
 #define PROF(slot)                                                          \
   do {                                                                      \
     __syncthreads();                                                        \
@@ -652,6 +659,7 @@ __device__ unsigned long long g_fte_prof[32];
 #define PROF_T0
 #define PROF(slot)
 #define PROFW(slot, w)
+#define PROFA(slot, w)
 #endif
 
 template <int NB>
@@ -903,6 +911,11 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
       for (int q = 0; q < 4; ++q) G0[(K * 16 + lk + 4 * q) * GR + c0 + li] = t[K][q];
   }
+  PROFA(32, 0);
+  PROFA(33, NB);
+#ifdef FTE_PROFILE
+  if (prof_on && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fte_prof[63], 1ull);
+#endif
   PROF(0);
   // Gauss-Jordan elimination, pivot block k
 #pragma unroll
@@ -928,6 +941,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
           for (int q = 0; q < 4; ++q) Rk[(lk + 4 * q) * BP + K * 16 + li] = acc[q];
         }
+        PROFA(34 + k, k);
       } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q) Ck[(wave * 16 + lk + 4 * q) * TS + li] = t[k][q];
@@ -960,6 +974,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
       }
     }
   }
+  PROFA(40, NB);
   PROF(1);
   if (dwave || J < 0) return;
   // W_i (back substitution), Schur terms for the neighbours, Tau_i
@@ -1007,6 +1022,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   };
   // left term E_i^T W (columns W_l and W_gb)
   if (J < NB || J >= 2 * NB) term(aEiT, put_L);
+  PROFA(41, NB);
   PROFW(3, NB);
   PROFW(3 + 8, 15);
   // right term E_r W (columns W_r and W_gb) and the new coupling -E_r W_l
@@ -1023,6 +1039,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
         term(aEr_glb, put_R);
     }
   }
+  PROFA(42, NB);
   PROFW(4, NB);
   PROFW(4 + 8, 15);
   if (J >= 2 * NB) {
@@ -1038,6 +1055,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     }
   }
   PROFW(5 + 8, 15);
+  PROFA(43, NB);
 }
 
 // Fixed-order partial sums feeding the tau border (parallel over chunks, summed in chunk

@@ -7,6 +7,8 @@
 // K of 4. Every routine is called by all threads of the workgroup (blockDim = 256, 4 waves)
 // and ends with a __syncthreads().
 #pragma once
+#include <utility>
+
 #include "common.hpp"
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
@@ -41,39 +43,77 @@ __device__ void wg_mgemm(double* C, int ldc, const double* A, int lda, const dou
   __syncthreads();
 }
 
+// Cross-lane moves for a 16x16 f64 tile in accumulator layout (lane l: column l & 15 of
+// rows (l >> 4) + 4q), all on the VALU (no LDS round trip):
+//   tile_row_bcast<R>(x): every lane gets x from lane 16 R + (l & 15) — the row-of-16 R copied
+//                         to all four (gfx950 v_permlane32_swap + v_permlane16_swap);
+//   tile_col_bcast<S>(x): every lane gets x from lane 16 (l >> 4) + S — DPP row_newbcast:S.
+template <int R>
+__device__ __forceinline__ unsigned tile_row_bcast_u32(unsigned x) {
+  const auto h = __builtin_amdgcn_permlane32_swap(x, x, false, false);  // [lo|lo], [hi|hi]
+  const unsigned y = R < 2 ? h[0] : h[1];
+  const auto q = __builtin_amdgcn_permlane16_swap(y, y, false, false);  // even rows, odd rows
+  return (R & 1) ? q[1] : q[0];
+}
+template <int R>
+__device__ __forceinline__ double tile_row_bcast(double x) {
+  return __hiloint2double((int)tile_row_bcast_u32<R>((unsigned)__double2hiint(x)),
+                          (int)tile_row_bcast_u32<R>((unsigned)__double2loint(x)));
+}
+template <int S>
+__device__ __forceinline__ double tile_col_bcast(double x) {
+  return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(x), 0x150 + S, 0xf, 0xf, true),
+                          __builtin_amdgcn_mov_dpp(__double2loint(x), 0x150 + S, 0xf, 0xf, true));
+}
+__device__ __forceinline__ double read_lane_f64(double x, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                          __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+// 1/p: v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient)
+__device__ __forceinline__ double rcp_nr(double p) {
+  double r = __builtin_amdgcn_rcp(p);
+  r = fma(r, fma(-p, r, 1.0), r);
+  return fma(r, fma(-p, r, 1.0), r);
+}
+
+// One Gauss-Jordan step (pivot S) of tile16_gj_inverse; nbad counts failed pivots (uniform).
+template <int S, bool SPD>
+__device__ __forceinline__ void tile16_gj_step(double* v, int lane, int& nbad) {
+  constexpr int QS = S >> 2, RS = S & 3;
+  const bool rowS = (lane >> 4) == RS, colS = (lane & 15) == S;
+  double p = read_lane_f64(v[QS], RS * 16 + S);  // A[S][S] (uniform)
+  const double asc = tile_row_bcast<RS>(v[QS]);  // A[S][c]
+  double ais[4];                                 // A[i][S], i = (lane >> 4) + 4q
+#pragma unroll
+  for (int q = 0; q < 4; ++q) ais[q] = tile_col_bcast<S>(v[q]);
+  const bool ok = SPD ? p > 0.0 : fabs(p) > 1e-300;
+  nbad += ok ? 0 : 1;
+  p = ok ? p : 1e-300;
+  const double ip = rcp_nr(p);
+  const double aip = asc * ip;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    // a_ic - a_iS a_Sc / p off the pivot row / column, -a_iS / p on the column
+    const double t = colS ? -ais[q] * ip : fma(-ais[q], aip, v[q]);
+    // pivot row (only register QS holds it): a_Sc / p, and 1 / p on the diagonal
+    v[q] = (q == QS && rowS) ? (colS ? ip : aip) : t;
+  }
+}
+template <bool SPD, int... S>
+__device__ __forceinline__ void tile16_gj_steps(double* v, int lane, int& nbad, std::integer_sequence<int, S...>) {
+  (tile16_gj_step<S, SPD>(v, lane, nbad), ...);
+}
+
 // In-register Gauss-Jordan inverse of one 16x16 tile held by a wave in accumulator layout
-// (lane l: column l & 15 of rows (l >> 4) + 4q). Pivot row / column travel by shuffles:
-// 16 steps, no barrier. SPD: pivots must be positive; otherwise |p| > 1e-300. A failed
+// (lane l: column l & 15 of rows (l >> 4) + 4q). The pivot (v_readlane), pivot row
+// (permlane swaps) and pivot column (DPP row_newbcast) of each of the 16 steps move on the
+// VALU: no barrier, no LDS. SPD: pivots must be positive; otherwise |p| > 1e-300. A failed
 // pivot is replaced by 1e-300 and counted in *bad.
 template <bool SPD>
 __device__ __forceinline__ void tile16_gj_inverse(double* v, int lane, int* bad) {
-  const int r0 = lane >> 4, c = lane & 15;
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int qs = s >> 2, rs = s & 3;
-    double p = __shfl(v[qs], rs * 16 + s);          // A[s][s]
-    const double asc = __shfl(v[qs], rs * 16 + c);  // A[s][c]
-    double ais[4];                                  // A[i][s], i = r0 + 4q
-#pragma unroll
-    for (int q = 0; q < 4; ++q) ais[q] = __shfl(v[q], r0 * 16 + s);
-    if (SPD ? !(p > 0.0) : !(fabs(p) > 1e-300)) {
-      if (bad && lane == 0) atomicAdd(bad, 1);
-      p = 1e-300;
-    }
-    const double ip = 1.0 / p;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = r0 + 4 * q;
-      if (i == s && c == s)
-        v[q] = ip;
-      else if (i == s)
-        v[q] = asc * ip;
-      else if (c == s)
-        v[q] = -ais[q] * ip;
-      else
-        v[q] = v[q] - ais[q] * asc * ip;
-    }
-  }
+  int nbad = 0;
+  tile16_gj_steps<SPD>(v, lane, nbad, std::make_integer_sequence<int, 16>{});
+  if (nbad && bad && lane == 0) atomicAdd(bad, nbad);
 }
 
 // In-place inverse of an SPD matrix (n = 16*nb, LDS or global, ld) by blocked
