@@ -68,6 +68,55 @@ int acs_obs_to_slots(acs_ctx* ctx, const double* duv, const int32_t* dpi, const 
                      int64_t n_pts, int n_cams, double2** uv_pad, uint8_t** mask, uint8_t** camid, int* K_out);
 
 // ------------------------------------------------------------------------------------
+// Short-latency f64 math for the per-iteration dependency chains (measured on gfx950,
+// tools/probe/valu_lat_probe.hip: IEEE 1/x 72 cycles, sqrt 109, log1p 569; v_rcp_f64 +
+// two Newton steps 39, v_rsq_f64 + two Newton steps 49). Each result is within ~1 ulp of
+// the correctly rounded value (tests/test_native_abi.py checks the host build of the same
+// code). On the host the hardware estimates are replaced by the exact operation.
+// ------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ double rcp_nr(double p) {
+#ifdef __HIP_DEVICE_COMPILE__
+  double r = __builtin_amdgcn_rcp(p);
+  r = fma(r, fma(-p, r, 1.0), r);
+  return fma(r, fma(-p, r, 1.0), r);
+#else
+  return 1.0 / p;
+#endif
+}
+// 1/sqrt(x), x > 0
+__host__ __device__ __forceinline__ double rsq_nr(double x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const double h = 0.5 * x;
+  double r = __builtin_amdgcn_rsq(x);
+  r = r * fma(-h * r, r, 1.5);
+  return r * fma(-h * r, r, 1.5);
+#else
+  return 1.0 / std::sqrt(x);
+#endif
+}
+// log1p(t) for t >= 0 (finite): u = 1 + t with its exact rounding error c, u = 2^k m with
+// m in [1/sqrt2, sqrt2), log m = f - f^2/2 + s (f^2/2 + R(s^2)), s = f / (2 + f), f = m - 1
+// (the classic fdlibm reduction and minimax coefficients), one reciprocal, no table.
+__host__ __device__ __forceinline__ double log1p_pos(double t) {
+  const double u = 1.0 + t;
+  const double c = (t >= 1.0 ? 1.0 - (u - t) : t - (u - 1.0)) * rcp_nr(u);
+  int k;
+  double m = std::frexp(u, &k);  // [0.5, 1)
+  if (m < 0.70710678118654752440) {
+    m *= 2.0;
+    --k;
+  }
+  const double f = m - 1.0;
+  const double s = f * rcp_nr(2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
+  const double t2 = z * (6.666666666666735130e-01 +
+                         w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+  const double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
+  return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + (dk * 1.90821492927058770002e-10 + c))) - f);
+}
+
+// ------------------------------------------------------------------------------------
 // Fisheye camera model (cv::fisheye::projectPoints with alpha = 0; src/lib/calib.py:132,
 // restated by the reference itself in src/core/fte.py:80-96). Camera record layout:
 // [fx fy cx cy k1 k2 k3 k4 R00..R22 t0 t1 t2] (ACS_CAM_STRIDE = 20 doubles).
@@ -85,18 +134,21 @@ __device__ __forceinline__ void fisheye_project(const double* __restrict__ c, do
   const double Y0 = fma(c[8], X0, fma(c[9], X1, fma(c[10], X2, c[17])));
   const double Y1 = fma(c[11], X0, fma(c[12], X1, fma(c[13], X2, c[18])));
   const double Y2 = fma(c[14], X0, fma(c[15], X1, fma(c[16], X2, c[19])));
-  const double iz = 1.0 / Y2;
+  const double iz = rcp_nr(Y2);
   const double a = Y0 * iz;
   const double b = Y1 * iz;
   const double r2 = a * a + b * b;
   const double k1 = c[4], k2 = c[5], k3 = c[6], k4 = c[7];
-  double r = FTE_FORM ? sqrt(r2 + 1e-12) : sqrt(r2);
+  // r and 1/r from one reciprocal square root; OpenCV's guard r > 1e-8 (the FTE form's
+  // r = sqrt(r2 + 1e-12) needs none)
+  const bool big = FTE_FORM ? true : (r2 > 1e-16);
+  const double rr = FTE_FORM ? r2 + 1e-12 : (big ? r2 : 1.0);
+  const double ir = rsq_nr(rr);
+  const double r = big ? rr * ir : 0.0;
   const double th = atan(r);
   const double th2 = th * th;
   const double poly = 1.0 + th2 * (k1 + th2 * (k2 + th2 * (k3 + th2 * k4)));
   const double thd = th * poly;
-  const bool big = FTE_FORM ? true : (r > 1e-8);
-  const double ir = big ? 1.0 / r : 1.0;
   const double s = big ? thd * ir : 1.0;
   o.u = c[0] * (a * s) + c[2];
   o.v = c[1] * (b * s) + c[3];
@@ -106,9 +158,9 @@ __device__ __forceinline__ void fisheye_project(const double* __restrict__ c, do
     double spr;
     if (FTE_FORM) {
       // r = sqrt(a^2+b^2+eps): dr/da = a/r, same formula with this r
-      spr = (dthd * r / (1.0 + r * r) - thd) * (ir * ir * ir);
+      spr = (dthd * r * rcp_nr(1.0 + r * r) - thd) * (ir * ir * ir);
     } else {
-      spr = (r2 > 1e-16) ? (dthd * r / (1.0 + r2) - thd) * (ir * ir * ir) : 0.0;
+      spr = big ? (dthd * r * rcp_nr(1.0 + r2) - thd) * (ir * ir * ir) : 0.0;
     }
     const double duda = c[0] * (s + a * a * spr);
     const double dudb = c[0] * (a * b * spr);

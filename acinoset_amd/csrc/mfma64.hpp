@@ -69,13 +69,6 @@ __device__ __forceinline__ double read_lane_f64(double x, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
                           __builtin_amdgcn_readlane(__double2loint(x), l));
 }
-// 1/p: v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient)
-__device__ __forceinline__ double rcp_nr(double p) {
-  double r = __builtin_amdgcn_rcp(p);
-  r = fma(r, fma(-p, r, 1.0), r);
-  return fma(r, fma(-p, r, 1.0), r);
-}
-
 // One Gauss-Jordan step (pivot S) of tile16_gj_inverse; nbad counts failed pivots (uniform).
 template <int S, bool SPD>
 __device__ __forceinline__ void tile16_gj_step(double* v, int lane, int& nbad) {

@@ -105,11 +105,11 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
       fisheye_project<true>(oc[s], X0, X1, X2, o);
       const double r[2] = {o.u - ou[s], o.v - ov[s]};
       const double zu = r[0] * r[0] * if2, zv = r[1] * r[1] * if2;
-      Fl += log1p(zu + zv + zu * zv);  // log1p(zu) + log1p(zv) with one logarithm
+      Fl += log1p_pos(zu + zv + zu * zv);  // log1p(zu) + log1p(zv) with one logarithm
 #pragma unroll
       for (int d = 0; d < 2; ++d) {
         const double z = d ? zv : zu;
-        const double w = 1.0 / (1.0 + z);                   // rho'(z): gradient weight
+        const double w = rcp_nr(1.0 + z);                   // rho'(z): gradient weight
         const double wh = fmax((1.0 - z) * w * w, 0.1 * w);  // rho' + 2 z rho'' (Triggs), floored
         const double j0 = o.J[3 * d], j1 = o.J[3 * d + 1], j2 = o.J[3 * d + 2];
         const double hj0 = wh * j0, hj1 = wh * j1, hj2 = wh * j2;
@@ -151,15 +151,15 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     const double dl = 1.0 + lam;
     const double a00 = H[0] * dl, a11 = H[3] * dl, a22 = H[5] * dl;
     bool pd = a00 > 0.0;
-    const double i00 = pd ? 1.0 / sqrt(a00) : 1.0;  // reciprocal Cholesky diagonal
+    const double i00 = pd ? rsq_nr(a00) : 1.0;  // reciprocal Cholesky diagonal
     const double L10 = H[1] * i00, L20 = H[2] * i00;
     const double d11 = a11 - L10 * L10;
     pd = pd && d11 > 0.0;
-    const double i11 = pd ? 1.0 / sqrt(d11) : 1.0;
+    const double i11 = pd ? rsq_nr(d11) : 1.0;
     const double L21 = (H[4] - L20 * L10) * i11;
     const double d22 = a22 - L20 * L20 - L21 * L21;
     pd = pd && d22 > 0.0;
-    const double i22 = pd ? 1.0 / sqrt(d22) : 1.0;
+    const double i22 = pd ? rsq_nr(d22) : 1.0;
     double dx0 = 0.0, dx1 = 0.0, dx2 = 0.0;
     if (pd) {
       const double y0 = -g[0] * i00;
@@ -184,8 +184,11 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     linearize(n0, n1, n2, Hn, gn, Fn);
     ++nfev;
     ++iters;
-    const double xn = sqrt(x0 * x0 + x1 * x1 + x2 * x2);
-    const bool small = sqrt(dx0 * dx0 + dx1 * dx1 + dx2 * dx2) <= prm.xtol * (prm.xtol + xn);
+    // |dx| <= xtol (xtol + |x|), compared squared
+    const double xx = x0 * x0 + x1 * x1 + x2 * x2;
+    const double xn = xx > 0.0 ? xx * rsq_nr(xx) : 0.0;
+    const double xb = prm.xtol * (prm.xtol + xn);
+    const bool small = dx0 * dx0 + dx1 * dx1 + dx2 * dx2 <= xb * xb;
     if (pd && Fn < F) {
       const bool fconv = (F - Fn) <= prm.ftol * F;
       x0 = n0;

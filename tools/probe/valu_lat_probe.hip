@@ -23,6 +23,10 @@ __global__ void k(double* out, long long* cyc, int n, double seed) {
       if (OP == 8) x = rcp_nr(x);
       if (OP == 9) x = sqrt(x);
       if (OP == 10) x = (float)x * 1.0000001f;
+      if (OP == 11) x = atan(x) + 0.5;
+      if (OP == 12) x = log1p(x);
+      if (OP == 13) x = exp(-x);
+      if (OP == 14) { double r = __builtin_amdgcn_rsq(x); r = r * fma(-0.5 * x * r, r, 1.5); x = r * fma(-0.5 * x * r, r, 1.5) + 0.1; }
     }
   }
   long long t1 = clock64();
@@ -51,5 +55,9 @@ int main() {
   run<4>("readlane x2 + mul");
   run<5>("__shfl f64 + mul");
   run<10>("cvt f32 mul cvt");
+  run<11>("atan f64 (+add)");
+  run<12>("log1p f64");
+  run<13>("exp f64");
+  run<14>("rsq + 2 Newton (+add)");
   return 0;
 }
