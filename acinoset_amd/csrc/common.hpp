@@ -98,7 +98,7 @@ __device__ __forceinline__ void fisheye_project(const double* __restrict__ c, do
   const double rr = FTE_FORM ? r2 + 1e-12 : (big ? r2 : 1.0);
   const double ir = rsq_nr(rr);
   const double r = big ? rr * ir : 0.0;
-  const double th = atan(r);
+  const double th = atan_pos(r);
   const double th2 = th * th;
   const double poly = 1.0 + th2 * (k1 + th2 * (k2 + th2 * (k3 + th2 * k4)));
   const double thd = th * poly;
@@ -150,18 +150,19 @@ struct LossOut {
 
 __device__ __forceinline__ LossOut redescending(double err, double a, double b, double c) {
   const double E = fabs(err);
-  const double sa = 1.0 / (1.0 + exp(-(E - a)));
-  const double sb = 1.0 / (1.0 + exp(-(E - b)));
-  const double sc = 1.0 / (1.0 + exp(-(E - c)));
+  const double sa = rcp_nr(1.0 + exp(-(E - a)));
+  const double sb = rcp_nr(1.0 + exp(-(E - b)));
+  const double sc = rcp_nr(1.0 + exp(-(E - c)));
   const double da = sa * (1.0 - sa), db = sb * (1.0 - sb), dc = sc * (1.0 - sc);
   const double dda = da * (1.0 - 2.0 * sa), ddb = db * (1.0 - 2.0 * sb), ddc = dc * (1.0 - 2.0 * sc);
   const double lin = a * E - 0.5 * a * a;
   const double K3 = a * b - 0.5 * a * a;
   const double cb = c - b;
-  const double w = (c - E) / cb;
+  const double icb = rcp_nr(cb);
+  const double w = (c - E) * icb;
   const double q = K3 + (0.5 * a * cb) * (1.0 - w * w);
-  const double q1 = a * (c - E) / cb;
-  const double q2 = -a / cb;
+  const double q1 = a * (c - E) * icb;
+  const double q2 = -a * icb;
   const double K4 = K3 + 0.5 * a * cb;
   LossOut o;
   o.f = (1.0 - sa) * 0.5 * E * E + (sa - sb) * lin + (sb - sc) * q + sc * K4;

@@ -56,3 +56,29 @@ __host__ __device__ __forceinline__ double log1p_pos(double t) {
   const double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
   return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + (dk * 1.90821492927058770002e-10 + c))) - f);
 }
+
+// atan(x) for x >= 0 with one reciprocal: |v| <= tan(pi/8) after
+//   x <= tan(pi/8):            v = x,                 atan x = atan v
+//   tan(pi/8) < x <= tan(3pi/8): v = (x - 1)/(x + 1),   atan x = pi/4 + atan v
+//   x > tan(3pi/8):            v = -1/x,               atan x = pi/2 + atan v
+// and atan v = v - v (z S1(z^2) + z^2 S2(z^2)), z = v^2, with the fdlibm minimax
+// coefficients for |v| < 7/16 (odd and even halves evaluated as two independent chains).
+__host__ __device__ __forceinline__ double atan_pos(double x) {
+  const bool a = x <= 0.41421356237309504880, c = x > 2.41421356237309504880;
+  const double num = a ? x : (c ? -1.0 : x - 1.0);
+  const double den = a ? 1.0 : (c ? x : x + 1.0);
+  const double v = a ? x : num * rcp_nr(den);
+  const double hi = a ? 0.0 : (c ? 1.57079632679489655800e+00 : 7.85398163397448278999e-01);
+  const double lo = a ? 0.0 : (c ? 6.12323399573676603587e-17 : 3.06161699786838301793e-17);
+  const double z = v * v, w = z * z;
+  const double s1 = z * (3.33333333333329318027e-01 +
+                         w * (1.42857142725034663711e-01 +
+                              w * (9.09088713343650656196e-02 +
+                                   w * (6.66107313738753120669e-02 +
+                                        w * (4.97687799461593236017e-02 + w * 1.62858201153657823623e-02)))));
+  const double s2 = w * (-1.99999999998764832476e-01 +
+                         w * (-1.11111104054623557880e-01 +
+                              w * (-7.69187620504482999495e-02 +
+                                   w * (-5.83357013379057348645e-02 + w * -3.65315727442169155270e-02))));
+  return hi + ((v - v * (s1 + s2)) + lo);
+}
