@@ -129,27 +129,38 @@ def _read_dlc(path):
 
 def load_dlc_points_as_df(dlc_df_fpaths, frame_shifts=None, verbose=False):
     """`src/lib/utils.py:77-151` for standard DLC outputs (scorer/bodyparts/coords columns):
-    long DataFrame [frame, camera, marker, x, y, likelihood]."""
+    long DataFrame [frame, camera, marker, x, y, likelihood], camera-major, then frame, then
+    marker in sorted order (the reference's `.T.unstack().T` sorts the bodyparts level,
+    :115). A missing likelihood column becomes 1 where x is finite (:98-110). A frame shift
+    moves every marker's (x, y, likelihood) by that many frames; the frames shifted in are
+    NaN with likelihood 0 and the frame column is not shifted (:118-132)."""
     assert frame_shifts is None or len(dlc_df_fpaths) == len(frame_shifts)
     out = []
     for i, path in enumerate(dlc_df_fpaths):
         df = _read_dlc(path)
         df = df.droplevel(0, axis=1)                        # scorer
-        parts = list(dict.fromkeys(df.columns.get_level_values(0)))
+        parts = sorted(dict.fromkeys(df.columns.get_level_values(0)))
         coords = set(df.columns.get_level_values(1))
-        rows = []
         idx = df.index
         frames = np.array([int(str(s)[-7:-4]) if not np.issubdtype(type(s), np.integer) else int(s) for s in idx])
         shift = 0 if frame_shifts is None else int(frame_shifts[i])
-        for bp in parts:
+        n, L = len(frames), len(parts)
+        vals = np.full((3, n, L), np.nan)
+        for j, bp in enumerate(parts):
             x = df[(bp, 'x')].to_numpy(np.float64)
-            y = df[(bp, 'y')].to_numpy(np.float64)
-            lk = df[(bp, 'likelihood')].to_numpy(np.float64) if 'likelihood' in coords else np.isfinite(x) * 1.0
-            if shift:
-                x, y, lk = (np.roll(v, shift) for v in (x, y, lk))
-            rows.append(pd.DataFrame({'frame': frames, 'camera': i, 'marker': bp, 'x': x, 'y': y,
-                                      'likelihood': np.nan_to_num(lk)}))
-        out.append(pd.concat(rows, ignore_index=True).sort_values(['frame'], kind='stable'))
+            vals[0, :, j] = x
+            vals[1, :, j] = df[(bp, 'y')].to_numpy(np.float64)
+            vals[2, :, j] = df[(bp, 'likelihood')].to_numpy(np.float64) if 'likelihood' in coords else np.isfinite(x)
+        if shift:
+            sh = np.full_like(vals, np.nan)
+            if shift > 0:
+                sh[:, shift:] = vals[:, :n - shift]
+            else:
+                sh[:, :n + shift] = vals[:, -shift:]
+            vals = sh
+        out.append(pd.DataFrame({'frame': np.repeat(frames, L), 'camera': i, 'marker': np.tile(parts, n),
+                                 'x': vals[0].ravel(), 'y': vals[1].ravel(),
+                                 'likelihood': np.nan_to_num(vals[2].ravel())}))
     dlc = pd.concat(out, ignore_index=True)[['frame', 'camera', 'marker', 'x', 'y', 'likelihood']]
     if verbose:
         print(f'DLC points dataframe:\n{dlc}\n')

@@ -1,4 +1,5 @@
 """CPU: host-side glue of the drop-in layer (no GPU calls)."""
+import pytest
 import numpy as np
 import pandas as pd
 
@@ -106,3 +107,58 @@ def test_states_variable_shutter_delay_layout():
     tau = np.arange(15.0).reshape(5, 3) * 1e-4
     st = cfte.states_from_solution(X, tau, 1 / 90, True, 5)
     assert np.array_equal(np.asarray(st['shutter_delay']), tau.T)
+
+
+def _dlc_csv(path, parts, n, seed, likelihood=True, str_index=False):
+    """A DLC-style export: 3 header rows (scorer / bodyparts / coords), one row per frame."""
+    rng = np.random.default_rng(seed)
+    coords = ['x', 'y', 'likelihood'] if likelihood else ['x', 'y']
+    cols = pd.MultiIndex.from_product([['DLC_resnet50_cheetahOct1shuffle1_200000'], parts, coords],
+                                      names=['scorer', 'bodyparts', 'coords'])
+    v = rng.uniform(0, 1000, (n, len(cols)))
+    v[rng.random(v.shape) < 0.05] = np.nan
+    idx = [f'labeled-data/run/img{k:03d}.png' for k in range(n)] if str_index else np.arange(n)
+    df = pd.DataFrame(v, index=idx, columns=cols)
+    df.to_csv(path)
+    return df
+
+
+def _expected_long(df, cam, shift):
+    """Row-by-row restatement of src/lib/utils.py:77-151 on one file: markers in sorted order
+    within a frame (the `.T.unstack().T` reshape sorts the bodyparts level, :115), rows moved
+    by `shift` frames with NaN / likelihood 0 shifted in (:118-132), frame column unshifted."""
+    d = df.droplevel(0, axis=1)
+    parts = sorted(set(d.columns.get_level_values(0)))
+    has_lk = 'likelihood' in set(d.columns.get_level_values(1))
+    n = len(d)
+    frames = [int(str(s)[-7:-4]) if isinstance(s, str) else int(s) for s in d.index]
+    rows = []
+    for k in range(n):
+        src = k - shift
+        for bp in parts:
+            if 0 <= src < n:
+                x, y = d[(bp, 'x')].iloc[src], d[(bp, 'y')].iloc[src]
+                lk = d[(bp, 'likelihood')].iloc[src] if has_lk else (0.0 if np.isnan(x) else 1.0)
+            else:
+                x = y = lk = np.nan
+            rows.append((frames[k], cam, bp, x, y, 0.0 if np.isnan(lk) else lk))
+    return pd.DataFrame(rows, columns=['frame', 'camera', 'marker', 'x', 'y', 'likelihood'])
+
+
+@pytest.mark.parametrize('shifts', [None, [0, 2, -3]])
+def test_load_dlc_points_as_df_matches_reference_reshape(tmp_path, shifts):
+    from acinoset_amd.lib import utils as lu
+    parts = ['nose', 'r_eye', 'l_eye', 'neck_base', 'tail_tip']
+    paths, dfs = [], []
+    for c in range(3):
+        p = str(tmp_path / f'cam{c + 1}DLC.csv')
+        dfs.append(_dlc_csv(p, parts, 12, seed=c, likelihood=(c != 1), str_index=(c == 2)))
+        paths.append(p)
+    got = lu.load_dlc_points_as_df(paths, frame_shifts=shifts)
+    exp = pd.concat([_expected_long(df, c, 0 if shifts is None else shifts[c]) for c, df in enumerate(dfs)],
+                    ignore_index=True)
+    assert list(got.columns) == ['frame', 'camera', 'marker', 'x', 'y', 'likelihood']
+    assert got[['frame', 'camera', 'marker']].astype(str).equals(exp[['frame', 'camera', 'marker']].astype(str))
+    for col in ('x', 'y', 'likelihood'):
+        np.testing.assert_allclose(got[col].to_numpy(float), exp[col].to_numpy(float), rtol=0, atol=1e-9,
+                                   equal_nan=True)
