@@ -925,18 +925,23 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     double* Ck = Rk + 16 * BP;         // old pivot column-block of D, BP x 16 (stride TS)
     if (dwave) {
       if (wave == k) {
-        double v[4] = {t[k][0], t[k][1], t[k][2], t[k][3]};
-        tile16_gj_inverse<true>(v, lane, part ? nullptr : bad);
+        // pivot tile inverse: pivot 0 here, pivot k > 0 already inverted by this wave at the
+        // end of step k-1 (overlapped with its remaining row updates)
+        if (k == 0) {
+          double v[4] = {t[0][0], t[0][1], t[0][2], t[0][3]};
+          tile16_gj_inverse<true>(v, lane, part ? nullptr : bad);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          t[k][q] = v[q];
-          Pk[(lk + 4 * q) * TS + li] = v[q];
+          for (int q = 0; q < 4; ++q) t[0][q] = v[q];
         }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Pk[(lk + 4 * q) * TS + li] = t[k][q];
+        // R_kK = D_kk^-1 D_kK; the A operand (row li, column 4ks + lk of the symmetric
+        // inverse) is register ks of the inverse itself: no LDS round trip
 #pragma unroll
         for (int K = k + 1; K < NB; ++K) {
           dbl4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int ks = 0; ks < 4; ++ks) acc = mfma64(Pk[li * TS + 4 * ks + lk], t[K][ks], acc);
+          for (int ks = 0; ks < 4; ++ks) acc = mfma64(t[k][ks], t[K][ks], acc);
           t[K] = acc;
 #pragma unroll
           for (int q = 0; q < 4; ++q) Rk[(lk + 4 * q) * BP + K * 16 + li] = acc[q];
@@ -949,7 +954,28 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     }
     __syncthreads();
     if (dwave) {
-      if (wave != k) {
+      if (wave == k + 1) {
+        // next pivot: its diagonal tile first, then its inverse with the remaining row
+        // updates (MFMA) slotted between the pivot steps (VALU)
+        PROFA(44 + k, k + 1);
+        {
+          dbl4 acc = t[k + 1];
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks)
+            acc = mfma64(-Ck[(wave * 16 + li) * TS + 4 * ks + lk], Rk[(4 * ks + lk) * BP + (k + 1) * 16 + li], acc);
+          t[k + 1] = acc;
+        }
+        double v[4] = {t[k + 1][0], t[k + 1][1], t[k + 1][2], t[k + 1][3]};
+        tile16_gj_inverse_hook<true>(v, lane, part ? nullptr : bad, [&](auto sc) {
+          constexpr int S = decltype(sc)::value;
+          const int K = k + 2 + S / 4, ks = S % 4;  // constants once the k loop is unrolled
+          if (K < NB)
+            t[K] = mfma64(-Ck[(wave * 16 + li) * TS + 4 * ks + lk], Rk[(4 * ks + lk) * BP + K * 16 + li], t[K]);
+        });
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[k + 1][q] = v[q];
+        PROFA(50 + k, k + 1);
+      } else if (wave != k) {
 #pragma unroll
         for (int K = k + 1; K < NB; ++K) {
           dbl4 acc = t[K];
@@ -976,6 +1002,83 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   }
   PROFA(40, NB);
   PROF(1);
+  if (nsplit >= 3 && ((NBB + nsplit - 1) / nsplit) * BP * 16 <= 2 * BUF) {
+    // Deep levels (few column-blocks per workgroup): the Schur terms are dealt out to all 16
+    // waves instead of each column wave forming its own 2 NB output tiles, which would
+    // serialise on one SIMD's matrix core. The W column-blocks go to LDS (the pivot buffers
+    // are free once every wave is past the last pivot step) and to global memory.
+    const int nJ = (NBB - part + nsplit - 1) / nsplit;
+    double* sWl = lds;  // nJ x (BP x 16)
+    __syncthreads();
+    if (!dwave && J >= 0) {
+      const int jl = wave - NB;
+      double* W = Wc + (size_t)i * BP * WL;
+      const int wcol = J < NB ? J * 16 : (J < 2 * NB ? BP + (J - NB) * 16 : 2 * BP + (J - 2 * NB) * 16);
+#pragma unroll
+      for (int K = 0; K < NB; ++K)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          W[(size_t)(K * 16 + lk + 4 * q) * WL + wcol + li] = t[K][q];
+          sWl[(size_t)jl * BP * 16 + (K * 16 + lk + 4 * q) * 16 + li] = t[K][q];
+        }
+    }
+    __syncthreads();
+    const int per = 2 * NB + 1;
+    for (int task = wave; task < nJ * per; task += 16) {
+      const int jl = task / per, rr = task - jl * per;
+      const int Jt = part + nsplit * jl;
+      const double* w = sWl + (size_t)jl * BP * 16;
+      const int ocol = Jt < NB ? Jt * 16 : (Jt < 2 * NB ? (Jt - NB) * 16 : BP + (Jt - 2 * NB) * 16);
+      auto chain = [&](auto aop, int I) {
+        dbl4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int K = 0; K < NB; K += 2) {
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            a0 = mfma64(aop(I, K, ks), w[(K * 16 + 4 * ks + lk) * 16 + li], a0);
+            if (K + 1 < NB) a1 = mfma64(aop(I, K + 1, ks), w[((K + 1) * 16 + 4 * ks + lk) * 16 + li], a1);
+          }
+        }
+        return a0 + a1;
+      };
+      if (rr < NB) {  // left term E_i^T [W_l | W_gb], output tile I
+        if (Jt >= NB && Jt < 2 * NB) continue;
+        const dbl4 acc = chain([&](int I, int K, int ks) { return sEi[(K * 16 + 4 * ks + lk) * BP + I * 16 + li]; }, rr);
+        double* o = dL + (size_t)i * BP * LDD;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[(size_t)(rr * 16 + lk + 4 * q) * LDD + ocol + li] = acc[q];
+      } else if (rr < 2 * NB) {  // right term E_r [W_r | W_gb] and the new coupling -E_r W_l
+        if (!Er) continue;
+        const int I = rr - NB;
+        const dbl4 acc = sEr ? chain([&](int I_, int K, int ks) { return sEr[(I_ * 16 + li) * (BP + 1) + K * 16 + 4 * ks + lk]; }, I)
+                             : chain([&](int I_, int K, int ks) { return Er[(I_ * 16 + li) * BP + K * 16 + 4 * ks + lk]; }, I);
+        if (Jt < NB) {
+          double* o = Eout + (size_t)r * BP * BP;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[(size_t)(I * 16 + lk + 4 * q) * BP + Jt * 16 + li] = -acc[q];
+        } else {
+          double* o = dR + (size_t)i * BP * LDD;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[(size_t)(I * 16 + lk + 4 * q) * LDD + ocol + li] = acc[q];
+        }
+      } else {  // Tau_i = GB_i^T W_gb
+        if (Jt < 2 * NB) continue;
+        const int g = Jt - 2 * NB;
+        for (int g2 = 0; g2 < GRB; ++g2) {
+          dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int K = 0; K < NB; ++K)
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+              acc = mfma64(G0[(K * 16 + 4 * ks + lk) * GR + g2 * 16 + li], w[(K * 16 + 4 * ks + lk) * 16 + li], acc);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Tau[(size_t)i * GR * GR + (g2 * 16 + lk + 4 * q) * GR + g * 16 + li] = acc[q];
+        }
+      }
+    }
+    PROFA(43, 0);
+    return;
+  }
   if (dwave || J < 0) return;
   // W_i (back substitution), Schur terms for the neighbours, Tau_i
   double* W = Wc + (size_t)i * BP * WL;
@@ -1077,17 +1180,28 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
   const int fc = (nf + CR_NCHUNK - 1) / CR_NCHUNK, bc = (nb + CR_NCHUNK - 1) / CR_NCHUNK;
   const int k0 = k_lo + ch * fc, k1 = min(k_hi, k0 + fc);
   const int b0 = b_lo + ch * bc, b1 = min(b_hi, b0 + bc);
-  for (int e = threadIdx.x; e < nE; e += blockDim.x) {
+  // 8 loads in flight per thread (the frame / block loops are strided gathers), summed in
+  // index order
+  auto sum8 = [](const double* base, size_t stride, int lo, int hi) {
     double v = 0.0;
+    for (int k = lo; k < hi; k += 8) {
+      double t[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t[q] = k + q < hi ? base[(size_t)(k + q) * stride] : 0.0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v += t[q];
+    }
+    return v;
+  };
+  for (int e = threadIdx.x; e < nE; e += blockDim.x) {
+    double v;
     if (e < nH) {
       const int r = e / Cg, c = e % Cg;
-      for (int k = k0; k < k1; ++k) v += Hloc[(size_t)k * FTE_NZP * FTE_NZP + (P + 6 + r) * FTE_NZP + P + 6 + c];
+      v = sum8(Hloc + (P + 6 + r) * FTE_NZP + P + 6 + c, (size_t)FTE_NZP * FTE_NZP, k0, k1);
     } else if (e < nH + Cg) {
-      const int r = e - nH;
-      for (int k = k0; k < k1; ++k) v += gloc[(size_t)k * FTE_NZP + P + 6 + r];
+      v = sum8(gloc + P + 6 + (e - nH), FTE_NZP, k0, k1);
     } else {
-      const int t = e - nH - Cg;
-      for (int b = b0; b < b1; ++b) v += Tau[(size_t)b * GR * GR + t];
+      v = sum8(Tau + (e - nH - Cg), (size_t)GR * GR, b0, b1);
     }
     part[(size_t)ch * nE + e] = v;
   }
@@ -1601,7 +1715,9 @@ static void cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int
   // workgroups per eliminated block: enough column waves (16 - NB per workgroup), and more
   // of them when few blocks are left (the deep levels are latency-bound)
   const int need = (NBB + 16 - NB - 1) / (16 - NB);
-  const int want = ne <= 32 ? 4 : (ne <= 96 ? 2 : 1);
+  // one column-block per workgroup while the grid still fits the 256 CUs in one wave of
+  // workgroups (one 1024-thread workgroup per CU: the LDS is full)
+  const int want = ne * NBB + ns <= 256 ? NBB : (ne <= 32 ? 4 : (ne <= 96 ? 2 : 1));
   const int nsplit = std::min(std::max(need, want), NBB);
   const int nwg = ne * nsplit + ns;
   const size_t lds = sizeof(double) * (2 * (16 * 17 + 16 * (size_t)d.BP + 17 * (size_t)d.BP) + (size_t)d.BP * d.GR +

@@ -7,6 +7,7 @@
 // K of 4. Every routine is called by all threads of the workgroup (blockDim = 256, 4 waves)
 // and ends with a __syncthreads().
 #pragma once
+#include <type_traits>
 #include <utility>
 
 #include "common.hpp"
@@ -95,6 +96,21 @@ __device__ __forceinline__ void tile16_gj_step(double* v, int lane, int& nbad) {
 template <bool SPD, int... S>
 __device__ __forceinline__ void tile16_gj_steps(double* v, int lane, int& nbad, std::integer_sequence<int, S...>) {
   (tile16_gj_step<S, SPD>(v, lane, nbad), ...);
+}
+
+// The same 16 steps with hook(std::integral_constant<int, s>) called after step s: lets
+// a caller slot independent MFMA work (the matrix core runs it asynchronously) into the
+// VALU-bound pivot chain.
+template <bool SPD, typename Hook, int... S>
+__device__ __forceinline__ void tile16_gj_steps_hook(double* v, int lane, int& nbad, Hook& hook,
+                                                     std::integer_sequence<int, S...>) {
+  ((tile16_gj_step<S, SPD>(v, lane, nbad), hook(std::integral_constant<int, S>{})), ...);
+}
+template <bool SPD, typename Hook>
+__device__ __forceinline__ void tile16_gj_inverse_hook(double* v, int lane, int* bad, Hook&& hook) {
+  int nbad = 0;
+  tile16_gj_steps_hook<SPD>(v, lane, nbad, hook, std::make_integer_sequence<int, 16>{});
+  if (nbad && bad && lane == 0) atomicAdd(bad, nbad);
 }
 
 // In-register Gauss-Jordan inverse of one 16x16 tile held by a wave in accumulator layout

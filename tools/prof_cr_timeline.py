@@ -26,5 +26,5 @@ names = {32: 'wave 0 loads done', 33: 'col wave loads done', 34: 'pivot 0 inv+ro
          37: 'pivot 3', 38: 'pivot 4', 39: 'pivot 5', 40: 'col wave GJ done', 41: 'left term done',
          42: 'right term done', 43: 'Tau done'}
 print(f'deep launches {buf[63]}; mean us since kernel start:')
-for k, nm in names.items():
+for k, nm in sorted(names.items(), key=lambda kv: v[kv[0]]):
     print(f'{nm:24s} {v[k]:8.2f}')
