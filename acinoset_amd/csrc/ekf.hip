@@ -8,7 +8,8 @@
 //   1. constant-acceleration prediction; P <- F P F^T + Q column/row-wise in LDS (F is
 //      identity plus two scaled block shifts, so no dense product is needed)
 //   2. measurement model: the P+1 poses of the forward-difference Jacobian (:81-96) are
-//      evaluated one per wave (table FK in LDS + fisheye projection of C x L markers)
+//      evaluated together, every thread on independent (pose, joint) / (pose, marker) items
+//      (ekf_fk_batch), then the fisheye projection of (P+1) x C x L markers
 //   3. Kalman update in information form on the pose block: with H = [H_x 0 0] and R
 //      diagonal, K r = P[:,x] (I + A P_xx)^-1 b and (I - K H) P = P - P[:,x] (I + A P_xx)^-1
 //      A P[x,:], A = H_x^T R^-1 H_x, b = H_x^T R^-1 r (Woodbury; one P x P solve by
@@ -17,25 +18,170 @@
 // With F32 (the reference numerics) the predicted state is rounded to float32 (:79), the
 // FK trig runs in float32, and the Jacobian perturbation is x + 1e-3 in float32.
 //
-// k_ekf_smooth (256 threads): RTS backward pass (:280-287) with the predicted covariance
-// inverted by blocked Gauss-Jordan on f64 MFMA tiles and the gain / covariance products on
-// wg_mgemm.
+// RTS backward pass (:292-296): the gains A_i = P_est[i] F^T P_pred[i+1]^-1 do not depend
+// on the smoothed states, so k_ekf_gain computes them for every (sequence, frame) pair in
+// parallel (blocked Gauss-Jordan on f64 MFMA tiles), and k_ekf_smooth_x runs the state
+// recursion per sequence; k_ekf_smooth (sequential) when the smoothed covariances are asked.
 #include "fk.hpp"
 #include "mfma64.hpp"
 
 #define EKF_WAVES 8
 
 struct EkfDims {
-  int N, C, L, P, n, npad, Ppad, m, mpad, S, n_ints, n_reals;
+  int N, C, L, P, J, n, npad, Ppad, m, mpad, S, n_ints, n_reals;
   double sT, thresh, maxpix, eps;
 };
 
-__device__ __forceinline__ void ekf_pose(const double* s, int P, int q, bool f32, double eps, double* xq, int lane) {
-  for (int p = lane; p < P; p += 64) {
-    double v = s[p];
-    if (q > 0 && p == q - 1) v = f32 ? (double)((float)v + (float)eps) : v + eps;
-    xq[p] = v;
+// LDS doubles of the batched FK of the P+1 Jacobian poses (ekf_fk_batch)
+__host__ __device__ inline size_t ekf_fk_lds(int P, int J, int L) {
+  return (size_t)FK_MAXJ * 9 + (size_t)(FK_MAXP + 1) * 9 + (size_t)(P + 1) * (9 * J + 3 * L + 6) + 4 * FK_MAXP;
+}
+
+// Parameter p of Jacobian pose q (q = 0: the predicted state; q > 0: parameter q-1 moved by
+// eps, in float32 with the reference numerics, src/core/ekf.py:81-96).
+template <bool F32>
+__device__ __forceinline__ double ekf_xq(const double* s, int q, int p, double eps) {
+  const double v = s[p];
+  if (q > 0 && p == q - 1) return F32 ? (double)((float)v + (float)eps) : v + eps;
+  return v;
+}
+
+// Marker positions of all P+1 poses of the forward-difference Jacobian at once, every
+// thread of the workgroup on independent (pose, joint) / (pose, marker) items. Same
+// arithmetic as fk_frame (fk.hpp), so bit-identical positions: G_j = A_{n-1}..A_0 per
+// joint, M_j = G_root .. G_parent G_j by 3x3 products walking to the root, node = sum of
+// M_frame offsets walking to the root. A pose differs from pose 0 in one parameter, so
+// only one G per pose is recomputed (that of the parameter's joint, if a rotation).
+// Output: pos (P+1) x L x 3 in LDS (after the final barrier).
+template <bool F32>
+__device__ void ekf_fk_batch(const SkelView& sk, const double* ss, double eps, double* fk, int tid, int nth) {
+  const int P = sk.P, J = sk.J, L = sk.L, NQ = P + 1;
+  double* Gb = fk;                        // FK_MAXJ x 9: G of pose 0
+  double* Gq = Gb + FK_MAXJ * 9;          // (FK_MAXP + 1) x 9: G of the moved joint of pose q
+  double* M = Gq + (FK_MAXP + 1) * 9;     // NQ x J x 9
+  double* pos = M + (size_t)NQ * J * 9;   // NQ x L x 3
+  double* rw = pos + (size_t)NQ * L * 3;  // NQ x 6: root, world translation
+  double* sc = rw + (size_t)NQ * 6;       // sin, cos of pose 0; sin, cos of the moved parameter
+  const int* pk = sk.pk;
+  // 0. trig of every parameter (as given and as moved), per-pose translations
+  for (int e = tid; e < 2 * P + 2 * NQ; e += nth) {
+    if (e < 2 * P) {
+      const int p = e % P, mv = e / P;
+      const double v = ekf_xq<F32>(ss, mv ? p + 1 : 0, p, eps);
+      double sn, cs;
+      if (F32) {
+        float sf, cf;
+        sincosf((float)v, &sf, &cf);
+        sn = sf;
+        cs = cf;
+      } else {
+        sincos(v, &sn, &cs);
+      }
+      sc[(2 * mv) * FK_MAXP + p] = sn;
+      sc[(2 * mv + 1) * FK_MAXP + p] = cs;
+    } else {
+      const int q = (e - 2 * P) >> 1, kind = ((e - 2 * P) & 1) ? PK_WORLD : PK_TRANS;
+      double t[3] = {0.0, 0.0, 0.0};
+      for (int p = 0; p < P; ++p)
+        if (pk[4 * p] == kind) {
+          const int a = pk[4 * p + 1];
+          const double x = ekf_xq<F32>(ss, q, p, eps);
+          t[0] += a == 0 ? x : 0.0;
+          t[1] += a == 1 ? x : 0.0;
+          t[2] += a == 2 ? x : 0.0;
+        }
+      double* dst = rw + q * 6 + (kind == PK_WORLD ? 3 : 0);
+      dst[0] = t[0];
+      dst[1] = t[1];
+      dst[2] = t[2];
+    }
   }
+  __syncthreads();
+  // 1. G of every joint at pose 0, and of the moved joint of each pose q > 0
+  for (int e = tid; e < J + P; e += nth) {
+    int j, moved;
+    double* out;
+    if (e < J) {
+      j = e;
+      moved = -1;
+      out = Gb + 9 * j;
+    } else {
+      moved = e - J;  // pose q = moved + 1
+      if (pk[4 * moved] != PK_ROT) continue;
+      j = pk[4 * moved + 1];
+      out = Gq + 9 * (moved + 1);
+    }
+    const int* jt = sk.joints + 8 * j;
+    const int nrot = jt[1];
+#pragma unroll
+    for (int col = 0; col < 3; ++col) {
+      double v[3] = {col == 0 ? 1.0 : 0.0, col == 1 ? 1.0 : 0.0, col == 2 ? 1.0 : 0.0};
+      for (int r = 0; r < nrot; ++r) {
+        double w[3];
+        const int p = jt[5 + r];
+        const int mv = p == moved ? 2 : 0;
+        act_rot_vec(jt[2 + r], sc[mv * FK_MAXP + p], sc[(mv + 1) * FK_MAXP + p], v, w);
+        v[0] = w[0];
+        v[1] = w[1];
+        v[2] = w[2];
+      }
+      out[col] = v[0];
+      out[3 + col] = v[1];
+      out[6 + col] = v[2];
+    }
+  }
+  __syncthreads();
+  // 2. M_j of every pose
+  for (int e = tid; e < NQ * J; e += nth) {
+    const int q = e / J, j = e - q * J;
+    const int mj = (q > 0 && pk[4 * (q - 1)] == PK_ROT) ? pk[4 * (q - 1) + 1] : -1;
+    auto G = [&](int k) -> const double* { return k == mj ? Gq + 9 * q : Gb + 9 * k; };
+    double Mm[9], T[9];
+    const double* g0 = G(j);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Mm[i] = g0[i];
+    int k = sk.joints[8 * j];
+    while (k >= 0) {
+      mat3_mul(G(k), Mm, T);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Mm[i] = T[i];
+      k = sk.joints[8 * k];
+    }
+    double* o = M + (size_t)e * 9;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o[i] = Mm[i];
+  }
+  __syncthreads();
+  // 3. marker positions
+  for (int e = tid; e < NQ * L; e += nth) {
+    const int q = e / L, l = e - q * L;
+    const double* Mq = M + (size_t)q * J * 9;
+    double p0 = 0.0, p1 = 0.0, p2 = 0.0;
+    int node = sk.outn[l];
+    while (true) {
+      const int* nd = sk.nodes + 4 * node;
+      const int base = nd[0];
+      if (base == -2 || base == -1) {
+        const double* t = rw + q * 6 + (base == -2 ? 3 : 0);
+        p0 += t[0];
+        p1 += t[1];
+        p2 += t[2];
+        break;
+      }
+      const double* Mf = Mq + 9 * nd[1];
+      double o0 = sk.off[3 * node], o1 = sk.off[3 * node + 1], o2 = sk.off[3 * node + 2];
+      if (nd[2] >= 0) o0 = ekf_xq<F32>(ss, q, nd[2], eps);
+      p0 += Mf[0] * o0 + Mf[1] * o1 + Mf[2] * o2;
+      p1 += Mf[3] * o0 + Mf[4] * o1 + Mf[5] * o2;
+      p2 += Mf[6] * o0 + Mf[7] * o1 + Mf[8] * o2;
+      node = base;
+    }
+    double* o = pos + (size_t)e * 3;
+    o[0] = p0;
+    o[1] = p1;
+    o[2] = p2;
+  }
+  __syncthreads();
 }
 
 template <bool F32>
@@ -55,18 +201,16 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   extern __shared__ double lds[];
   double* sP = lds;                                   // npad x LDP: covariance
   double* U = sP + (size_t)d.npad * LDP;              // union: FK phase / algebra phase
-  FkShared* fks = reinterpret_cast<FkShared*>(U);     // EKF_WAVES poses
+  double* fkb = U;                                    // batched FK of the P+1 poses
   double* sPx = U;                                    // npad x Pp: P[:, x] before the update
   double* aug = sPx + (size_t)d.npad * Pp;            // Pp x AW
   double* sA = aug + (size_t)Pp * AW;                 // Pp x Pp
   // the FK and algebra phases share U; what follows must start past the larger of the two
-  const size_t u_fk = (size_t)EKF_WAVES * sizeof(FkShared) / sizeof(double);
+  const size_t u_fk = ekf_fk_lds(P, d.J, d.L);
   const size_t u_la = (size_t)d.npad * Pp + (size_t)Pp * AW + (size_t)Pp * Pp;
   double* ss = U + (u_fk > u_la ? u_fk : u_la);      // n: state
-  double* sx = ss + d.npad;                           // EKF_WAVES x FK_MAXP pose vectors
-  double* sRl = sx + EKF_WAVES * FK_MAXP;             // skeleton table (reals, then ints)
+  double* sRl = ss + d.npad;                          // skeleton table (reals, then ints)
   int* sI = reinterpret_cast<int*>(sRl + d.n_reals);
-  __shared__ int s_piv;
 #ifdef EKF_PROFILE  // per-phase cycle counts (tools/prof_ekf_phases.py)
   __shared__ unsigned long long s_prof[8];
   unsigned long long t_last = 0;
@@ -155,29 +299,24 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
 
     EKF_TICK(1);
     // ---- 2. poses of the forward-difference Jacobian --------------------------------
-    for (int b0 = 0; b0 <= P; b0 += EKF_WAVES) {
-      const int q = b0 + wave;
-      double* xq = sx + wave * FK_MAXP;
-      ekf_pose(ss, P, q <= P ? q : 0, F32, d.eps, xq, lane);
-      __syncthreads();
+    {
 #ifdef EKF_PROFILE
       const unsigned long long tf0 = clock64();
 #endif
-      fk_frame<F32>(sk, xq, fks[wave], lane, 64);
-      __syncthreads();
+      ekf_fk_batch<F32>(sk, ss, d.eps, fkb, tid, nth);
 #ifdef EKF_PROFILE
-      if (tid == 0) s_prof[7] += clock64() - tf0;   // FK share of the FK/proj phase
+      if (tid == 0) s_prof[7] += clock64() - tf0;  // FK share of the FK/proj phase
 #endif
-      if (q <= P) {
-        for (int o = lane; o < d.C * d.L; o += 64) {
-          const int c = o / d.L, l = o % d.L;
-          const int node = sk.outn[l];
-          ProjOut po;
-          fisheye_project<false>(cams + c * ACS_CAM_STRIDE, fks[wave].pos[node][0], fks[wave].pos[node][1],
-                                 fks[wave].pos[node][2], po);
-          hpose[(size_t)q * m + 2 * o] = po.u;
-          hpose[(size_t)q * m + 2 * o + 1] = po.v;
-        }
+      const double* pos = fkb + FK_MAXJ * 9 + (FK_MAXP + 1) * 9 + (size_t)(P + 1) * d.J * 9;
+      const int CL = d.C * d.L;
+      for (int e = tid; e < (P + 1) * CL; e += nth) {
+        const int q = e / CL, o = e - q * CL;
+        const int c = o / d.L, l = o - c * d.L;
+        const double* x = pos + ((size_t)q * d.L + l) * 3;
+        ProjOut po;
+        fisheye_project<false>(cams + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
+        hpose[(size_t)q * m + 2 * o] = po.u;
+        hpose[(size_t)q * m + 2 * o + 1] = po.v;
       }
       __syncthreads();
     }
@@ -254,50 +393,94 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     if (tid >= P && tid < Pp) aug[tid * AW + Pp + d.npad] = 0.0;
     __syncthreads();
     EKF_TICK(5);
-    // Gauss-Jordan with partial pivoting on the P x P block (4 barriers per pivot):
-    // pivot search | row swap | eliminate with the unscaled pivot row (row k and column k
-    // untouched) | scale row k, clear column k
-    for (int k = 0; k < P; ++k) {
-      if (wave == 0) {
-        double best = -1.0;
-        int bi = k;
-        for (int r = k + lane; r < P; r += 64) {
-          const double v = fabs(aug[r * AW + k]);
-          if (v > best) {
-            best = v;
-            bi = r;
-          }
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-          const double ob = __shfl_xor(best, off);
-          const int oi = __shfl_xor(bi, off);
-          if (ob > best || (ob == best && oi < bi)) {
-            best = ob;
-            bi = oi;
-          }
-        }
-        if (lane == 0) s_piv = bi;
+    // Gauss-Jordan with partial pivoting on the P x P block, register-resident and one
+    // barrier per pivot. Thread (row gr = tid & 31, column group cg = tid >> 5) holds
+    // aug[gr][cg + 16 j]; pivoting is implicit (rows stay in place, a row is "used" once it
+    // has been a pivot). Step k: the 32 lanes owning column k pick the unused row with the
+    // largest |a[r][k]| (ties: lowest row), publish column k and the pivot row index in LDS;
+    // after the barrier every other row subtracts f_r = a[r][k] / a[pv][k] times the pivot
+    // row (read from the owning lane of the same wave by v_readlane). Columns <= k of the
+    // P x P block are finished and left stale. At the end row pv_k, divided by its pivot,
+    // is the solution row k.
+    {
+      constexpr int NCG = 9;  // AW <= Ppad + npad + 1 <= 32 + 96 + 1 <= 16 * NCG
+      const int gr = tid & 31, cg = tid >> 5, half = cg & 1;
+      double av[NCG];
+#pragma unroll
+      for (int j = 0; j < NCG; ++j) {
+        const int c = cg + 16 * j;
+        av[j] = (c < AW && gr < Pp) ? aug[gr * AW + c] : 0.0;
       }
-      __syncthreads();
-      const int pv = s_piv;
-      if (pv != k)
-        for (int c = tid; c < AW; c += nth) {
-          const double t = aug[k * AW + c];
-          aug[k * AW + c] = aug[pv * AW + c];
-          aug[pv * AW + c] = t;
+      double* colb = sA;                          // 2 x 32 doubles (A is consumed)
+      int* pvb = reinterpret_cast<int*>(sA + 64);  // 2 ints
+      bool used = gr >= P;
+      int myk = -1;
+      double myp = 1.0;
+      __syncthreads();  // sA free
+      for (int k = 0; k < P; ++k) {
+        const int buf = k & 1;
+        if (cg == (k & 15)) {
+          const int jk = k >> 4;
+          double colv = av[0];
+#pragma unroll
+          for (int j = 1; j < NCG; ++j) colv = (j == jk) ? av[j] : colv;
+          // arg max over the 32 lanes on the VALU: DPP inside each 16-lane row, then the
+          // row pair by v_permlane16_swap ((max, lowest row) is commutative and associative)
+          double best = used ? -1.0 : fabs(colv);
+          int bi = gr;
+          auto take = [&](double ob, int oi) {
+            const bool t = ob > best || (ob == best && oi < bi);
+            best = t ? ob : best;
+            bi = t ? oi : bi;
+          };
+          take(dpp_f64<0xB1>(best), __builtin_amdgcn_mov_dpp(bi, 0xB1, 0xF, 0xF, false));
+          take(dpp_f64<0x4E>(best), __builtin_amdgcn_mov_dpp(bi, 0x4E, 0xF, 0xF, false));
+          take(dpp_f64<0x141>(best), __builtin_amdgcn_mov_dpp(bi, 0x141, 0xF, 0xF, false));
+          take(dpp_f64<0x140>(best), __builtin_amdgcn_mov_dpp(bi, 0x140, 0xF, 0xF, false));
+          {
+            const auto bh = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(best),
+                                                             (unsigned)__double2hiint(best), false, false);
+            const auto bl = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(best),
+                                                             (unsigned)__double2loint(best), false, false);
+            const auto bx = __builtin_amdgcn_permlane16_swap((unsigned)bi, (unsigned)bi, false, false);
+            // [0]: the even row's value, [1]: the odd row's, in every lane of the pair
+            const double b0 = __hiloint2double((int)bh[0], (int)bl[0]), b1 = __hiloint2double((int)bh[1], (int)bl[1]);
+            best = b0;
+            bi = (int)bx[0];
+            take(b1, (int)bx[1]);
+          }
+          colb[buf * 32 + gr] = colv;
+          if (gr == 0) pvb[buf] = bi;
         }
-      __syncthreads();
-      const double ip = 1.0 / aug[k * AW + k];
-      for (int c = tid; c < AW; c += nth) {  // one column per thread, rows in a loop
-        if (c == k) continue;
-        const double pkc = aug[k * AW + c] * ip;
-        for (int r = 0; r < P; ++r)
-          if (r != k) aug[r * AW + c] -= aug[r * AW + k] * pkc;
+        __syncthreads();
+        const int pv = pvb[buf];
+        const double p = colb[buf * 32 + pv];
+        const double f = colb[buf * 32 + gr] / p;
+        const bool piv = gr == pv;
+        if (piv) {
+          used = true;
+          myk = k;
+          myp = p;
+        }
+        const bool upd = !piv && gr < P;
+        const int src0 = pv, src1 = pv + 32;
+#pragma unroll
+        for (int j = 0; j < NCG; ++j) {
+          const double r0 = read_lane_f64(av[j], src0), r1 = read_lane_f64(av[j], src1);
+          const double prow = half ? r1 : r0;
+          const int c = cg + 16 * j;
+          if (upd && (c > k)) av[j] = fma(-f, prow, av[j]);
+        }
       }
-      __syncthreads();
-      for (int c = tid; c < AW; c += nth) aug[k * AW + c] = (c == k) ? 1.0 : aug[k * AW + c] * ip;
-      for (int r = tid; r < P; r += nth)
-        if (r != k) aug[r * AW + k] = 0.0;
+      __syncthreads();  // every thread past its last read of aug
+      if (myk >= 0) {
+        const double ip = 1.0 / myp;
+#pragma unroll
+        for (int j = 0; j < NCG; ++j) {
+          const int c = cg + 16 * j;
+          if (c >= Pp && c < AW) aug[myk * AW + c] = av[j] * ip;
+        }
+      }
       __syncthreads();
     }
     EKF_TICK(6);
@@ -320,7 +503,9 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   if (tid == 0) outliers[seq] = (long long)s_out;
 }
 
-// RTS smoother (src/core/ekf.py:280-287), one workgroup per sequence.
+// RTS smoother with the smoothed covariances (src/core/ekf.py:292-296), one workgroup per
+// sequence walking back through the frames (k_ekf_gain + k_ekf_smooth_x when the
+// covariances are not wanted).
 __global__ __launch_bounds__(256) void k_ekf_smooth(EkfDims d, const double* __restrict__ xpred,
                                                     const double* __restrict__ xest, const double* __restrict__ Ppred,
                                                     const double* __restrict__ Pest, double* __restrict__ xs,
@@ -373,28 +558,6 @@ __global__ __launch_bounds__(256) void k_ekf_smooth(EkfDims d, const double* __r
     for (int r = tid; r < np_; r += nth)
       sv[r] = r < n ? xs[(base + i + 1) * n + r] - xpred[(base + i + 1) * n + r] : 0.0;
     __syncthreads();
-    if (!keep_P) {
-      // xs[i] = x_est[i] + P_est F^T (P_pred^-1 v): two matrix-vector products, no gain matrix
-      double* sy = tmp;  // np <= 96 < 512
-      for (int r = tid; r < np_; r += nth) {
-        double v = 0.0;
-        for (int c = 0; c < np_; ++c) v += sInv[r * LD + c] * sv[c];
-        sy[r] = v;
-      }
-      __syncthreads();
-      for (int r = tid; r < n; r += nth) {
-        double v = xest[(base + i) * n + r];
-        for (int c = 0; c < n; ++c) {
-          double z = sy[c];  // (F^T y)[c]
-          if (c >= P) z += sT * sy[c - P];
-          if (c >= 2 * P) z += h2 * sy[c - 2 * P];
-          v += Pe[r * n + c] * z;
-        }
-        xs[(base + i) * n + r] = v;
-      }
-      __syncthreads();
-      continue;
-    }
     wg_mgemm<false, false>(A, np_, T, np_, sInv, LD, np_, np_, np_, 1.0, 0.0);  // A = T Pp^-1
     for (int r = tid; r < n; r += nth) {
       double v = xest[(base + i) * n + r];
@@ -410,6 +573,117 @@ __global__ __launch_bounds__(256) void k_ekf_smooth(EkfDims d, const double* __r
     wg_mgemm<false, true>(Pn, np_, E, np_, A, np_, np_, np_, np_, 1.0, 1.0);  // Ps[i] = P_est + E A^T
     for (int e = tid; e < (int)nn0; e += nth) Ps[(base + i) * nn0 + e] = Pn[(size_t)(e / n) * np_ + e % n];
     __syncthreads();
+  }
+}
+
+// RTS gains without the smoothed covariances (the reference never outputs them): the gain
+// A_i = P_est[i] F^T P_pred[i+1]^-1 (src/core/ekf.py:294) does not depend on the smoothed
+// states, so every (sequence, frame) pair is an independent workgroup here, and only the
+// state recursion below is sequential. A_i overwrites P_pred[i+1] (read first, by this
+// workgroup only). Product order as the reference: (P_est F^T) P_pred^-1, with P_est F^T
+// formed on the fly as the MFMA A operand.
+__global__ __launch_bounds__(256) void k_ekf_gain(EkfDims d, const double* __restrict__ Pest, double* Ppred,
+                                                  int* __restrict__ bad) {
+  const int N1 = d.N - 1;
+  const int seq = blockIdx.x / N1, i = blockIdx.x - seq * N1;
+  const int tid = threadIdx.x, nth = blockDim.x, lane = tid & 63, wave = tid >> 6;
+  const int n = d.n, P = d.P, np_ = d.npad, LD = np_ + 1, nb = np_ >> 4;
+  const double sT = d.sT, h2 = 0.5 * sT * sT;
+  extern __shared__ double lds[];
+  double* sInv = lds;                      // np x LD
+  double* tmp = sInv + (size_t)np_ * LD;   // 512
+  const size_t nn0 = (size_t)n * n, base = (size_t)seq * d.N;
+  const double* Pe = Pest + (base + i) * nn0;
+  double* Pp1 = Ppred + (base + i + 1) * nn0;
+  for (int e = tid; e < np_ * LD; e += nth) {
+    const int r = e / LD, c = e - r * LD;
+    sInv[e] = (r < n && c < n) ? Pp1[r * n + c] : (r == c ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  wg_gj_inverse<false>(sInv, LD, nb, tmp, bad);
+  const int li = lane & 15, lk = lane >> 4;
+  for (int t = wave; t < nb * nb; t += nth >> 6) {
+    const int i0 = (t / nb) << 4, j0 = (t % nb) << 4;
+    const int r = i0 + li;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < np_; k0 += 4) {
+      const int k = k0 + lk;
+      double a = 0.0;  // (P_est F^T)[r][k]
+      if (r < n && k < n) {
+        a = Pe[r * n + k];
+        if (k < 2 * P) a += sT * Pe[r * n + k + P];
+        if (k < P) a += h2 * Pe[r * n + k + 2 * P];
+      }
+      acc = mfma64(a, sInv[k * LD + j0 + li], acc);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = i0 + lk + 4 * q, cc = j0 + li;
+      if (rr < n && cc < n) Pp1[rr * n + cc] = acc[q];
+    }
+  }
+}
+
+// Smoothed states x_s[i] = x_est[i] + A_i (x_s[i+1] - x_pred[i+1]) (src/core/ekf.py:295), one
+// workgroup per sequence: a row per aligned group of 8 lanes (3 passes cover n <= 96), the
+// gain of the next frame loaded while this frame's products are summed.
+#define EKF_SX_NQ 12
+__global__ __launch_bounds__(256) void k_ekf_smooth_x(EkfDims d, const double* __restrict__ xpred,
+                                                      const double* __restrict__ xest, const double* __restrict__ Ag,
+                                                      double* __restrict__ xs) {
+  const int seq = blockIdx.x, tid = threadIdx.x;
+  const int n = d.n;
+  const size_t nn0 = (size_t)n * n, base = (size_t)seq * d.N;
+  __shared__ double sv[2][96];
+  const int j = tid & 7, g = tid >> 3;  // 32 groups of 8 lanes
+  for (int r = tid; r < n; r += blockDim.x) {
+    const double v = xest[(base + d.N - 1) * n + r];
+    xs[(base + d.N - 1) * n + r] = v;
+    sv[(d.N - 1) & 1][r] = v - xpred[(base + d.N - 1) * n + r];
+  }
+  double a[3][EKF_SX_NQ], xe[3], xp[3];
+  auto load = [&](int i) {  // A_i = the gain stored in P_pred[i+1]'s slot; x_est[i], x_pred[i]
+    const double* A = Ag + (base + i + 1) * nn0;
+#pragma unroll
+    for (int ps = 0; ps < 3; ++ps) {
+      const int r = ps * 32 + g;
+#pragma unroll
+      for (int q = 0; q < EKF_SX_NQ; ++q) {
+        const int c = j + 8 * q;
+        a[ps][q] = (r < n && c < n) ? A[r * n + c] : 0.0;
+      }
+      xe[ps] = (j == 0 && r < n) ? xest[(base + i) * n + r] : 0.0;
+      xp[ps] = (j == 0 && r < n) ? xpred[(base + i) * n + r] : 0.0;
+    }
+  };
+  if (d.N >= 2) load(d.N - 2);
+  for (int i = d.N - 2; i >= 0; --i) {
+    __syncthreads();
+    const double* v = sv[(i + 1) & 1];
+    double acc[3], xe_i[3], xp_i[3];
+#pragma unroll
+    for (int ps = 0; ps < 3; ++ps) {
+      xe_i[ps] = xe[ps];
+      xp_i[ps] = xp[ps];
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < EKF_SX_NQ; ++q) {
+        const int c = j + 8 * q;
+        if (c < n) s = fma(a[ps][q], v[c], s);
+      }
+      acc[ps] = s;
+    }
+    if (i > 0) load(i - 1);
+#pragma unroll
+    for (int ps = 0; ps < 3; ++ps) {
+      const double s = group_sum<8>(acc[ps]);
+      const int r = ps * 32 + g;
+      if (j == 0 && r < n) {
+        const double x = xe_i[ps] + s;
+        xs[(base + i) * n + r] = x;
+        sv[i & 1][r] = x - xp_i[ps];
+      }
+    }
   }
 }
 
@@ -440,6 +714,7 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
   d.C = n_cams;
   d.L = L;
   d.P = P;
+  d.J = Jn;
   d.n = 3 * P;
   d.npad = ((d.n + 15) / 16) * 16;
   d.Ppad = ((P + 15) / 16) * 16;
@@ -483,9 +758,9 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
   long long* dout = (long long*)(scr + std::max(scr_f, scr_s));
   int* dbad = (int*)(dout + n_seq);
   ACS_HIP(ctx, hipMemsetAsync(dbad, 0, sizeof(int), s));
-  const size_t U = std::max((size_t)EKF_WAVES * sizeof(FkShared) / sizeof(double),
+  const size_t U = std::max(ekf_fk_lds(P, Jn, L),
                             (size_t)d.npad * d.Ppad + (size_t)d.Ppad * (d.Ppad + d.npad + 1) + (size_t)d.Ppad * d.Ppad);
-  const size_t lds_f = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + U + d.npad + EKF_WAVES * FK_MAXP +
+  const size_t lds_f = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + U + d.npad +
                                           n_reals + (n_ints + 1) / 2 + 1);
   ACS_CHECK(ctx, lds_f <= 160 * 1024, "ekf: P = %d needs %zu bytes of LDS", P, lds_f);
   if (ref_numerics)
@@ -498,8 +773,20 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
                        (const double*)dP0, (const double*)dS0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof);
   ACS_HIP(ctx, hipGetLastError());
   const size_t lds_s = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + 512 + d.npad);
-  hipLaunchKernelGGL(k_ekf_smooth, dim3(n_seq), dim3(256), lds_s, s, d, dxp, dxe, dPp, dPe, dxs, dPs, scr, dbad,
-                     dPs ? 1 : 0);
+  if (dPs) {
+    hipLaunchKernelGGL(k_ekf_smooth, dim3(n_seq), dim3(256), lds_s, s, d, dxp, dxe, dPp, dPe, dxs, dPs, scr, dbad, 1);
+  } else {
+    // gains in parallel over (sequence, frame), then the state recursion per sequence
+    ACS_CHECK(ctx, d.npad <= 96, "ekf: n = %d", d.n);
+    if (n_frames >= 2) {
+      const size_t lds_g = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + 512);
+      hipLaunchKernelGGL(k_ekf_gain, dim3((unsigned)((size_t)n_seq * (n_frames - 1))), dim3(256), lds_g, s, d,
+                         (const double*)dPe, dPp, dbad);
+      ACS_HIP(ctx, hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_ekf_smooth_x, dim3(n_seq), dim3(256), 0, s, d, (const double*)dxp, (const double*)dxe,
+                       (const double*)dPp, dxs);
+  }
   ACS_HIP(ctx, hipGetLastError());
   if (x_pred && (rc = acs_stage_out(ctx, x_pred, dxp, sizeof(double) * NF * n, flags))) return rc;
   if ((rc = acs_stage_out(ctx, x_est, dxe, sizeof(double) * NF * n, flags))) return rc;
