@@ -261,7 +261,8 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
         rho += ls.f;
         if (ok) {
           const double cw = wt * wt * loss_curv(e, ls), gw = wt * ls.d1;
-          const double j0 = po.J[3 * side], j1 = po.J[3 * side + 1], j2 = po.J[3 * side + 2];
+          // selects, not po.J[3 * side]: a dynamic index would put the whole ProjOut in scratch
+          const double j0 = side ? po.J[3] : po.J[0], j1 = side ? po.J[4] : po.J[1], j2 = side ? po.J[5] : po.J[2];
           z[0] += cw * j0 * j0;
           z[1] += cw * j0 * j1;
           z[2] += cw * j0 * j2;

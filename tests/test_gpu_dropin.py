@@ -140,3 +140,31 @@ def test_core_fte_end_to_end_matches_oracle(mode, sd_mode, tmp_path):
                                atol=1e-6)
     rms = metric.reprojection_rms(st['reprj_errors'])
     assert rms < 10.0  # includes the 1 % +-30 px outliers and dropouts, as the reference metric does
+
+
+@pytest.mark.gpu
+def test_all_optimizations_cli_end_to_end(tmp_path):
+    """The drop-in pipeline script (src/all_optimizations.py): scene file + DLC exports in a
+    data directory -> automatic frame range -> GPU FTE -> fte.pickle."""
+    import pandas as pd
+    from acinoset_amd import all_optimizations as ao
+    scene = synth.load_scene_file()
+    N = 30
+    seq = synth.make_sequence(N, scene, mode='head', seed=21)
+    os.makedirs(tmp_path / 'extrinsic_calib')
+    scene.to_json(str(tmp_path / 'extrinsic_calib' / '6_cam_scene_sba.json'))
+    os.makedirs(tmp_path / 'dlc')
+    lik = seq.likelihood.copy()
+    lik[:2, :, 0] = 0.0      # nose unseen in frames 0-1 -> the range starts at frame 2
+    for c in range(scene.n_cams):
+        cols = pd.MultiIndex.from_product([['DLC_resnet50'], seq.markers, ['x', 'y', 'likelihood']],
+                                          names=['scorer', 'bodyparts', 'coords'])
+        v = np.stack([seq.uv[:, c, :, 0], seq.uv[:, c, :, 1], lik[:, c, :]], -1).reshape(N, -1)
+        pd.DataFrame(v, index=np.arange(N), columns=cols).to_csv(tmp_path / 'dlc' / f'cam{c + 1}DLC.csv')
+    out = ao.main(['--data_dir', str(tmp_path), '--dlc_thresh', '0.5', '--fps', '90'])
+    with open(out, 'rb') as f:
+        st = pickle.load(f)
+    assert st['start_frame'] == 2
+    assert np.asarray(st['x']).shape == (N - 1 - 2 + 1, 6)
+    assert os.path.exists(tmp_path / 'fte' / 'reconstruction_params.json')
+    assert metric.reprojection_rms(st['reprj_errors']) < 10.0

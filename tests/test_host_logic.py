@@ -162,3 +162,38 @@ def test_load_dlc_points_as_df_matches_reference_reshape(tmp_path, shifts):
     for col in ('x', 'y', 'likelihood'):
         np.testing.assert_allclose(got[col].to_numpy(float), exp[col].to_numpy(float), rtol=0, atol=1e-9,
                                    equal_nan=True)
+
+
+def _reference_frame_range(filtered, target_markers):
+    """`src/all_optimizations.py:79-111` as written: one query per frame."""
+    def frame_condition(i):
+        cond = ' or '.join([f'marker=="{ref}"' for ref in target_markers])
+        return len(filtered.query(f'frame == {i} and ({cond})')['marker'].unique()) >= len(target_markers)
+    start, end = None, None
+    max_idx = int(filtered['frame'].max() + 1)
+    for i in range(max_idx):
+        if frame_condition(i):
+            start = i
+            break
+    for i in range(max_idx, 0, -1):
+        if frame_condition(i):
+            end = i
+            break
+    return start, end
+
+
+@pytest.mark.parametrize('seed', [0, 1, 2])
+def test_all_optimizations_frame_range_matches_reference(seed):
+    from acinoset_amd import all_optimizations as ao
+    rng = np.random.default_rng(seed)
+    seq = synth.make_sequence(30, synth.load_scene_file(), mode='head', seed=seed)
+    df = seq.to_df(start_frame=3)
+    lik = df['likelihood'].to_numpy().copy()
+    # whole frames without some marker at the start and the end, random dropouts elsewhere
+    f = df['frame'].to_numpy()
+    lik[(f < 3 + 2 + seed) & (df['marker'].to_numpy() == 'nose')] = 0.0
+    lik[(f > 3 + 25 - seed) & (df['marker'].to_numpy() == 'r_eye')] = 0.0
+    lik[rng.random(len(lik)) < 0.5] = 0.0
+    df['likelihood'] = lik
+    filt = df.query('likelihood > 0.8')
+    assert ao.auto_frame_range(filt, get_markers('head')) == _reference_frame_range(filt, get_markers('head'))
