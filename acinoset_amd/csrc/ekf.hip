@@ -233,13 +233,12 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   __syncthreads();  // skel_view reads the header right away
   const SkelView sk = skel_view(sI, sRl);
   const double sT = d.sT, h2 = 0.5 * sT * sT;
-  // per-sequence scratch: hpose (P+1) x m; H, W H, G = H P_xx (mpad x Pp); res, w (mpad)
+  // per-sequence scratch: hpose (P+1) x m; H, W H (mpad x Pp); res, w (mpad)
   const int mp = d.mpad;
-  double* hpose = scratch + (size_t)seq * ((size_t)(P + 1) * m + 3 * (size_t)mp * Pp + 2 * mp);
+  double* hpose = scratch + (size_t)seq * ((size_t)(P + 1) * m + 2 * (size_t)mp * Pp + 2 * mp);
   double* H = hpose + (size_t)(P + 1) * m;
   double* HW = H + (size_t)mp * Pp;
-  double* G = HW + (size_t)mp * Pp;
-  double* res = G + (size_t)mp * Pp;
+  double* res = HW + (size_t)mp * Pp;
   double* wr = res + mp;
   const size_t fstride = (size_t)d.C * d.L;  // measurements per frame
   for (int e = tid; e < d.npad * LDP; e += nth) {
@@ -321,62 +320,166 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       __syncthreads();
     }
     EKF_TICK(2);
-    // H, W H, residual, R^-1 (row r = 2 (c L + l) + d, the reference's ordering; rows
-    // past m are zero padding for the MFMA products)
+    // residual and R^-1 per row (row r = 2 (c L + l) + d, the reference's ordering; rows
+    // past m are zero padding for the MFMA products), then H and W H element-parallel
+    // (coalesced stores)
     for (int r = tid; r < mp; r += nth) {
+      double e = 0.0, w = 0.0;
       if (r < m) {
-        const double h0 = hpose[r];
         const int o = r >> 1, c = o / d.L;
-        const double z = meas[fo * fstride * 2 + r];
-        double e = z - h0;
+        e = meas[fo * fstride * 2 + r] - hpose[r];
         if (!isfinite(e)) e = (e != e) ? 0.0 : (e > 0 ? 1.7976931348623157e308 : -1.7976931348623157e308);
-        res[r] = e;
         const double lk = lik[fo * fstride + o];
         const double sd = (lk < d.thresh) ? d.maxpix : rbase[c];
-        const double w = 1.0 / (sd * sd);
-        wr[r] = w;
-        for (int q = 0; q < Pp; ++q) {
-          const double hq = q < P ? (hpose[(size_t)(q + 1) * m + r] - h0) / d.eps : 0.0;
-          H[(size_t)r * Pp + q] = hq;
-          HW[(size_t)r * Pp + q] = w * hq;
-        }
-      } else {
-        res[r] = 0.0;
-        wr[r] = 0.0;
-        for (int q = 0; q < Pp; ++q) H[(size_t)r * Pp + q] = HW[(size_t)r * Pp + q] = 0.0;
+        w = 1.0 / (sd * sd);
       }
+      res[r] = e;
+      wr[r] = w;
+    }
+    __syncthreads();
+    for (int e = tid; e < mp * Pp; e += nth) {
+      const int r = e / Pp, q = e - r * Pp;
+      double hq = 0.0;
+      if (r < m && q < P) hq = (hpose[(size_t)(q + 1) * m + r] - hpose[r]) / d.eps;
+      H[e] = hq;
+      HW[e] = wr[r] * hq;
     }
     __syncthreads();
     EKF_TICK(3);
     // ---- 3. information-form update -------------------------------------------------
-    wg_mgemm<true, false>(sA, Pp, HW, Pp, H, Pp, Pp, Pp, mp, 1.0, 0.0);        // A = H^T R^-1 H
-    wg_mgemm<false, false>(G, Pp, H, Pp, sP, LDP, mp, Pp, Pp, 1.0, 0.0);       // G = H P[0:Pp, 0:Pp]
-    for (int e = tid; e < d.npad * Pp; e += nth) {  // P[:, x]
-      const int r = e / Pp, c = e % Pp;
-      sPx[e] = (r < n && c < P) ? sP[r * LDP + c] : 0.0;
-    }
-    for (int a = wave; a < Pp; a += EKF_WAVES) {  // b = H^T R^-1 r (fixed-order wave sums)
-      double v = 0.0;
-      if (a < P)
-        for (int r = lane; r < mp; r += 64) v += HW[(size_t)r * Pp + a] * res[r];
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-      if (lane == 0) aug[a * AW + Pp + d.npad] = v;
-    }
-    // 3-sigma outlier count (:259-264): diag S = rows of H_x P_xx . H_x, + R
-    unsigned long long cnt = 0;
-    for (int pt = tid; pt < m / 2; pt += nth) {
-      bool outl = false;
-      for (int dd = 0; dd < 2; ++dd) {
-        const int r = 2 * pt + dd;
-        double q = 0.0;
-        for (int b = 0; b < P; ++b) q += G[(size_t)r * Pp + b] * H[(size_t)r * Pp + b];
-        const double Srr = q + 1.0 / wr[r];
-        if (fabs(res[r]) > 3.0 * sqrt(Srr)) outl = true;
+    {
+      // A = H^T R^-1 H (upper tiles) and b = H^T R^-1 r (a 16-column tile whose column 0 is
+      // r) on MFMA, the k-steps (4 rows of H each) dealt round-robin to KS waves, 4 k-steps
+      // of operands loaded before their MFMAs; the KS partial tiles are summed in a fixed
+      // tree through LDS (sPx / aug are free until the products below)
+      const int li = lane & 15, lk = lane >> 4;
+      const int NTt = Pp >> 4, nAt = NTt * (NTt + 1) / 2, nt = nAt + NTt, nks = mp >> 2;
+      const size_t avail = (size_t)d.npad * Pp + (size_t)Pp * AW;
+      int KS = EKF_WAVES;
+      while (KS > 1 && (size_t)(KS / 2) * nt * 256 > avail) KS >>= 1;
+      double* red = sPx;
+      constexpr int NTMAX = 5;  // 3 upper A tiles + 2 b tiles at Ppad = 32
+      dbl4 acc[NTMAX];
+#pragma unroll
+      for (int t = 0; t < NTMAX; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+      auto tile_ij = [&](int t, int& i0, int& j0) {  // t < nAt: upper A tiles; then b tiles
+        if (t < nAt) {
+          i0 = (NTt == 2 && t == 2) ? 16 : 0;
+          j0 = (NTt == 2 && t >= 1) ? 16 : 0;
+        } else {
+          i0 = (t - nAt) * 16;
+          j0 = -1;
+        }
+      };
+      if (wave < KS) {
+        constexpr int UB = 2;  // k-steps per batch of loads
+        for (int s0 = wave; s0 < nks; s0 += UB * KS) {
+          double av[UB][2], bv[UB][2], rv[UB];
+#pragma unroll
+          for (int u = 0; u < UB; ++u) {
+            const int k = 4 * (s0 + u * KS) + lk;
+            const bool ok = s0 + u * KS < nks;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              av[u][h] = (ok && h < NTt) ? HW[(size_t)k * Pp + 16 * h + li] : 0.0;
+              bv[u][h] = (ok && h < NTt) ? H[(size_t)k * Pp + 16 * h + li] : 0.0;
+            }
+            rv[u] = (ok && li == 0) ? res[k] : 0.0;
+          }
+#pragma unroll
+          for (int u = 0; u < UB; ++u)
+#pragma unroll
+            for (int t = 0; t < NTMAX; ++t) {
+              if (t >= nt) break;
+              int i0, j0;
+              tile_ij(t, i0, j0);
+              const double aop = i0 ? av[u][1] : av[u][0];  // selects: no dynamic register index
+              const double bop = j0 < 0 ? rv[u] : (j0 ? bv[u][1] : bv[u][0]);
+              acc[t] = mfma64(aop, bop, acc[t]);
+            }
+        }
       }
-      cnt += outl;
+      // fixed-order tree over the KS partials
+      for (int h = KS >> 1; h >= 1; h >>= 1) {
+        if (wave >= h && wave < 2 * h)
+#pragma unroll
+          for (int t = 0; t < NTMAX; ++t)
+            if (t < nt)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) red[((size_t)(wave - h) * nt + t) * 256 + q * 64 + lane] = acc[t][q];
+        __syncthreads();
+        if (wave < h)
+#pragma unroll
+          for (int t = 0; t < NTMAX; ++t)
+            if (t < nt)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) acc[t][q] += red[((size_t)wave * nt + t) * 256 + q * 64 + lane];
+        __syncthreads();
+      }
+      if (wave == 0) {
+#pragma unroll
+        for (int t = 0; t < NTMAX; ++t) {
+          if (t >= nt) break;
+          int i0, j0;
+          tile_ij(t, i0, j0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = i0 + lk + 4 * q;
+            if (j0 >= 0) {
+              sA[row * Pp + j0 + li] = acc[t][q];
+              sA[(j0 + li) * Pp + row] = acc[t][q];  // lower triangle (symmetric)
+            } else if (li == 0) {
+              aug[row * AW + Pp + d.npad] = row < P ? acc[t][q] : 0.0;
+            }
+          }
+        }
+      }
+      // 3-sigma outlier count (:259-264): diag S = rows of H_x P_xx . H_x, + R. Row tiles of
+      // H P_xx on MFMA (operands loaded first), each row's dot with its own H row summed
+      // across the 16 column lanes (DPP) and the column tiles
+      unsigned long long cnt = 0;
+      for (int rt = wave; rt < (mp >> 4); rt += EKF_WAVES) {
+        const int i0 = rt << 4;
+        double ha[8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) ha[s] = (4 * s < Pp) ? H[(size_t)(i0 + li) * Pp + 4 * s + lk] : 0.0;
+        double hr[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) hr[h][q] = h < NTt ? H[(size_t)(i0 + lk + 4 * q) * Pp + 16 * h + li] : 0.0;
+        double dq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (h >= NTt) break;
+          dbl4 g = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int s = 0; s < 8; ++s)
+            if (4 * s < Pp) g = mfma64(ha[s], sP[(4 * s + lk) * LDP + 16 * h + li], g);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dq[q] += g[q] * hr[h][q];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          dq[q] = group_sum<16>(dq[q]);
+          const int r = i0 + lk + 4 * q;
+          bool outl = false;
+          if (li == 0 && r < m) {
+            const double Srr = dq[q] + 1.0 / wr[r];
+            outl = fabs(res[r]) > 3.0 * sqrt(Srr);
+          }
+          // rows 2 pt (lk even) and 2 pt + 1 (lane + 16)
+          const int other = __shfl_xor((int)outl, 16);
+          if (li == 0 && !(lk & 1) && r < m && (outl || other)) ++cnt;
+        }
+      }
+      if (cnt) atomicAdd(&s_out, cnt);
+      for (int e = tid; e < d.npad * Pp; e += nth) {  // P[:, x] (after the tree used sPx)
+        const int r = e / Pp, c = e % Pp;
+        sPx[e] = (r < n && c < P) ? sP[r * LDP + c] : 0.0;
+      }
+      __syncthreads();
     }
-    if (cnt) atomicAdd(&s_out, cnt);
-    __syncthreads();
     EKF_TICK(4);
     // aug = [I + A P_xx | A P[x, :] | b]: G2 = A P[0:Pp, :] on MFMA (A is zero outside
     // P x P), then the M block gets the identity and its padding columns are cleared
@@ -751,7 +854,7 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
   double* dPs = P_smooth ? ((flags & ACS_DEVICE_PTRS) ? P_smooth
                                                       : (double*)acs_ws(ctx, WS_FTE15, sizeof(double) * NF * n * n))
                          : nullptr;
-  const size_t scr_f = (size_t)n_seq * ((size_t)(P + 1) * d.m + 3 * (size_t)d.mpad * d.Ppad + 2 * d.mpad);
+  const size_t scr_f = (size_t)n_seq * ((size_t)(P + 1) * d.m + 2 * (size_t)d.mpad * d.Ppad + 2 * d.mpad);
   const size_t scr_s = (size_t)n_seq * 5 * d.npad * d.npad;
   double* scr = (double*)acs_ws(ctx, WS_FTE6, sizeof(double) * std::max(scr_f, scr_s) + 64 * (size_t)n_seq * 8);
   if (!dxp || !dxe || !dxs || !dPe || !dPp || !scr || (P_smooth && !dPs)) return ACS_E_NOMEM;
