@@ -795,9 +795,11 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     double* G = GBc + (size_t)j * BP * GR;
     for (int e = tid; e < BP * LDD; e += blockDim.x) {
       const int r = e / LDD, c = e - r * LDD;
+      // D parts of the pending terms hold their upper tiles only (symmetric)
+      const int es = (c < BP && (r >> 4) > (c >> 4)) ? c * LDD + r : e;
       double v = 0.0;
-      if (pr) v += pr[e];
-      if (pl) v += pl[e];
+      if (pr) v += pr[es];
+      if (pl) v += pl[es];
       if (c < BP)
         D[r * BP + c] -= v;
       else
@@ -826,6 +828,18 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   if (!dwave) {
     const int jj = part + nsplit * (wave - NB);
     if (jj < NBB) J = jj;
+    if (nsplit == 1 && NB == 5 && NBB == 11) {
+      // one workgroup holds all 11 column-blocks: deal them so that the four SIMDs (wave
+      // w runs on SIMD w % 4) carry about the same MFMA work (GJ 5 + Schur tiles, in units
+      // of 4-MFMA chains: J0-4: 6..10 + 5, J5-9: 1..5 + 5, J10: 11 + 5)
+      constexpr int perm[11] = {4, 3, 2, 10, 8, 1, 0, 9, 6, 5, 7};
+      J = perm[wave - NB];
+    } else if (nsplit == 2 && NB == 5 && NBB == 11) {
+      // two workgroups per block (even / odd column-blocks), the same balancing
+      constexpr int perm2[2][11] = {{4, 2, 0, 10, -1, 8, 6, -1, -1, -1, -1},
+                                    {1, 9, 7, 3, -1, 5, -1, -1, -1, -1, -1}};
+      J = perm2[part][wave - NB];
+    }
   }
   PROF_T0
   {
@@ -855,12 +869,15 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
       for (int q = 0; q < 4; ++q) t[K][q] = src[(r0 + lk + 4 * q) * ld + K * 16 + li];
   };
+  // pending D terms are stored as upper tiles: tile (r0/16, K) with K < r0/16 is the
+  // transpose of tile (K, r0/16)
   auto sub_rows = [&](const double* src, int ld, int r0) {
     double v[NB][4];
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[K][q] = src[(r0 + lk + 4 * q) * ld + K * 16 + li];
+      for (int q = 0; q < 4; ++q)
+        v[K][q] = (K * 16 < r0) ? src[(K * 16 + li) * ld + r0 + lk + 4 * q] : src[(r0 + lk + 4 * q) * ld + K * 16 + li];
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
@@ -1093,9 +1110,9 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     for (int q = 0; q < 4; ++q) W[(size_t)(K * 16 + lk + 4 * q) * WL + wcol + li] = t[K][q];
   const int ocol = J < NB ? J * 16 : (J < 2 * NB ? (J - NB) * 16 : BP + (J - 2 * NB) * 16);
   // out tile I = sum_K A(I, K) W(K): two independent MFMA chains (even / odd K)
-  auto term = [&](auto aop, auto store) {
+  auto term = [&](auto aop, auto store, int Imax) {  // output tiles I = 0 .. Imax
 #pragma unroll 1
-    for (int I = 0; I < NB; ++I) {
+    for (int I = 0; I <= Imax; ++I) {
       dbl4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int K = 0; K < NB; K += 2) {
@@ -1124,8 +1141,8 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
     for (int q = 0; q < 4; ++q) Er_out[(size_t)(I * 16 + lk + 4 * q) * BP + J * 16 + li] = -acc[q];
   };
-  // left term E_i^T W (columns W_l and W_gb)
-  if (J < NB || J >= 2 * NB) term(aEiT, put_L);
+  // left term E_i^T W (columns W_l and W_gb); E_i^T W_l is symmetric: upper tiles only
+  if (J < NB || J >= 2 * NB) term(aEiT, put_L, J < NB ? J : NB - 1);
   PROFA(41, NB);
   PROFW(3, NB);
   PROFW(3 + 8, 15);
@@ -1133,14 +1150,16 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   if (Er) {
     if (J < NB) {
       if (sEr)
-        term(aEr_lds, put_E);
+        term(aEr_lds, put_E, NB - 1);
       else
-        term(aEr_glb, put_E);
+        term(aEr_glb, put_E, NB - 1);
     } else {
+      // E_r W_r is symmetric: upper tiles only
+      const int Imax = J < 2 * NB ? J - NB : NB - 1;
       if (sEr)
-        term(aEr_lds, put_R);
+        term(aEr_lds, put_R, Imax);
       else
-        term(aEr_glb, put_R);
+        term(aEr_glb, put_R, Imax);
     }
   }
   PROFA(42, NB);
