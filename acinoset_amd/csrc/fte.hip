@@ -771,7 +771,7 @@ static void cr_launch_build(const FteDims& d, hipStream_t s, int nblk, const Fte
 // loaded at the next level (or by an apply workgroup), so a level is one launch.
 template <int NB>
 __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int iend, int top, int ne, int astep,
-                                                   int nsplit, const FteState* __restrict__ st,
+                                                   int nsplit, int sym_in, const FteState* __restrict__ st,
                                                    double* __restrict__ Dc, const double* __restrict__ Ein,
                                                    double* __restrict__ Eout, double* __restrict__ GBc,
                                                    double* __restrict__ Wc, double* __restrict__ Tau,
@@ -796,7 +796,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     for (int e = tid; e < BP * LDD; e += blockDim.x) {
       const int r = e / LDD, c = e - r * LDD;
       // D parts of the pending terms hold their upper tiles only (symmetric)
-      const int es = (c < BP && (r >> 4) > (c >> 4)) ? c * LDD + r : e;
+      const int es = (sym_in && c < BP && (r >> 4) > (c >> 4)) ? c * LDD + r : e;
       double v = 0.0;
       if (pr) v += pr[es];
       if (pl) v += pl[es];
@@ -869,15 +869,17 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
       for (int q = 0; q < 4; ++q) t[K][q] = src[(r0 + lk + 4 * q) * ld + K * 16 + li];
   };
-  // pending D terms are stored as upper tiles: tile (r0/16, K) with K < r0/16 is the
-  // transpose of tile (K, r0/16)
+  // pending D terms of a level that took the one-wave-per-column-block path (sym_in) are
+  // stored as upper tiles: tile (r0/16, K) with K < r0/16 is the transpose of tile (K, r0/16);
+  // the deep path writes full tiles (rows read contiguously)
   auto sub_rows = [&](const double* src, int ld, int r0) {
     double v[NB][4];
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        v[K][q] = (K * 16 < r0) ? src[(K * 16 + li) * ld + r0 + lk + 4 * q] : src[(r0 + lk + 4 * q) * ld + K * 16 + li];
+        v[K][q] = (sym_in && K * 16 < r0) ? src[(K * 16 + li) * ld + r0 + lk + 4 * q]
+                                          : src[(r0 + lk + 4 * q) * ld + K * 16 + li];
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
@@ -1728,9 +1730,13 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
 }
 
 // one k_cr_level launch (template on the tile count NB = BP/16)
-static void cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int iend, int top, int ne, int ns,
-                            int astep, const FteState* st, FteBuffers& b, const double* Ein, double* Eout, int* bad) {
-  if (ne + ns == 0) return;
+// Returns whether this level's pending Schur terms are stored as upper tiles (the
+// one-wave-per-column-block path; the deep path of k_cr_level writes full tiles). `sym_in`:
+// the same for the level whose terms this launch applies.
+static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int iend, int top, int ne, int ns,
+                           int astep, const FteState* st, FteBuffers& b, const double* Ein, double* Eout, int* bad,
+                           int sym_in) {
+  if (ne + ns == 0) return 0;
   const int NB = d.BP >> 4, NBB = 2 * NB + d.GR / 16;
   // workgroups per eliminated block: enough column waves (16 - NB per workgroup), and more
   // of them when few blocks are left (the deep levels are latency-bound)
@@ -1743,8 +1749,8 @@ static void cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int
   const size_t lds = sizeof(double) * (2 * (16 * 17 + 16 * (size_t)d.BP + 17 * (size_t)d.BP) + (size_t)d.BP * d.GR +
                                        (NB <= 5 ? 2 * (size_t)d.BP + 1 : (size_t)d.BP) * d.BP);
 #define CR_LEVEL(nb)                                                                                               \
-  hipLaunchKernelGGL((k_cr_level<nb>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, top, ne, astep, nsplit, st, \
-                     b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
+  hipLaunchKernelGGL((k_cr_level<nb>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, top, ne, astep, nsplit, \
+                     sym_in, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
   switch (NB) {
     case 1: CR_LEVEL(1); break;
     case 2: CR_LEVEL(2); break;
@@ -1754,6 +1760,10 @@ static void cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int
     default: CR_LEVEL(6); break;
   }
 #undef CR_LEVEL
+  // the kernel's deep-path test (full tiles)
+  const int BPq = d.BP, BUF = 16 * 17 + 16 * BPq + BPq * 17;
+  const bool deep = nsplit >= 3 && ((NBB + nsplit - 1) / nsplit) * BPq * 16 <= 2 * BUF;
+  return (ne > 0 && !deep) ? 1 : 0;
 }
 
 // Block cyclic reduction of super-blocks [a0, top] (blocks < iend may be eliminated; a
@@ -1763,13 +1773,13 @@ static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* 
                                int top, int nlev, int* bad) {
   const double* Ein = b.Ec;
   double* Eout = b.Ec2;
-  int sl = 1;
+  int sl = 1, sym = 0;
   for (int lv = 0; lv < nlev; ++lv, sl <<= 1) {
     int ne = 0, ns = 0;
     for (int i = a0 + sl; i < iend; i += 2 * sl) ++ne;
     if (sl > 1)
       for (int j = a0; j <= top; j += 2 * sl) ++ns;
-    cr_launch_level(d, s, sl, a0, iend, top, ne, ns, 2 * sl, st, b, Ein, Eout, bad);
+    sym = cr_launch_level(d, s, sl, a0, iend, top, ne, ns, 2 * sl, st, b, Ein, Eout, bad, sym);
     double* t = const_cast<double*>(Ein);
     Ein = Eout;
     Eout = t;
@@ -1777,7 +1787,7 @@ static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* 
   if (nlev > 0) {
     int ns = 0;
     for (int j = a0; j <= top; j += sl) ++ns;
-    cr_launch_level(d, s, sl, a0, iend, top, 0, ns, sl, st, b, Ein, Eout, bad);
+    cr_launch_level(d, s, sl, a0, iend, top, 0, ns, sl, st, b, Ein, Eout, bad, sym);
   }
   return Ein;
 }
