@@ -771,7 +771,8 @@ static void cr_launch_build(const FteDims& d, hipStream_t s, int nblk, const Fte
 // loaded at the next level (or by an apply workgroup), so a level is one launch.
 template <int NB>
 __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int iend, int top, int ne, int astep,
-                                                   int nsplit, int sym_in, const FteState* __restrict__ st,
+                                                   int nsplit, int sym_in, int top_mode,
+                                                   const FteState* __restrict__ st,
                                                    double* __restrict__ Dc, const double* __restrict__ Ein,
                                                    double* __restrict__ Eout, double* __restrict__ GBc,
                                                    double* __restrict__ Wc, double* __restrict__ Tau,
@@ -808,11 +809,13 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     return;
   }
   const int part = (int)blockIdx.x % nsplit;
-  const int i = a0 + s * (2 * ((int)blockIdx.x / nsplit) + 1);
-  const int r = (i + s <= top) ? i + s : -1;
-  const double* qR = hs ? dR + (size_t)(i - hs) * BP * LDD : nullptr;  // pending of level hs
+  // top_mode: the last surviving block a0 itself (no neighbours, only its GB column-blocks:
+  // W_gb = D^-1 GB and Tau = GB^T W_gb for k_cr_top), after its pending terms
+  const int i = top_mode ? a0 : a0 + s * (2 * ((int)blockIdx.x / nsplit) + 1);
+  const int r = (!top_mode && i + s <= top) ? i + s : -1;
+  const double* qR = (hs && !top_mode) ? dR + (size_t)(i - hs) * BP * LDD : nullptr;  // pending of level hs
   const double* qL = (hs && i + hs < iend) ? dL + (size_t)(i + hs) * BP * LDD : nullptr;
-  const double* Ei = Ein + (size_t)i * BP * BP;
+  const double* Ei = top_mode ? nullptr : Ein + (size_t)i * BP * BP;
   const double* Er = r >= 0 ? Ein + (size_t)r * BP * BP : nullptr;
   extern __shared__ double lds[];
   double* G0 = lds + 2 * BUF;  // GB_i (pending applied), BP x GR, for Tau
@@ -828,7 +831,9 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   if (!dwave) {
     const int jj = part + nsplit * (wave - NB);
     if (jj < NBB) J = jj;
-    if (nsplit == 1 && NB == 5 && NBB == 11) {
+    if (top_mode) {
+      J = (wave - NB < GRB) ? 2 * NB + (wave - NB) : -1;
+    } else if (nsplit == 1 && NB == 5 && NBB == 11) {
       // one workgroup holds all 11 column-blocks: deal them so that the four SIMDs (wave
       // w runs on SIMD w % 4) carry about the same MFMA work (GJ 5 + Schur tiles, in units
       // of 4-MFMA chains: J0-4: 6..10 + 5, J5-9: 1..5 + 5, J10: 11 + 5)
@@ -849,7 +854,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
     for (int q = 0; q < NCP; ++q) {
       const int e = tid + 1024 * q;
-      ve[q] = e < BP * BP ? Ei[e] : 0.0;
+      ve[q] = (Ei && e < BP * BP) ? Ei[e] : 0.0;
       vr[q] = (sEr && e < BP * BP) ? Er[e] : 0.0;
     }
 #pragma unroll
@@ -955,13 +960,14 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) Pk[(lk + 4 * q) * TS + li] = t[k][q];
-        // R_kK = D_kk^-1 D_kK; the A operand (row li, column 4ks + lk of the symmetric
-        // inverse) is register ks of the inverse itself: no LDS round trip
+        // R_kK = D_kk^-1 D_kK. The A operand is read back from Pk (row li, column 4ks + lk):
+        // the computed inverse is not exactly symmetric, and its transpose (register ks of
+        // the tile) costs accuracy on ill-conditioned blocks (the last, most reduced one)
 #pragma unroll
         for (int K = k + 1; K < NB; ++K) {
           dbl4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int ks = 0; ks < 4; ++ks) acc = mfma64(t[k][ks], t[K][ks], acc);
+          for (int ks = 0; ks < 4; ++ks) acc = mfma64(Pk[li * TS + 4 * ks + lk], t[K][ks], acc);
           t[K] = acc;
 #pragma unroll
           for (int q = 0; q < 4; ++q) Rk[(lk + 4 * q) * BP + K * 16 + li] = acc[q];
@@ -1144,7 +1150,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     for (int q = 0; q < 4; ++q) Er_out[(size_t)(I * 16 + lk + 4 * q) * BP + J * 16 + li] = -acc[q];
   };
   // left term E_i^T W (columns W_l and W_gb); E_i^T W_l is symmetric: upper tiles only
-  if (J < NB || J >= 2 * NB) term(aEiT, put_L, J < NB ? J : NB - 1);
+  if (!top_mode && (J < NB || J >= 2 * NB)) term(aEiT, put_L, J < NB ? J : NB - 1);
   PROFA(41, NB);
   PROFW(3, NB);
   PROFW(3 + 8, 15);
@@ -1229,17 +1235,16 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
   }
 }
 
-__global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ Dc,
-                                                const double* __restrict__ GBc, const double* __restrict__ part,
-                                                const double* __restrict__ gmaxp, const double* __restrict__ taubuf,
-                                                double* __restrict__ dcv, double* __restrict__ dtau,
-                                                int* __restrict__ bad) {
+__global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ W0,
+                                                const double* __restrict__ part, const double* __restrict__ gmaxp,
+                                                const double* __restrict__ taubuf, double* __restrict__ dcv,
+                                                double* __restrict__ dtau, int* __restrict__ bad) {
+  // block 0 has been eliminated by k_cr_level (top_mode): W0 = its W (BP x WL), its tau Schur
+  // term is in the Tau sums like every other block's
   if (st->status != 0) return;
   const int tid = threadIdx.x, nth = blockDim.x;
-  const int P = d.P, BP = d.BP, GR = d.GR, Cg = d.Cg;
+  const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
   const double lam = st->lam;
-  __shared__ double sD[CR_MAXBP * CR_MAXBP];
-  __shared__ double sW[CR_MAXBP * 32];
   __shared__ double sS[32 * 32];
   __shared__ double sr[32];
   __shared__ double tmp[512];
@@ -1272,18 +1277,12 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
     mx = block_max(mx, s_red);
     if (tid == 0) st->gmax = mx;
   }
-  for (int e = tid; e < BP * BP; e += nth) sD[e] = Dc[e];
-  __syncthreads();
-  wg_spd_inverse(sD, BP, BP >> 4, tmp, bad);
-  // W0 = D0^-1 GB0 (BP x GR)
-  wg_mgemm<false, false>(sW, GR, sD, BP, GBc, GR, BP, GR, BP, 1.0, 0.0);
   if (Cg) {
-    // S = D_tau - sum_i Tau_i - G0^T W0g ;  rhs = b_tau - sum_i Tau_i[:, Cg] - G0^T W0b   (GR x GR, padded)
-    wg_mgemm<true, false>(sS, GR, GBc, GR, sW, GR, GR, GR, BP, -1.0, 0.0);
+    // S = D_tau - sum_i Tau_i ;  rhs = b_tau - sum_i Tau_i[:, Cg]   (GR x GR, padded)
     for (int e = tid; e < GR * GR; e += nth) {
       const int r = e / GR, c = e % GR;
+      double h = 0.0;
       if (r < Cg && c <= Cg) {
-        double h;
         if (c < Cg) {
           h = s_sum[r * Cg + c];
           if (r == c) h += lam * fmax(h, 1e-12);
@@ -1291,8 +1290,8 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
           h = -s_sum[nH + r];
         }
         h -= s_sum[nH + Cg + r * GR + c];
-        sS[e] += h;
       }
+      sS[e] = h;
     }
     __syncthreads();
     if (tid < GR) sr[tid] = (tid < Cg && !s_held[tid]) ? sS[tid * GR + Cg] : 0.0;
@@ -1312,8 +1311,9 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
     __syncthreads();
   }
   for (int r = tid; r < BP; r += nth) {
-    double v = sW[r * GR + Cg];
-    for (int c = 0; c < Cg; ++c) v -= sW[r * GR + c] * dtau[c];
+    const double* w = W0 + (size_t)r * WL + 2 * BP;
+    double v = w[Cg];
+    for (int c = 0; c < Cg; ++c) v -= w[c] * dtau[c];
     dcv[r] = v;
   }
 }
@@ -1750,7 +1750,7 @@ static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int 
                                        (NB <= 5 ? 2 * (size_t)d.BP + 1 : (size_t)d.BP) * d.BP);
 #define CR_LEVEL(nb)                                                                                               \
   hipLaunchKernelGGL((k_cr_level<nb>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, top, ne, astep, nsplit, \
-                     sym_in, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
+                     sym_in, 0, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
   switch (NB) {
     case 1: CR_LEVEL(1); break;
     case 2: CR_LEVEL(2); break;
@@ -1770,7 +1770,7 @@ static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int 
 // chain end at iend survives), nlev levels, then the last level's pending Schur terms are
 // applied to the survivors. Returns the buffer holding the final couplings E.
 static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* st, FteBuffers& b, int a0, int iend,
-                               int top, int nlev, int* bad) {
+                               int top, int nlev, int* bad, bool final_apply = true, int* sym_out = nullptr) {
   const double* Ein = b.Ec;
   double* Eout = b.Ec2;
   int sl = 1, sym = 0;
@@ -1784,12 +1784,35 @@ static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* 
     Ein = Eout;
     Eout = t;
   }
-  if (nlev > 0) {
+  if (nlev > 0 && final_apply) {
     int ns = 0;
     for (int j = a0; j <= top; j += sl) ++ns;
     cr_launch_level(d, s, sl, a0, iend, top, 0, ns, sl, st, b, Ein, Eout, bad, sym);
   }
+  if (sym_out) *sym_out = sym;
   return Ein;
+}
+
+// The single surviving block a0 after nlev levels (step sl = 2^nlev): its pending terms,
+// then W_gb = D^-1 GB and Tau = GB^T W_gb on the register-tiled Gauss-Jordan of k_cr_level
+// (top_mode); k_cr_top finishes with the tau border.
+static void cr_launch_top(const FteDims& d, hipStream_t s, int nlev, int a0, int iend, const FteState* st,
+                          FteBuffers& b, int* bad, int sym_in) {
+  const int sl = 1 << nlev, NB = d.BP >> 4;
+  const size_t lds = sizeof(double) * (2 * (16 * 17 + 16 * (size_t)d.BP + 17 * (size_t)d.BP) + (size_t)d.BP * d.GR +
+                                       (NB <= 5 ? 2 * (size_t)d.BP + 1 : (size_t)d.BP) * d.BP);
+#define CR_TOP(nb)                                                                                                \
+  hipLaunchKernelGGL((k_cr_level<nb>), dim3(1), dim3(1024), lds, s, d, sl, a0, iend, a0, 1, sl, 1, sym_in, 1, st, \
+                     b.Dc, b.Ec, b.Ec2, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
+  switch (NB) {
+    case 1: CR_TOP(1); break;
+    case 2: CR_TOP(2); break;
+    case 3: CR_TOP(3); break;
+    case 4: CR_TOP(4); break;
+    case 5: CR_TOP(5); break;
+    default: CR_TOP(6); break;
+  }
+#undef CR_TOP
 }
 
 static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
@@ -1809,11 +1832,13 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   fte_enqueue_linearize(S, s, 0);
   cr_launch_build(d, s, d.nblk, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, 0, -1, -1, d.var ? b.Adiag : nullptr);
   const int bend = d.nblk - 1;
-  cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad);
+  int sym = 0;
+  cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad, false, &sym);
+  cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, sym);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
-                     d.N, 1, d.nblk);
-  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, d, b.st, b.Dc, b.GBc, b.part, b.gmaxp, b.tau, b.dcv, b.dtau,
-                     b.bad);
+                     d.N, 0, d.nblk);
+  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, d, b.st, (const double*)b.Wc, b.part, b.gmaxp, b.tau, b.dcv,
+                     b.dtau, b.bad);
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
@@ -2443,13 +2468,15 @@ int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
   hipLaunchKernelGGL(k_red_build, dim3(dr.nblk), dim3(256), 0, s, d, b.st, h->Lo, h->R, h->span, p1, r.Dc, r.Ec,
                      r.GBc, r.gmaxp);
   const int rb = dr.nblk - 1;
-  cr_reduce(dr, s, b.st, r, 0, dr.nblk, rb, dr.nlev, b.bad);
+  int sym = 0;
+  cr_reduce(dr, s, b.st, r, 0, dr.nblk, rb, dr.nlev, b.bad, false, &sym);
+  cr_launch_top(dr, s, dr.nlev, 0, dr.nblk, b.st, r, b.bad, sym);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, dr, b.st, r.Hloc, r.gloc, r.Tau, r.part, 0,
-                     0, 1, dr.nblk);
+                     0, 0, dr.nblk);
   const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
   hipLaunchKernelGGL(k_red_part, dim3(1), dim3(256), 0, s, nE, h->Lo, b.st, p1, r.part);
-  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, dr, b.st, r.Dc, r.GBc, r.part, r.gmaxp, b.tau, r.dcv, b.dtau,
-                     b.bad);
+  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, dr, b.st, (const double*)r.Wc, r.part, r.gmaxp, b.tau, r.dcv,
+                     b.dtau, b.bad);
   for (int lv = dr.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (dr.nblk - st + 2 * st - 1) / (2 * st);
