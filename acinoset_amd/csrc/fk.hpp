@@ -53,6 +53,22 @@ __device__ __forceinline__ SkelView skel_view(const int* I, const double* R) {
   return s;
 }
 
+// Largest skeleton table (ints): header, joints + origins, nodes, outputs, parameter
+// kinds, node-parameter dependence.
+#define FK_MAX_INTS (FK_HDR + 9 * FK_MAXJ + 4 * FK_MAXN + FK_MAXN + 4 * FK_MAXP + FK_MAXN * FK_MAXP)
+
+// Stage the skeleton table (global) in LDS: the FK and its Jacobian walk it with dependent
+// loads, which must not be HBM round trips. Ends with a barrier.
+__device__ __forceinline__ SkelView skel_stage(const int* __restrict__ I, const double* __restrict__ R, int* sI,
+                                               double* sR, int tid, int nth) {
+  const int J = I[0], K = I[1], P = I[2], L = I[3];
+  const int ni = FK_HDR + 9 * J + 4 * K + L + 4 * P + K * P, nr = 3 * K;
+  for (int e = tid; e < ni; e += nth) sI[e] = I[e];
+  for (int e = tid; e < nr; e += nth) sR[e] = R[e];
+  __syncthreads();
+  return skel_view(sI, sR);
+}
+
 struct FkShared {
   double sn[FK_MAXP], cs[FK_MAXP], xp[FK_MAXP];
   double root[3], world[3];  // head-root translation (x_0, y_0, z_0) and world (lure) position

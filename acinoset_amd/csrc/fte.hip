@@ -131,7 +131,21 @@ __device__ double block_max(double v, double* s_red) {
 // Jacobian (C times fewer FK derivatives, 2C/2 = C times fewer MFMA K-steps); the second
 // touches only the 9 + C shift / delay columns and is added when H is stored.
 // ---------------------------------------------------------------------------------------
-#define LIN_OCH 256  // observations per aggregation chunk (= blockDim)
+#ifdef FTE_PROFILE
+__device__ unsigned long long g_fte_prof[64];  // wall-clock ticks (100 MHz) of block 0 phases
+// k_fte_linearize phases (block 0, thread 0, after a barrier), slots 56..61
+#define LPROF(slot)                                                          \
+  do {                                                                     \
+    __syncthreads();                                                       \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                               \
+      atomicAdd(&g_fte_prof[slot], wall_clock64() - lprof_t0);             \
+  } while (0)
+#define LPROF_T0 const unsigned long long lprof_t0 = wall_clock64();
+#else
+#define LPROF(slot)
+#define LPROF_T0
+#endif
+#define LIN_OCH 128  // observations per aggregation chunk (<= blockDim)
 #define LIN_MC 4     // markers per MFMA chunk (3 * LIN_MC operand rows)
 
 struct LinLds {
@@ -206,7 +220,10 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   __shared__ FkShared fk;
   __shared__ double s_dx[3], s_ddx[3];
   __shared__ double s_red[256];
-  const SkelView s = skel_view(I, Rl);
+  __shared__ int s_tabI[FK_MAX_INTS];
+  __shared__ double s_tabR[3 * FK_MAXN];
+  LPROF_T0
+  const SkelView s = skel_stage(I, Rl, s_tabI, s_tabR, tid, blockDim.x);
   const int f = k + 2;
   for (int i = tid; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
   for (int i = lo.am + tid; i < lo.cf; i += blockDim.x) lds[i] = 0.0;
@@ -217,6 +234,7 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   }
   fk_frame(s, X + f * P, fk, tid, blockDim.x);
   __syncthreads();
+  LPROF(56);
   if (tid < C) {
     const double tc = d.Ct ? tau[tid] : 0.0;
     const ShiftCoef sc = shift_coef(d.im, tc, d.Ts);
@@ -313,6 +331,7 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
     __syncthreads();
   }
 
+  LPROF(57);
   // (b) H = sum_l [D_l ; Q_l]^T [Z_l D_l + Q_l ; D_l] on v_mfma_f64_16x16x4f64: upper-triangle
   //     tiles of NT x NT, tile t on wave t % 4
   // tile t = wave + 4q (q = 0..2) of the NT (NT + 1) / 2 upper-triangle tiles, row-major
@@ -379,6 +398,7 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
     __syncthreads();
   }
 
+  LPROF(58);
   // (c) sum_c S_c^T Z_c S_c and sum_c S_c^T r_c (shift / delay columns), store
   auto zc_v = [&](int c, int i) {  // (Z_c v_c)[i]
     const double* z = s_ac + 9 * c;
@@ -431,6 +451,10 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   }
   const double tot = block_sum(rho, s_red);
   if (tid == 0) Floc[k] = tot;
+  LPROF(59);
+#ifdef FTE_PROFILE
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fte_prof[60], 1ull);
+#endif
 }
 
 static size_t lin_lds_bytes(const FteDims& d) {
@@ -629,7 +653,6 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
 #define CR_MAXBP 96
 
 #ifdef FTE_PROFILE  // per-phase wall-clock ticks (100 MHz) of block 0 (tools/prof_fte_phases.py)
-__device__ unsigned long long g_fte_prof[64];
 #define PROF_T0 unsigned long long t_prof = wall_clock64(); const unsigned long long t_start = t_prof; \
   const bool prof_on = ne * nsplit + (int)gridDim.x * 0 <= 12 && ne > 0;
 // timeline event: wave w of block 0 at time since the kernel start (deep levels only)
@@ -1462,7 +1485,7 @@ __global__ __launch_bounds__(64) void k_fte_cost(FteDims d, const int* __restric
   __shared__ FkShared fk;
   __shared__ double s_red[64];
   __shared__ double s_dx[3], s_ddx[3];
-  const SkelView s = skel_view(I, Rl);
+  const SkelView s = skel_view(I, Rl);  // 64 threads: staging the table in LDS costs more than it saves
   const int f = k + 2;
   if (tid < 3) {
     const double x0 = X[f * P + tid], x1 = X[(f - 1) * P + tid], x2 = X[(f - 2) * P + tid];

@@ -7,3 +7,4 @@ python tools/fte_iter_breakdown.py gpurun_out/ftetrace10k 10000 > gpurun_out/fte
 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ftetrace -o run -- python3 tools/prof_fte.py --reps 3 > gpurun_out/ftetrace.log 2>&1 || exit $?
 grep rep gpurun_out/ftetrace.log
 python tools/fte_iter_breakdown.py gpurun_out/ftetrace 1000 > gpurun_out/fte_breakdown.log; head -4 gpurun_out/fte_breakdown.log
+timeout -k 10 120 python tools/prof_lin_phases.py 1000 > gpurun_out/lin_phases.log 2>&1; cat gpurun_out/lin_phases.log
