@@ -204,13 +204,23 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
                                                        const double* __restrict__ taubuf,
                                                        const FteState* __restrict__ st, int force, int k0,
                                                        double* __restrict__ Hloc, double* __restrict__ gloc,
-                                                       double* __restrict__ Floc) {
-  if (!force && (st->status != 0 || !st->relin)) return;
+                                                       double* __restrict__ Floc, int spec,
+                                                       double* __restrict__ Fq, const double* __restrict__ qinv) {
+  // spec: speculative linearisation at the trial state X[cur ^ 1] into the second
+  // Hloc / gloc / Floc buffer, with the model cost of the frame's stencil in Fq: it is the
+  // trial cost for k_fte_lm, and an accepted step (cur ^= 1) needs no new linearisation
+  if (spec ? st->status != 0 : (!force && (st->status != 0 || !st->relin))) return;
+  {
+    const size_t hb = spec ? (size_t)(st->cur ^ 1) : 0;
+    Hloc += hb * d.N * FTE_NZP * FTE_NZP;
+    gloc += hb * d.N * FTE_NZP;
+    Floc += hb * d.N;
+  }
   const int k = blockIdx.x + k0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
   const int P = d.P, C = d.C, L = d.L, NZ = d.NZ;
   const int NZP = (NZ + 15) & ~15, LD = NZP + 1, NT = NZP >> 4;
-  const int cur = force ? 0 : st->cur;
+  const int cur = force ? 0 : (spec ? st->cur ^ 1 : st->cur);
   const double* X = Xbuf + (size_t)cur * d.M * P;
   const double* tau = taubuf + (size_t)cur * d.NT + (d.var ? (size_t)k * C : 0);
   extern __shared__ double lds[];
@@ -451,6 +461,18 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   }
   const double tot = block_sum(rho, s_red);
   if (tid == 0) Floc[k] = tot;
+  if (Fq) {  // the model stencil ending at row k + 2 (rows k-1 .. k+2), as k_fte_cost
+    double q = 0.0;
+    if (k >= 1) {
+      const double its2 = 1.0 / (d.Ts * d.Ts);
+      for (int p = tid; p < P; p += blockDim.x) {
+        const double sm = (X[f * P + p] - 3.0 * X[(f - 1) * P + p] + 3.0 * X[(f - 2) * P + p] - X[(f - 3) * P + p]) * its2;
+        q += qinv[p] * sm * sm;
+      }
+    }
+    q = block_sum(q, s_red);
+    if (tid == 0) Fq[k] = q;
+  }
   LPROF(59);
 #ifdef FTE_PROFILE
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fte_prof[60], 1ull);
@@ -471,7 +493,8 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
                                                       int hi, const double* __restrict__ Hloc,
                                                       const double* __restrict__ gloc, double* __restrict__ Ab,
                                                       double* __restrict__ gb, double* __restrict__ Bt,
-                                                      double* __restrict__ gmaxp, double* __restrict__ Adiag) {
+                                                      double* __restrict__ gmaxp, double* __restrict__ Adiag,
+                                                      int hsel) {
   // Terms are owned by the lowest X row they touch: frame k (rows k..k+2) iff lo <= k < hi,
   // model stencil m (rows m-3..m) iff lo <= m-3 < hi. The single-GPU solve owns all terms;
   // a frame-window rank owns the terms starting in its window (dist path below).
@@ -481,6 +504,10 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
   // 1e-12) (oracle damping), held delays skipped; Adiag keeps the raw diagonal for k_cr_build.
   const bool elim = d.var && !force;
   if (!force && (st->status != 0 || (!st->relin && !elim))) return;
+  if (hsel) {  // the linearisation of X[cur] (double-buffered by the speculative solve)
+    Hloc += (size_t)st->cur * d.N * FTE_NZP * FTE_NZP;
+    gloc += (size_t)st->cur * d.N * FTE_NZP;
+  }
   const int f = blockIdx.x + f0;
   const int tid = threadIdx.x, nth = blockDim.x;
   const int P = d.P, Cg = d.Cg, N = d.N, C = d.C;
@@ -1220,10 +1247,14 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
                                                         const double* __restrict__ Hloc,
                                                         const double* __restrict__ gloc,
                                                         const double* __restrict__ Tau, double* __restrict__ part,
-                                                        int k_lo, int k_hi, int b_lo, int b_hi) {
+                                                        int k_lo, int k_hi, int b_lo, int b_hi, int hsel) {
   // frames [k_lo, k_hi) (tau blocks of their normal matrices / gradients) and eliminated
   // super-blocks [b_lo, b_hi) (tau Schur terms), each range cut into CR_NCHUNK chunks
   if (st->status != 0) return;
+  if (hsel) {
+    Hloc += (size_t)st->cur * d.N * FTE_NZP * FTE_NZP;
+    gloc += (size_t)st->cur * d.N * FTE_NZP;
+  }
   const int ch = blockIdx.x;
   const int P = d.P, Cg = d.Cg, GR = d.GR;
   const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
@@ -1399,8 +1430,12 @@ __global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __r
                                                   const double* __restrict__ dcv, const double* __restrict__ dtau,
                                                   const double* __restrict__ Hloc, const double* __restrict__ gloc,
                                                   double* __restrict__ Xbuf, double* __restrict__ taubuf,
-                                                  double* __restrict__ normp) {
+                                                  double* __restrict__ normp, int hsel) {
   if (st->status != 0) return;
+  if (hsel) {
+    Hloc += (size_t)st->cur * d.N * FTE_NZP * FTE_NZP;
+    gloc += (size_t)st->cur * d.N * FTE_NZP;
+  }
   const int i = blockIdx.x;
   const int P = d.P, BP = d.BP;
   __shared__ double s_red[256];
@@ -1533,9 +1568,10 @@ __global__ __launch_bounds__(64) void k_fte_cost(FteDims d, const int* __restric
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict__ st, FteOptsDev o, int init,
                                                 const double* __restrict__ Fm, const double* __restrict__ Fq,
-                                                const double* __restrict__ normp) {
+                                                const double* __restrict__ normp, int spec) {
   __shared__ double s_red[256];
   const int tid = threadIdx.x;
+  if (spec) Fm += (size_t)(st->cur ^ 1) * d.N;  // the trial's measurement terms (Floc buffer)
   double a = 0.0, b = 0.0;
   for (int k = tid; k < d.N; k += blockDim.x) {
     a += Fm[k];
@@ -1663,8 +1699,8 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
     return o;
   };
   const size_t Cg1 = d.Cg ? d.Cg : 1;
-  const size_t oX = take((size_t)2 * M * P), oT = take(2 * (size_t)d.NT), oAd = take((size_t)M * P), oH = take((size_t)N * FTE_NZP * FTE_NZP),
-               og = take((size_t)N * FTE_NZP), oF = take(N), oAb = take((size_t)M * 4 * P * P),
+  const size_t oX = take((size_t)2 * M * P), oT = take(2 * (size_t)d.NT), oAd = take((size_t)M * P), oH = take((size_t)2 * N * FTE_NZP * FTE_NZP),
+               og = take((size_t)2 * N * FTE_NZP), oF = take((size_t)2 * N), oAb = take((size_t)M * 4 * P * P),
                ogb = take((size_t)M * P), oBt = take((size_t)M * P * Cg1), ogm = take(M),
                oD = take((size_t)n * BP * BP), oE = take((size_t)n * BP * BP), oG = take((size_t)n * BP * GR),
                oW = take((size_t)n * BP * (2 * BP + GR)), oTau = take((size_t)n * GR * GR),
@@ -1842,9 +1878,9 @@ static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
   hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
-                     b.st, force, 0, b.Hloc, b.gloc, b.Floc);
+                     b.st, force, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr);
   hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, force, 0, 0, INT_MAX,
-                     b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag);
+                     b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1);
 }
 
 // one LM iteration: linearise (if the last step was accepted), cyclic-reduction solve,
@@ -1852,14 +1888,18 @@ static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
 static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& o) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
-  fte_enqueue_linearize(S, s, 0);
+  // the linearisation of X[cur] is already there (initial, or speculative at the last
+  // accepted trial): assemble the banded rows when it is new (or when the variable delays
+  // must be re-eliminated for a new damping)
+  hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, 0, 0, 0, INT_MAX,
+                     b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1);
   cr_launch_build(d, s, d.nblk, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, 0, -1, -1, d.var ? b.Adiag : nullptr);
   const int bend = d.nblk - 1;
   int sym = 0;
   cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad, false, &sym);
   cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, sym);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
-                     d.N, 0, d.nblk);
+                     d.N, 0, d.nblk, 1);
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, d, b.st, (const double*)b.Wc, b.part, b.gmaxp, b.tau, b.dcv,
                      b.dtau, b.bad);
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
@@ -1868,10 +1908,12 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
     hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, d, st, 0, bend, b.st, b.Wc, b.dtau, b.dcv);
   }
   hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
-                     b.normp);
-  hipLaunchKernelGGL(k_fte_cost, dim3(d.N), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau, b.qinv,
-                     b.st, 1, 0, 0, INT_MAX, b.Fm, b.Fq);
-  hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 0, b.Fm, b.Fq, b.normp);
+                     b.normp, 1);
+  // speculative linearisation at the trial state: its measurement terms and the model terms
+  // are the trial cost (no separate cost pass)
+  hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
+                     b.X, b.tau, b.st, 0, 0, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv);
+  hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 0, b.Floc, b.Fq, b.normp, 1);
 }
 
 // =======================================================================================
@@ -2157,7 +2199,11 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   FteOptsDev o{op.max_iters, op.ftol, op.xtol, op.gtol};
   hipLaunchKernelGGL(k_fte_cost, dim3(d.N), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau, b.qinv,
                      b.st, 0, 0, 0, INT_MAX, b.Fm, b.Fq);
-  hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 1, b.Fm, b.Fq, b.normp);
+  hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 1, b.Fm, b.Fq, b.normp, 0);
+  // the linearisation of the initial state (buffer cur = 0); later ones are speculative
+  if (op.max_iters > 0)
+    hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
+                       b.X, b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr);
   ACS_HIP(ctx, hipGetLastError());
   // capture `chunk` iterations into one hipGraph (kernels read the LM state from device
   // memory, so the graph is static); replay until the device reports a stop status
@@ -2463,14 +2509,15 @@ int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
   if (h->a0 < d.nblk) {
     if (h->k_hi > h->k_lo)
       hipLaunchKernelGGL(k_fte_linearize, dim3(h->k_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
-                         b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc);
+                         b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr,
+                         (const double*)nullptr);
     hipLaunchKernelGGL(k_fte_assemble, dim3(h->f_hi - h->f_lo), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, 0,
-                       h->f_lo, h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag);
+                       h->f_lo, h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 0);
     const int top = std::min(h->bend, d.nblk - 1);
     cr_launch_build(d, s, top - h->a0 + 1, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, h->a0, h->a0, h->bend, nullptr);
     const double* Efin = dist_local_cr(h);
     hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part,
-                       h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk));
+                       h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk), 0);
     hipLaunchKernelGGL(k_dist_pack, dim3(32, 2), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.Dc, Efin,
                        b.GBc, b.Ab, b.gb, p1);
     hipLaunchKernelGGL(k_dist_pack_small, dim3(1), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.part,
@@ -2495,7 +2542,7 @@ int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
   cr_reduce(dr, s, b.st, r, 0, dr.nblk, rb, dr.nlev, b.bad, false, &sym);
   cr_launch_top(dr, s, dr.nlev, 0, dr.nblk, b.st, r, b.bad, sym);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, dr, b.st, r.Hloc, r.gloc, r.Tau, r.part, 0,
-                     0, 0, dr.nblk);
+                     0, 0, dr.nblk, 0);
   const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
   hipLaunchKernelGGL(k_red_part, dim3(1), dim3(256), 0, s, nE, h->Lo, b.st, p1, r.part);
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, dr, b.st, (const double*)r.Wc, r.part, r.gmaxp, b.tau, r.dcv,
@@ -2528,7 +2575,7 @@ int acs_fte_dist_phase3(acs_fte_dist* h, const double* p2, double* p3) {
   FteBuffers& b = h->S.b;
   hipStream_t s = ctx->stream;
   hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, p2, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
-                     b.normp);
+                     b.normp, 0);
   if (h->c_hi > h->c_lo)
     hipLaunchKernelGGL(k_fte_cost, dim3(h->c_hi - h->c_lo), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
                        b.tau, b.qinv, b.st, 1, h->c_lo, h->own_lo, h->own_hi, b.Fm, b.Fq);
