@@ -38,6 +38,27 @@ struct acs_ctx {
 
 int acs_fail(acs_ctx* ctx, int code, const char* fmt, ...);
 
+// Makes `device` current for the lifetime of the guard and restores the caller's current
+// device afterwards. Every exported entry point that allocates or launches holds one, so two
+// contexts on different devices (or a call from another host thread) allocate workspace and
+// launch on the context's own device, and the caller's (e.g. torch's) current device is left
+// as it was.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int device) {
+    if (device < 0) return;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != device) (void)hipSetDevice(device);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+#define ACS_DEVICE_GUARD(ctx) DeviceGuard _acs_dev_guard((ctx) ? (ctx)->device : -1)
+
 #define ACS_HIP(ctx, call)                                                                 \
   do {                                                                                     \
     hipError_t _e = (call);                                                                \

@@ -85,7 +85,7 @@ int acs_ctx_create(int device, acs_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return ACS_E_NODEV;
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ACS_E_NODEV;
-  if (hipSetDevice(device) != hipSuccess) return ACS_E_NODEV;
+  DeviceGuard guard(device);  // the stream belongs to `device`; the caller's device is restored
   acs_ctx* c = new acs_ctx();
   c->device = device;
   c->n_cu = prop.multiProcessorCount;
@@ -100,7 +100,7 @@ int acs_ctx_create(int device, acs_ctx** out) {
 
 int acs_ctx_destroy(acs_ctx* ctx) {
   if (!ctx) return ACS_OK;
-  (void)hipSetDevice(ctx->device);
+  ACS_DEVICE_GUARD(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (int i = 0; i < WS_NSLOTS; ++i)
     if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
@@ -117,6 +117,7 @@ int acs_ctx_set_stream(acs_ctx* ctx, void* s) {
 }
 
 int acs_ctx_sync(acs_ctx* ctx) {
+  ACS_DEVICE_GUARD(ctx);
   ACS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ACS_OK;
 }
@@ -180,6 +181,7 @@ extern "C" {
 int acs_project_fisheye(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* pts,
                         const int32_t* cam_idx, int64_t n, int32_t fte_form, double* uv_out,
                         uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   ACS_CHECK(ctx, n >= 0 && n_cams > 0, "acs_project_fisheye: n=%lld n_cams=%d", (long long)n, n_cams);
   if (n == 0) return ACS_OK;
   void *dc, *dp, *di = nullptr;
@@ -200,6 +202,7 @@ int acs_project_fisheye(acs_ctx* ctx, const double* cams, int32_t n_cams, const 
 int acs_sba_residuals(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
                       const int32_t* pt_idx, const int32_t* cam_idx, int64_t n_obs, const double* pts,
                       int64_t n_pts, double* resid_out, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   ACS_CHECK(ctx, n_obs >= 0 && n_pts >= 0 && n_cams > 0, "acs_sba_residuals: bad sizes");
   if (n_obs == 0) return ACS_OK;
   void *dc, *duv, *dpi, *dci, *dp;
@@ -222,6 +225,7 @@ int acs_sba_residuals(acs_ctx* ctx, const double* cams, int32_t n_cams, const do
 
 int acs_redescending_loss(acs_ctx* ctx, const double* err, int64_t n, double a, double b, double c,
                           double* out, double* dout, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   ACS_CHECK(ctx, n >= 0 && c > b, "acs_redescending_loss: bad args");
   if (n == 0) return ACS_OK;
   void* de;

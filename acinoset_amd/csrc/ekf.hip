@@ -800,6 +800,7 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
                 const double* Q, const double* P0, const double* s0, int32_t ref_numerics, double eps,
                 double* x_pred, double* x_est, double* x_smooth, double* P_est, double* P_smooth,
                 int64_t* outliers, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   int hdr[FK_HDR];
   if (flags & ACS_DEVICE_PTRS)
     ACS_HIP(ctx, hipMemcpy(hdr, skel_ints, sizeof(hdr), hipMemcpyDeviceToHost));

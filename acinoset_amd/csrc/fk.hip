@@ -70,6 +70,7 @@ __global__ __launch_bounds__(64) void k_fk(const int* __restrict__ I, const doub
 extern "C" int acs_fk(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
                       int64_t n_reals, const double* x, const double* dx, const double* ddx, const double* tau,
                       int64_t n, int32_t intermode, int32_t directions, double* out, double* jac, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   ACS_CHECK(ctx, n >= 0 && n_ints >= FK_HDR && skel_ints, "acs_fk: bad arguments");
   // table sizes are read on the host from the (host) header when possible
   int hdr[FK_HDR];

@@ -1699,8 +1699,12 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
     return o;
   };
   const size_t Cg1 = d.Cg ? d.Cg : 1;
-  const size_t oX = take((size_t)2 * M * P), oT = take(2 * (size_t)d.NT), oAd = take((size_t)M * P), oH = take((size_t)2 * N * FTE_NZP * FTE_NZP),
-               og = take((size_t)2 * N * FTE_NZP), oF = take((size_t)2 * N), oAb = take((size_t)M * 4 * P * P),
+  // the per-frame linearisation is double-buffered only for the speculative single-GPU
+  // solve (k_fte_linearize spec = 1 writes the trial's copy); the distributed handles
+  // (`owned`) linearise in place (hsel = spec = 0) and take one copy
+  const size_t nlin = owned ? 1 : 2;
+  const size_t oX = take((size_t)2 * M * P), oT = take(2 * (size_t)d.NT), oAd = take((size_t)M * P),
+               oH = take(nlin * N * FTE_NZP * FTE_NZP), og = take(nlin * N * FTE_NZP), oF = take(nlin * N), oAb = take((size_t)M * 4 * P * P),
                ogb = take((size_t)M * P), oBt = take((size_t)M * P * Cg1), ogm = take(M),
                oD = take((size_t)n * BP * BP), oE = take((size_t)n * BP * BP), oG = take((size_t)n * BP * GR),
                oW = take((size_t)n * BP * (2 * BP + GR)), oTau = take((size_t)n * GR * GR),
@@ -2179,6 +2183,7 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
                   const double* cams, int32_t n_cams, const double* meas, const double* w, int32_t n_frames,
                   int32_t shutter_delay, double Ts, const double* qinv, int32_t sd_mode, int32_t intermode, double* X,
                   double* tau, const acs_fte_opts* opts, acs_fte_report* report, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   acs_fte_opts op;
   acs_fte_default_opts(&op);
   if (opts) op = *opts;
@@ -2271,6 +2276,7 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
                  const double* cams, int32_t n_cams, const double* meas, const double* w, int32_t n_frames,
                  int32_t shutter_delay, double Ts, const double* qinv, int32_t sd_mode, int32_t intermode,
                  const double* X, const double* tau, double* cost3, double* grad, double* H, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   ACS_CHECK(ctx, !(flags & ACS_DEVICE_PTRS), "acs_fte_eval takes host pointers");
   FteSetup S;
   int rc;
@@ -2383,6 +2389,7 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
                         int32_t n_frames, int32_t shutter_delay, double Ts, const double* qinv, int32_t sd_mode,
                         int32_t intermode, const double* X, const double* tau, const acs_fte_opts* opts, int32_t rank,
                         int32_t world, acs_fte_dist** out, int64_t* payload_sizes, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   acs_fte_opts op;
   acs_fte_default_opts(&op);
   if (opts) op = *opts;
@@ -2478,6 +2485,7 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
 }
 
 int acs_fte_dist_destroy(acs_fte_dist* h) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   if (!h) return ACS_OK;
   (void)hipStreamSynchronize(h->ctx->stream);
   if (h->own) (void)hipFree(h->own);
@@ -2488,6 +2496,7 @@ int acs_fte_dist_destroy(acs_fte_dist* h) {
 
 // cost of the owned terms at the current state -> p3 (before the first phase 4, init = 1)
 int acs_fte_dist_init(acs_fte_dist* h, double* p3) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
@@ -2501,6 +2510,7 @@ int acs_fte_dist_init(acs_fte_dist* h, double* p3) {
 }
 
 int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
@@ -2528,6 +2538,7 @@ int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
 }
 
 int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
   const FteDims& dr = h->dr;
@@ -2570,6 +2581,7 @@ int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
 }
 
 int acs_fte_dist_phase3(acs_fte_dist* h, const double* p2, double* p3) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
@@ -2585,6 +2597,7 @@ int acs_fte_dist_phase3(acs_fte_dist* h, const double* p2, double* p3) {
 }
 
 int acs_fte_dist_phase4(acs_fte_dist* h, const double* p3, int32_t init, int32_t* status) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
@@ -2599,6 +2612,7 @@ int acs_fte_dist_phase4(acs_fte_dist* h, const double* p3, int32_t init, int32_t
 }
 
 int acs_fte_dist_result(acs_fte_dist* h, double* X, double* tau, acs_fte_report* report, uint32_t flags) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;

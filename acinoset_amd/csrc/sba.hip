@@ -179,17 +179,25 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
         break;
       }
     }
+    ++iters;
+    if (!pd) {
+      // not positive definite (lam near its floor on a degenerate point): no step, so no
+      // trial and no xtol test; raise lam as a rejection would (uniform over the group:
+      // pd comes from the group-summed H)
+      lam *= 10.0;
+      if (lam > 1e16) status = ACS_STATUS_STALLED;
+      continue;
+    }
     const double n0 = x0 + dx0, n1 = x1 + dx1, n2 = x2 + dx2;
     double Hn[6], gn[3], Fn;
     linearize(n0, n1, n2, Hn, gn, Fn);
     ++nfev;
-    ++iters;
     // |dx| <= xtol (xtol + |x|), compared squared
     const double xx = x0 * x0 + x1 * x1 + x2 * x2;
     const double xn = xx > 0.0 ? xx * rsq_nr(xx) : 0.0;
     const double xb = prm.xtol * (prm.xtol + xn);
     const bool small = dx0 * dx0 + dx1 * dx1 + dx2 * dx2 <= xb * xb;
-    if (pd && Fn < F) {
+    if (Fn < F) {
       const bool fconv = (F - Fn) <= prm.ftol * F;
       x0 = n0;
       x1 = n1;
@@ -474,6 +482,7 @@ extern "C" {
 int acs_sba_points_dense_io(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
                             const uint8_t* mask, int64_t n_pts, const double* pts_in, double* pts_out,
                             const acs_sba_opts* opts, acs_report* report, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   ACS_CHECK(ctx, n_pts >= 0 && n_cams >= 1 && n_cams <= 64, "acs_sba_points_dense: n_pts=%lld n_cams=%d (1..64)",
             (long long)n_pts, n_cams);
   if (n_pts == 0) {
@@ -504,12 +513,14 @@ int acs_sba_points_dense_io(acs_ctx* ctx, const double* cams, int32_t n_cams, co
 
 int acs_sba_points_dense(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv, const uint8_t* mask,
                          int64_t n_pts, double* pts, const acs_sba_opts* opts, acs_report* report, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   return acs_sba_points_dense_io(ctx, cams, n_cams, uv, mask, n_pts, pts, pts, opts, report, flags);
 }
 
 int acs_sba_points(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv, const int32_t* pt_idx,
                    const int32_t* cam_idx, int64_t n_obs, double* pts, int64_t n_pts, const acs_sba_opts* opts,
                    double* resid_before, double* resid_after, acs_report* report, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   ACS_CHECK(ctx, n_obs >= 0 && n_pts >= 0 && n_cams >= 1 && n_cams <= 255, "acs_sba_points: bad sizes");
   ACS_CHECK(ctx, n_obs < (int64_t)INT32_MAX, "acs_sba_points: n_obs too large");
   if (n_pts == 0 || n_obs == 0) {

@@ -507,6 +507,7 @@ int acs_sba_extrinsics(acs_ctx* ctx, double* cams, int32_t n_cams, const double*
                        const int32_t* cam_idx, int64_t n_obs, double* pts, int64_t n_pts,
                        const acs_sba_ext_opts* opts, double* resid_before, double* resid_after,
                        acs_sba_ext_report* report, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   acs_sba_ext_opts op;
   acs_sba_ext_default_opts(&op);
   if (opts) op = *opts;
@@ -798,6 +799,7 @@ int acs_sba_ext_dist_create(acs_ctx* ctx, const double* cams, int32_t n_cams, co
                             const int32_t* pt_idx, const int32_t* cam_idx, int64_t n_obs, const double* pts,
                             int64_t n_pts, const acs_sba_ext_opts* opts, int32_t rank, int32_t world,
                             acs_sba_ext_dist** out, int64_t* payload_sizes, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   acs_sba_ext_opts op;
   acs_sba_ext_default_opts(&op);
   if (opts) op = *opts;
@@ -885,6 +887,7 @@ int acs_sba_ext_dist_create(acs_ctx* ctx, const double* cams, int32_t n_cams, co
 }
 
 int acs_sba_ext_dist_destroy(acs_sba_ext_dist* h) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   if (!h) return ACS_OK;
   (void)hipStreamSynchronize(h->ctx->stream);
   if (h->own) (void)hipFree(h->own);
@@ -893,6 +896,7 @@ int acs_sba_ext_dist_destroy(acs_sba_ext_dist* h) {
 }
 
 int acs_sba_ext_dist_init(acs_sba_ext_dist* h, double* p3) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   hipStream_t s = h->ctx->stream;
 #define EXT_COST0(g) ext_dist_cost<g>(h, s, 0)
   EXT_G_SWITCH(h->d.G, EXT_COST0)
@@ -903,6 +907,7 @@ int acs_sba_ext_dist_init(acs_sba_ext_dist* h, double* p3) {
 }
 
 int acs_sba_ext_dist_phase1(acs_sba_ext_dist* h, double* p1) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   hipStream_t s = ctx->stream;
   const ExtDims& d = h->d;
@@ -919,6 +924,7 @@ int acs_sba_ext_dist_phase1(acs_sba_ext_dist* h, double* p1) {
 }
 
 int acs_sba_ext_dist_phase2(acs_sba_ext_dist* h, const double* p1, double* p3) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   hipStream_t s = ctx->stream;
   const ExtDims& d = h->d;
@@ -939,6 +945,7 @@ int acs_sba_ext_dist_phase2(acs_sba_ext_dist* h, const double* p1, double* p3) {
 }
 
 int acs_sba_ext_dist_phase3(acs_sba_ext_dist* h, const double* p3, int32_t init, int32_t* status) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   hipStream_t s = ctx->stream;
   hipLaunchKernelGGL(k_ext_lm_dist, dim3(1), dim3(64), 0, s, h->d, h->st, h->o, init, p3, h->camnorm);
@@ -952,6 +959,7 @@ int acs_sba_ext_dist_phase3(acs_sba_ext_dist* h, const double* p3, int32_t init,
 
 int acs_sba_ext_dist_result(acs_sba_ext_dist* h, double* cams, double* pts, acs_sba_ext_report* report,
                             uint32_t flags) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   hipStream_t s = ctx->stream;
   const ExtDims& d = h->d;

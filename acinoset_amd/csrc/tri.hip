@@ -159,6 +159,7 @@ extern "C" {
 
 int acs_triangulate_pairs(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv_a, const double* uv_b,
                           const int32_t* cam_a, const int32_t* cam_b, int64_t n, double* xyz_out, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   ACS_CHECK(ctx, n >= 0 && n_cams >= 1, "acs_triangulate_pairs: bad sizes");
   if (n == 0) return ACS_OK;
   void *dc, *da, *db, *dca, *dcb;
@@ -180,6 +181,7 @@ int acs_triangulate_pairs(acs_ctx* ctx, const double* cams, int32_t n_cams, cons
 
 int acs_triangulate_dense(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv, const uint8_t* mask,
                           int64_t n_pts, double* xyz_out, int32_t* n_pairs_out, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
   ACS_CHECK(ctx, n_pts >= 0 && n_cams >= 2, "acs_triangulate_dense: bad sizes");
   if (n_pts == 0) return ACS_OK;
   void *dc, *duv, *dm;

@@ -292,10 +292,14 @@ def solve(prob, X0, tau0=None, max_iters=200, ftol=1e-12, xtol=1e-12, gtol=1e-8,
     pin0 = prob.pinned() if prob.sd else None
     pin = pin0
     while iters < max_iters:
+        gp = g
         if pin0 is not None:
+            # the active set comes from the true gradient at the current state; the pinned
+            # (projected) copy drives the step, so a rejected step leaves g untouched
             pin = np.concatenate([pin0, active_bounds(prob, tau, g)])
-            g[pin] = 0.0
-        gmax = float(np.abs(g).max())
+            gp = g.copy()
+            gp[pin] = 0.0
+        gmax = float(np.abs(gp).max())
         if gmax <= gtol:
             status = 'gtol'
             break
@@ -305,7 +309,7 @@ def solve(prob, X0, tau0=None, max_iters=200, ftol=1e-12, xtol=1e-12, gtol=1e-8,
             A[pin, :] = 0.0
             A[:, pin] = 0.0
             A[pin, pin] = 1.0
-        d = spla.spsolve(A.tocsc(), -g)
+        d = spla.spsolve(A.tocsc(), -gp)
         dX, dtau = prob.unpack(d)
         Xn = X + dX
         taun = np.clip(tau + dtau, -prob.Ts, prob.Ts) if prob.sd else tau

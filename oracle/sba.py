@@ -23,6 +23,8 @@ Marquardt damping H + lam*diag(H); accept only on strict cost decrease. Spec sha
           float64 cost resolution, checked before the trial) |
           accepted and (dF <= ftol*F or |dx| <= xtol*(xtol+|x|))
           | rejected and |dx| <= xtol*(xtol+|x|) | lam > 1e16 | iters >= max_iters
+    A damped matrix that is not positive definite yields no step: the iteration counts as
+    a rejection (lam *= 10, no trial evaluation, no xtol test).
 """
 import numpy as np
 
@@ -135,13 +137,18 @@ def sba_points(points_2d, points_3d, point_idx, cam_idx, K, D, R, t, f_scale=50.
         act &= ~res
         dx[res] = 0.0
         xn = x + dx
-        Fn = np.where(act, cost(np.where(act[:, None], xn, x)), F)
-        nfev += act
+        # a damped matrix that is not positive definite gives no step: no trial, raise lam
+        pdm = np.zeros(n_pts, bool)
+        pdm[ia] = ok
+        trial = act & pdm
+        Fn = np.where(trial, cost(np.where(trial[:, None], xn, x)), F)
+        nfev += trial
         iters += act
         accept = act & np.zeros(n_pts, bool)
         accept[ia] = ok & (Fn[ia] < F[ia])
         reject = act & ~accept
-        small = np.linalg.norm(dx, axis=1) <= xtol * (xtol + np.linalg.norm(x, axis=1))
+        # the xtol test needs a step: only where the Cholesky succeeded
+        small = pdm & (np.linalg.norm(dx, axis=1) <= xtol * (xtol + np.linalg.norm(x, axis=1)))
         ftol_hit = accept & ((F - Fn) <= ftol * F)
         x = np.where(accept[:, None], xn, x)
         lam = np.where(accept, np.maximum(lam * 0.1, 1e-15), np.where(reject, lam * 10.0, lam))

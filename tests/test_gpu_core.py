@@ -135,6 +135,26 @@ def test_sba_edge_cases(ctx):
         ctx.sba_points(cams, g['points_2d'], g['point_indices'] + 10 ** 6, g['camera_indices'], g['points_3d'])
 
 
+def test_sba_single_observation_points(ctx):
+    """Degenerate points seen by one camera (rank-2 Gauss-Newton matrix): the solve must
+    follow the oracle (a damped matrix that is not positive definite raises lambda instead
+    of stopping on a zero step) and reproject onto the observation."""
+    g = golden('sba_cfg1')
+    rng = np.random.default_rng(0)
+    n = 64
+    X = g['points_3d'][:n] + rng.normal(0, 0.05, (n, 3))
+    ci = (np.arange(n) % 2).astype(np.int32)
+    pi = np.arange(n, dtype=np.int32)
+    uv = fisheye.project(g['points_3d'][:n], g['K'][ci], g['D'][ci], g['R'][ci], g['t'][ci]) + 1.0
+    pts, rb, ra, rep = ctx.sba_points(_cams(g), uv, pi, ci, X)
+    x_or, info = osba.sba_points(uv, X, pi, ci, g['K'], g['D'], g['R'], g['t'], return_info=True)
+    counts = np.bincount(info['status'], minlength=7)
+    names = ['running', 'gtol', 'ftol', 'xtol', 'stalled', 'maxiter', 'noobs']
+    assert {k: rep['status_counts'][k] for k in names} == dict(zip(names, counts.tolist()))
+    assert np.abs(ra).max() < 1e-9  # reprojects exactly (the depth along the ray is free)
+    assert np.abs(pts - x_or).max() < 1e-6
+
+
 def test_sba_dense_io_matches_inplace(ctx):
     """acs_sba_points_dense_io: separate initial/solution buffers give the in-place result
     bit for bit and leave the initial points untouched (incl. a point with no views)."""
@@ -156,3 +176,29 @@ def test_sba_dense_io_matches_inplace(ctx):
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
     np.testing.assert_array_equal(d['pts0'].cpu().numpy(), pts0)
     np.testing.assert_array_equal(ref[3], pts0[3])
+
+
+def test_context_keeps_caller_device(ctx):
+    """Every entry point makes the context's device current for its own work and restores
+    the caller's current device (torch shares the HIP runtime's current device)."""
+    import torch
+    n = torch.cuda.device_count()
+    dev = n - 1
+    torch.cuda.set_device(0)
+    c = _native.Context(dev)
+    g = golden('sba_cfg1')
+    a = c.sba_points(_cams(g), g['points_2d'], g['point_indices'], g['camera_indices'], g['points_3d'])[0]
+    assert torch.cuda.current_device() == 0
+    b = ctx.sba_points(_cams(g), g['points_2d'], g['point_indices'], g['camera_indices'], g['points_3d'])[0]
+    np.testing.assert_array_equal(a, b)
+    if n > 1:
+        # two contexts on two devices, used alternately from a thread whose current device
+        # is neither's: workspace and launches follow each context
+        torch.cuda.set_device(0)
+        c0 = _native.Context(0)
+        for _ in range(2):
+            np.testing.assert_array_equal(c.sba_points(_cams(g), g['points_2d'], g['point_indices'],
+                                                       g['camera_indices'], g['points_3d'])[0], b)
+            np.testing.assert_array_equal(c0.sba_points(_cams(g), g['points_2d'], g['point_indices'],
+                                                        g['camera_indices'], g['points_3d'])[0], b)
+        assert torch.cuda.current_device() == 0
