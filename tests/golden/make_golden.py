@@ -326,8 +326,205 @@ def board_fixture(n_img=8, cams=(0, 1, 2), board_shape=(9, 6), square=0.088, see
     print(f'board: {len(b2)} board obs + {len(m2)} manual obs, ref {dt:.1f}s')
 
 
+def _load_ref_fte():
+    """The reference's `core.fte` module (src/core/fte.py), loaded from its file with the
+    numeric Pyomo stand-in (`_pyomo_eval`) and stubs for what it imports but does not
+    compute with: seaborn, `core.metrics.save_error_dists` (plots) and `lib.app`
+    (logging, plots, the pickle/video writer). The stub `save_fte` captures the states
+    dict the reference hands to it."""
+    import importlib.util
+    import types
+    from unittest import mock
+    import _pyomo_eval
+    _pyomo_eval.install()
+    sys.modules.setdefault('seaborn', mock.MagicMock())
+    captured = {}
+    app = types.ModuleType('lib.app')
+    app.start_logging = lambda *a, **k: None
+    app.stop_logging = lambda *a, **k: None
+    app.plot_cheetah_states = lambda *a, **k: None
+    app.plot_shutter_delay = lambda *a, **k: None
+
+    def save_fte(states, mode, out_dir, scene_fpath, start_frame, **k):
+        captured.clear()
+        captured.update(states=states, start_frame=start_frame, kwargs=k)
+        return os.path.join(out_dir, 'fte.pickle')
+    app.save_fte = save_fte
+    sys.modules['lib.app'] = app
+    import lib
+    lib.app = app
+    core = types.ModuleType('core')
+    core.__path__ = [os.path.join(REF_SRC, 'core')]
+    metrics = types.ModuleType('core.metrics')
+    metrics.save_error_dists = lambda *a, **k: 0.0
+    sys.modules['core'] = core
+    sys.modules['core.metrics'] = metrics
+    spec = importlib.util.spec_from_file_location('core.fte', os.path.join(REF_SRC, 'core', 'fte.py'))
+    ref_fte = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ref_fte)
+    return ref_fte, _pyomo_eval, captured
+
+
+def fte_fixture(name, mode, n_frames, cams, sd, sd_mode, intermode, start_frame=2, seed=41, n_points=3):
+    """Runs the reference's own `core.fte.fte` (src/core/fte.py:28-588) up to the IPOPT call
+    and evaluates ITS model at chosen points (see `_pyomo_eval`). Recorded:
+
+    * the reference's initial point (x, dx, ddx, poses, slack_meas, shutter delay;
+      :254-292) and the triangulated nose it was fitted to;
+    * which constraint blocks the reference creates (the joint-angle bounds :330-430 are
+      gated on parameter names being in the MARKER list, so none is ever created);
+    * `n_points` feasible points: x, dx[1], ddx[1], tau chosen at random, dx/ddx for n >= 2
+      by the differences the build's elimination claims, poses / slack_meas / slack_model
+      from the reference's own constraint bodies. At each: every constraint residual
+      (the integration and shutter constraints must hold exactly) and the objective;
+    * one infeasible point (every variable random): every constraint body and the
+      objective, so each block can be restated term by term;
+    * the states dict and reprojection table the reference builds from feasible point 0
+      (:540-575) after the 'solve'.
+
+    DLC rows that are not visible carry NaN in the synthetic table; they have likelihood 0
+    (weight 0), and are written as 0 px here because a NaN measurement would make the
+    reference's 0 * slack term NaN."""
+    ref_fte, pe, captured = _load_ref_fte()
+    scene = synth.load_scene_file().subset(list(cams))
+    total = n_frames + start_frame + 2
+    seq = synth.make_sequence(total, scene, mode=mode, seed=seed, tau_max=0.004 if sd else 0.0)
+    df = seq.to_df()
+    df['x'] = df['x'].fillna(0.0)
+    df['y'] = df['y'].fillna(0.0)
+    end_frame = start_frame + n_frames - 1
+    fps = 90.0
+    Ts = 1.0 / fps
+    rng = np.random.default_rng(seed + 100)
+    rec = {}
+
+    nose = {}
+    orig_pair = ref_fte.utils.get_pairwise_3d_points_from_df
+
+    def pair_spy(*a, **k):
+        out = orig_pair(*a, **k)
+        nz = out[out['marker'] == 'nose']
+        nose.update(frame=nz['frame'].to_numpy(np.float64), xyz=nz[['x', 'y', 'z']].to_numpy(np.float64))
+        return out
+    ref_fte.utils.get_pairwise_3d_points_from_df = pair_spy
+
+    def evaluate(m):
+        out = {}
+        for cname, con in m.components(pe.Constraint).items():
+            ev = con.evaluate(m)
+            kinds = {v[0] for v in ev.values()}
+            assert len(kinds) <= 1, (cname, kinds)
+            if kinds == {'range'}:
+                out[cname] = np.array([[v[1], v[2], v[3]] for v in ev.values()])
+            elif ev:
+                out[cname] = np.array([v[1] for v in ev.values()])
+            else:
+                out[cname] = np.zeros(0)
+        return out, m.components(pe.Objective)['obj'].evaluate(m)
+
+    def body_with(m, cname, vname, zero_first=None):
+        """Set variable `vname` to the body of constraint `cname` evaluated with it at 0
+        (the constraint's index set equals the variable's; missing indices stay 0)."""
+        var = m.components(pe.Var)[vname]
+        var.set_values(np.zeros(len(var.data)))
+        ev = m.components(pe.Constraint)[cname].evaluate(m)
+        vals = np.array([ev[k][1] if k in ev else 0.0 for k in var.keys()])
+        var.set_values(vals)
+
+    def hook(m):
+        V = m.components(pe.Var)
+        N, P = len(m.N), len(m.P)
+        rec['init'] = {k: v.values() for k, v in V.items()}
+        rec['constraints'] = sorted(m.components(pe.Constraint))
+        truth = seq.x[start_frame:end_frame + 1]
+        tau_shape = (N, len(cams)) if sd_mode == 'variable' else (len(cams),)
+        for i in range(n_points + 1):
+            x = truth + rng.normal(0, 0.02, truth.shape)
+            if i < n_points:       # feasible: backward-Euler differences, constant-acc slack
+                dx = np.zeros_like(x)
+                ddx = np.zeros_like(x)
+                dx[0] = rng.normal(0, 1.0, P)
+                ddx[0] = rng.normal(0, 10.0, P)
+                dx[1:] = (x[1:] - x[:-1]) / Ts
+                for n in range(1, N):
+                    ddx[n] = (dx[n] - dx[n - 1]) / Ts
+            else:                  # infeasible: everything random
+                dx = rng.normal(0, 1.0, x.shape)
+                ddx = rng.normal(0, 10.0, x.shape)
+            V['x'].set_values(x)
+            V['dx'].set_values(dx)
+            V['ddx'].set_values(ddx)
+            if sd:
+                tau = rng.uniform(-Ts, Ts, tau_shape)
+                if i < n_points:
+                    tau[..., 0] = 0.0
+                V['shutter_delay'].set_values(tau)
+            if i < n_points:
+                body_with(m, 'pose_constraint', 'poses')
+                body_with(m, 'measurement', 'slack_meas')
+                body_with(m, 'constant_acc', 'slack_model')
+            else:
+                V['poses'].set_values(rec['init']['poses'] + rng.normal(0, 0.01, len(V['poses'].data)))
+                V['slack_meas'].set_values(rng.normal(0, 5.0, len(V['slack_meas'].data)))
+                V['slack_model'].set_values(rng.normal(0, 20.0, len(V['slack_model'].data)))
+            cons, obj = evaluate(m)
+            tag = f'pt{i}' if i < n_points else 'rand'
+            rec[tag] = dict(vars={k: v.values() for k, v in V.items()}, cons=cons, obj=obj)
+        # leave the model at feasible point 0 for the reference's post-processing
+        for k, v in rec['pt0']['vars'].items():
+            V[k].set_values(v)
+        return None
+
+    pe.SOLVE_HOOK = hook
+    cam_params = (scene.K, scene.D, scene.R, scene.t, tuple(scene.res), scene.n_cams)
+    scene_path = f'/tmp/golden_{name}_scene.json'
+    scene.to_json(scene_path)
+    out_dir = f'/tmp/golden_{name}'
+    t0 = time.time()
+    try:
+        ref_fte.fte(out_dir, df, mode, cam_params, start_frame, end_frame, 0.5, scene_path,
+                    params={'vid_fps': fps}, shutter_delay=sd, shutter_delay_mode=sd_mode,
+                    interpolation_mode=intermode, video=False, plot=False)
+    finally:
+        ref_fte.utils.get_pairwise_3d_points_from_df = orig_pair
+        pe.SOLVE_HOOK = None
+    dt = time.time() - t0
+    out = dict(K=scene.K, D=scene.D, R=scene.R, t=scene.t, res=np.array(scene.res), fps=fps, thresh=0.5,
+               mode=mode, sd=sd, sd_mode=sd_mode, intermode=intermode, start_frame=start_frame,
+               end_frame=end_frame, n_points=n_points, ref_seconds=dt, constraints=np.array(rec['constraints']),
+               **_df_arrays(df, seq.markers), nose_frame=nose['frame'], nose_xyz=nose['xyz'])
+    for k, v in rec['init'].items():
+        out[f'init_{k}'] = v
+    for tag in [f'pt{i}' for i in range(n_points)] + ['rand']:
+        for k, v in rec[tag]['vars'].items():
+            out[f'{tag}_var_{k}'] = v
+        for k, v in rec[tag]['cons'].items():
+            out[f'{tag}_con_{k}'] = v
+        out[f'{tag}_obj'] = rec[tag]['obj']
+    st = captured['states']
+    for k in ('x', 'dx', 'ddx', 'shutter_delay'):
+        if k in st:
+            out[f'out_{k}'] = np.asarray(st[k], np.float64)
+    errs = st.get('reprj_errors') or {}
+    for c, e in errs.items():
+        if e is not None and len(e):
+            out[f'out_reprj_{c}'] = e[['frame', 'pixel_residual']].to_numpy(np.float64)
+    out['out_start_frame'] = captured['start_frame']
+    np.savez_compressed(os.path.join(HERE, f'{name}.npz'), **out)
+    worst = max(float(np.abs(v).max()) for k, v in rec['pt0']['cons'].items()
+                if v.size and v.ndim == 1)
+    print(f'{name}: N={n_frames} C={len(cams)} mode={mode} sd={sd}/{sd_mode}/{intermode}, '
+          f'constraints {rec["constraints"]}, feasible-point max |residual| {worst:.2e}, '
+          f'objective {rec["pt0"]["obj"]:.6f}, reference build+eval {dt:.1f}s')
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['loss', 'fk', 'tri', 'cfg1', 'cfg2', 'ext']
+    if 'fte' in which:
+        fte_fixture('fte_head_const', 'head', 8, range(6), True, 'const', 'vel')
+        fte_fixture('fte_default_const', 'default', 5, range(6), True, 'const', 'vel')
+        fte_fixture('fte_default_var_acc', 'default', 4, range(3), True, 'variable', 'acc')
+        fte_fixture('fte_head_nosd', 'head', 6, range(3), False, 'const', 'pos')
     if 'loss' in which:
         loss_fixture()
     if 'fk' in which:
