@@ -25,6 +25,7 @@ enum WsSlot {
   WS_FTE10, WS_FTE11, WS_FTE12, WS_FTE13, WS_FTE14, WS_FTE15,
   WS_NSLOTS
 };
+enum GraphSlot { GRAPH_FTE = 0, GRAPH_NSLOTS };
 
 struct acs_ctx {
   int device = 0;
@@ -34,7 +35,21 @@ struct acs_ctx {
   void* ws[WS_NSLOTS] = {};
   size_t ws_bytes[WS_NSLOTS] = {};
   int n_cu = 256;
+  // Instantiated hipGraphs kept across calls: `key` holds every value their kernels
+  // captured (dimensions, buffer pointers, options, stream), so a call with the same key
+  // replays the graph instead of capturing and instantiating it again.
+  struct GraphCache {
+    hipGraphExec_t exec = nullptr;
+    std::string key;
+  };
+  GraphCache graphs[GRAPH_NSLOTS];
 };
+
+// append the bytes of a trivially copyable value to a graph-cache key
+template <typename T>
+inline void key_put(std::string& k, const T& v) {
+  k.append(reinterpret_cast<const char*>(&v), sizeof(T));
+}
 
 int acs_fail(acs_ctx* ctx, int code, const char* fmt, ...);
 

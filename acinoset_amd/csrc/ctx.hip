@@ -102,6 +102,8 @@ int acs_ctx_destroy(acs_ctx* ctx) {
   if (!ctx) return ACS_OK;
   ACS_DEVICE_GUARD(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto& g : ctx->graphs)
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
   for (int i = 0; i < WS_NSLOTS; ++i)
     if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);

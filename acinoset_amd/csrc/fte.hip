@@ -486,6 +486,85 @@ static size_t lin_lds_bytes(const FteDims& d) {
 // ---------------------------------------------------------------------------------------
 // 2. assembly of the banded normal matrix (row f: blocks (f, f-d), d = 0..3)
 // ---------------------------------------------------------------------------------------
+// Row f: A = blocks (f, f-dd), dd = 0..3 (4 P x P), g (P) and the tau border B (P x Cg),
+// from the local blocks of frames f-2 (own rows), f-1 (prev) and f (prev2) that are owned
+// (lo <= k < hi), plus the exact third-difference model term of the stencils starting in
+// [lo, hi). Threads t < nth of the calling group work; every thread of the workgroup must
+// call it (it holds barriers). Fixed accumulation order (own, prev, prev2, model).
+__device__ void assemble_row(const FteDims& d, int f, const double* __restrict__ X, const double* __restrict__ qinv,
+                             int lo, int hi, const double* __restrict__ Hloc, const double* __restrict__ gloc,
+                             double* A, double* g, double* B, int t, int nth) {
+  const int P = d.P, Cg = d.Cg, N = d.N;
+  for (int i = t; i < 4 * P * P; i += nth) A[i] = 0.0;
+  for (int i = t; i < P * Cg; i += nth) B[i] = 0.0;
+  for (int i = t; i < P; i += nth) g[i] = 0.0;
+  const int kown = f - 2, kprev = f - 1, kprev2 = f;
+  auto owned = [&](int k) { return k >= 0 && k < N && k >= lo && k < hi; };
+  __syncthreads();
+  if (owned(kown)) {
+    const double* H = Hloc + (size_t)kown * FTE_NZP * FTE_NZP;
+    for (int i = t; i < P * P; i += nth) {
+      const int r = i / P, c = i % P;
+      A[r * P + c] += H[r * FTE_NZP + c];
+    }
+    for (int i = t; i < P * 3; i += nth) {
+      const int r = i / 3, c = i % 3;
+      A[1 * P * P + r * P + c] += H[r * FTE_NZP + P + c];
+      A[2 * P * P + r * P + c] += H[r * FTE_NZP + P + 3 + c];
+    }
+    for (int i = t; i < P * Cg; i += nth) {
+      const int r = i / Cg, c = i % Cg;
+      B[r * Cg + c] += H[r * FTE_NZP + P + 6 + c];
+    }
+    for (int i = t; i < P; i += nth) g[i] += gloc[(size_t)kown * FTE_NZP + i];
+  }
+  __syncthreads();
+  if (owned(kprev)) {
+    const double* H = Hloc + (size_t)kprev * FTE_NZP * FTE_NZP;
+    for (int i = t; i < 9; i += nth) {
+      const int r = i / 3, c = i % 3;
+      A[r * P + c] += H[(P + r) * FTE_NZP + P + c];
+      A[1 * P * P + r * P + c] += H[(P + r) * FTE_NZP + P + 3 + c];
+    }
+    for (int i = t; i < 3 * Cg; i += nth) {
+      const int r = i / Cg, c = i % Cg;
+      B[r * Cg + c] += H[(P + r) * FTE_NZP + P + 6 + c];
+    }
+    for (int i = t; i < 3; i += nth) g[i] += gloc[(size_t)kprev * FTE_NZP + P + i];
+  }
+  __syncthreads();
+  if (owned(kprev2)) {
+    const double* H = Hloc + (size_t)kprev2 * FTE_NZP * FTE_NZP;
+    for (int i = t; i < 9; i += nth) {
+      const int r = i / 3, c = i % 3;
+      A[r * P + c] += H[(P + 3 + r) * FTE_NZP + P + 3 + c];
+    }
+    for (int i = t; i < 3 * Cg; i += nth) {
+      const int r = i / Cg, c = i % Cg;
+      B[r * Cg + c] += H[(P + 3 + r) * FTE_NZP + P + 6 + c];
+    }
+    for (int i = t; i < 3; i += nth) g[i] += gloc[(size_t)kprev2 * FTE_NZP + P + 3 + i];
+  }
+  __syncthreads();
+  // model term: stencils m in [3, M-1], s_m = (X_m - 3X_{m-1} + 3X_{m-2} - X_{m-3}) / Ts^2
+  const double cf[4] = {1.0, -3.0, 3.0, -1.0};
+  const double its2 = 1.0 / (d.Ts * d.Ts);
+  for (int p = t; p < P; p += nth) {
+    double gm = 0.0;
+    double hd[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = 0; i < 4; ++i) {
+      const int m = f + i;
+      if (m < 3 || m > d.M - 1 || m - 3 < lo || m - 3 >= hi) continue;
+      const double sm = (X[m * P + p] - 3.0 * X[(m - 1) * P + p] + 3.0 * X[(m - 2) * P + p] - X[(m - 3) * P + p]) * its2;
+      gm += 2.0 * qinv[p] * cf[i] * its2 * sm;
+      for (int dd = 0; dd < 4 && i + dd < 4; ++dd) hd[dd] += 2.0 * qinv[p] * cf[i] * cf[i + dd] * its2 * its2;
+    }
+    g[p] += gm;
+    for (int dd = 0; dd < 4; ++dd) A[dd * P * P + p * P + p] += hd[dd];
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* __restrict__ Xbuf,
                                                       const double* __restrict__ taubuf,
                                                       const double* __restrict__ qinv,
@@ -502,6 +581,7 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
   // iteration (the damping changes): block (f, f') -= sum_c h_c h_c'^T / T_c and
   // g_f -= sum_c h_c g_c / T_c over the frames touching row f, T_c = H_cc + lam max(H_cc,
   // 1e-12) (oracle damping), held delays skipped; Adiag keeps the raw diagonal for k_cr_build.
+  // (The single-GPU const / no-delay solve assembles inside k_cr_assemble_build instead.)
   const bool elim = d.var && !force;
   if (!force && (st->status != 0 || (!st->relin && !elim))) return;
   if (hsel) {  // the linearisation of X[cur] (double-buffered by the speculative solve)
@@ -518,11 +598,8 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
   double* B = Bt + (size_t)f * P * Cg;
   __shared__ double s_red[256];
   __shared__ double s_ti[3][FTE_MAXC], s_tg[3][FTE_MAXC];
-  for (int i = tid; i < 4 * P * P; i += nth) A[i] = 0.0;
-  for (int i = tid; i < P * Cg; i += nth) B[i] = 0.0;
-  for (int i = tid; i < P; i += nth) g[i] = 0.0;
-  const int kown = f - 2, kprev = f - 1, kprev2 = f;
   auto owned = [&](int k) { return k >= 0 && k < N && k >= lo && k < hi; };
+  const int kown = f - 2, kprev = f - 1, kprev2 = f;
   if (d.var && tid < 3 * C) {
     // j = 0, 1, 2: frames kown, kprev, kprev2
     const int j = tid / C, c = tid - j * C, k = f - 2 + j;
@@ -541,69 +618,7 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
     s_ti[j][c] = ti;
     s_tg[j][c] = tg;
   }
-  __syncthreads();
-  if (owned(kown)) {
-    const double* H = Hloc + (size_t)kown * FTE_NZP * FTE_NZP;
-    for (int i = tid; i < P * P; i += nth) {
-      const int r = i / P, c = i % P;
-      A[r * P + c] += H[r * FTE_NZP + c];
-    }
-    for (int i = tid; i < P * 3; i += nth) {
-      const int r = i / 3, c = i % 3;
-      A[1 * P * P + r * P + c] += H[r * FTE_NZP + P + c];
-      A[2 * P * P + r * P + c] += H[r * FTE_NZP + P + 3 + c];
-    }
-    for (int i = tid; i < P * Cg; i += nth) {
-      const int r = i / Cg, c = i % Cg;
-      B[r * Cg + c] += H[r * FTE_NZP + P + 6 + c];
-    }
-    for (int i = tid; i < P; i += nth) g[i] += gloc[(size_t)kown * FTE_NZP + i];
-  }
-  __syncthreads();
-  if (owned(kprev)) {
-    const double* H = Hloc + (size_t)kprev * FTE_NZP * FTE_NZP;
-    for (int i = tid; i < 9; i += nth) {
-      const int r = i / 3, c = i % 3;
-      A[r * P + c] += H[(P + r) * FTE_NZP + P + c];
-      A[1 * P * P + r * P + c] += H[(P + r) * FTE_NZP + P + 3 + c];
-    }
-    for (int i = tid; i < 3 * Cg; i += nth) {
-      const int r = i / Cg, c = i % Cg;
-      B[r * Cg + c] += H[(P + r) * FTE_NZP + P + 6 + c];
-    }
-    for (int i = tid; i < 3; i += nth) g[i] += gloc[(size_t)kprev * FTE_NZP + P + i];
-  }
-  __syncthreads();
-  if (owned(kprev2)) {
-    const double* H = Hloc + (size_t)kprev2 * FTE_NZP * FTE_NZP;
-    for (int i = tid; i < 9; i += nth) {
-      const int r = i / 3, c = i % 3;
-      A[r * P + c] += H[(P + 3 + r) * FTE_NZP + P + 3 + c];
-    }
-    for (int i = tid; i < 3 * Cg; i += nth) {
-      const int r = i / Cg, c = i % Cg;
-      B[r * Cg + c] += H[(P + 3 + r) * FTE_NZP + P + 6 + c];
-    }
-    for (int i = tid; i < 3; i += nth) g[i] += gloc[(size_t)kprev2 * FTE_NZP + P + 3 + i];
-  }
-  __syncthreads();
-  // model term: stencils m in [3, M-1], s_m = (X_m - 3X_{m-1} + 3X_{m-2} - X_{m-3}) / Ts^2
-  const double cf[4] = {1.0, -3.0, 3.0, -1.0};
-  const double its2 = 1.0 / (d.Ts * d.Ts);
-  for (int p = tid; p < P; p += nth) {
-    double gm = 0.0;
-    double hd[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int i = 0; i < 4; ++i) {
-      const int m = f + i;
-      if (m < 3 || m > d.M - 1 || m - 3 < lo || m - 3 >= hi) continue;
-      const double sm = (X[m * P + p] - 3.0 * X[(m - 1) * P + p] + 3.0 * X[(m - 2) * P + p] - X[(m - 3) * P + p]) * its2;
-      gm += 2.0 * qinv[p] * cf[i] * its2 * sm;
-      for (int dd = 0; dd < 4 && i + dd < 4; ++dd) hd[dd] += 2.0 * qinv[p] * cf[i] * cf[i + dd] * its2 * its2;
-    }
-    g[p] += gm;
-    for (int dd = 0; dd < 4; ++dd) A[dd * P * P + p * P + p] += hd[dd];
-  }
-  __syncthreads();
+  assemble_row(d, f, X, qinv, lo, hi, Hloc, gloc, A, g, B, tid, nth);
   double mx = 0.0;
   for (int i = tid; i < P; i += nth) mx = fmax(mx, fabs(g[i]));
   if (d.var)
@@ -780,6 +795,101 @@ __global__ __launch_bounds__(1024) void k_cr_build(FteDims d, const FteState* __
     }
     G[e] = v;
   }
+}
+
+// k_fte_assemble + k_cr_build in one pass for the single-GPU solve without per-frame delays
+// (d.var == 0): super-block i assembles its three banded rows f = 3i + a (one group of 320
+// threads per row) into LDS and builds D_i, E_i, GB_i from there, so the banded rows never
+// make an HBM round trip. Same arithmetic and order as the two kernels, so the same bits.
+// Runs every iteration (the damping changes on a rejected step; the rows are then
+// re-assembled from the unchanged linearisation).
+template <int NB>
+__global__ __launch_bounds__(1024) void k_cr_assemble_build(FteDims d, const double* __restrict__ Xbuf,
+                                                            const double* __restrict__ qinv,
+                                                            const FteState* __restrict__ st,
+                                                            const double* __restrict__ Hloc,
+                                                            const double* __restrict__ gloc, double* __restrict__ Dc,
+                                                            double* __restrict__ Ec, double* __restrict__ GBc,
+                                                            double* __restrict__ gmaxp) {
+  if (st->status != 0) return;
+  constexpr int BP = 16 * NB, NE = (BP * BP + 1023) / 1024;
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const int P = d.P, PP = P * P, GR = d.GR, Cg = d.Cg;
+  const int cur = st->cur;
+  Hloc += (size_t)cur * d.N * FTE_NZP * FTE_NZP;
+  gloc += (size_t)cur * d.N * FTE_NZP;
+  const double* X = Xbuf + (size_t)cur * d.M * P;
+  const double lam = st->lam;
+  extern __shared__ double lds[];
+  const int rowsz = 4 * PP + P + P * Cg;  // per row: A (4 P x P), g (P), B (P x Cg)
+  auto rowA = [&](int a) { return lds + (size_t)a * rowsz; };
+  auto rowg = [&](int a) { return lds + (size_t)a * rowsz + 4 * PP; };
+  auto rowB = [&](int a) { return lds + (size_t)a * rowsz + 4 * PP + P; };
+  __shared__ int s_a[BP], s_p[BP];
+  if (tid < BP) {
+    s_a[tid] = tid / P;
+    s_p[tid] = tid - (tid / P) * P;
+  }
+  {
+    const int grp = tid / 320, a = grp < 3 ? grp : 0;
+    const int f = 3 * i + a;
+    const bool act = grp < 3 && f < d.M;
+    // inactive threads (the 64 spare ones, rows past the sequence) start past every loop
+    assemble_row(d, f, X, qinv, 0, INT_MAX, Hloc, gloc, rowA(a), rowg(a), rowB(a), act ? tid - 320 * grp : 1 << 30,
+                 320);
+  }
+  // |g| max of each row (max is order-free): wave a < 3 takes row 3i + a
+  if (tid < 192) {
+    const int a = tid >> 6, lane = tid & 63, f = 3 * i + a;
+    double mx = 0.0;
+    for (int p = lane; p < P; p += 64) mx = fmax(mx, fabs(rowg(a)[p]));
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+    if (lane == 0 && f < d.M) gmaxp[f] = mx;
+  }
+  double* D = Dc + (size_t)i * BP * BP;
+  double* E = Ec + (size_t)i * BP * BP;
+  double* G = GBc + (size_t)i * BP * GR;
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int e = tid + 1024 * q;
+    if (e >= BP * BP) continue;
+    const int r = e / BP, c = e - (e / BP) * BP;
+    const int ar = s_a[r], pr = s_p[r], ac = s_a[c], pc = s_p[c];
+    const int fr = 3 * i + ar, fc = 3 * i + ac;
+    const bool rin = r < 3 * P && fr < d.M, cin = c < 3 * P && fc < d.M;
+    double dv = 0.0, ev = 0.0;
+    if (rin && cin) {
+      double v = (ar >= ac) ? rowA(ar)[(ar - ac) * PP + pr * P + pc] : rowA(ac)[(ac - ar) * PP + pc * P + pr];
+      if (r == c) v += lam * fmax(v, 1e-12);
+      dv = v;
+    } else if (r == c) {
+      dv = 1.0;  // padding: identity
+    }
+    // E_i = T(block i, block i-1): frames 3i+ar vs 3(i-1)+ac, distance 3 + ar - ac <= 3
+    const int fe = 3 * (i - 1) + ac;
+    if (i > 0 && rin && c < 3 * P && fe < d.M) {
+      const int dist = 3 + ar - ac;
+      if (dist <= 3) ev = rowA(ar)[dist * PP + pr * P + pc];
+    }
+    D[e] = dv;
+    E[e] = ev;
+  }
+  for (int e = tid; e < BP * GR; e += blockDim.x) {
+    const int r = e / GR, c = e - (e / GR) * GR;
+    const int pr = s_p[r], ar = s_a[r], fr = 3 * i + ar;
+    double v = 0.0;
+    if (r < 3 * P && fr < d.M) {
+      if (c < Cg)
+        v = rowB(ar)[pr * Cg + c];
+      else if (c == Cg)
+        v = -rowg(ar)[pr];
+    }
+    G[e] = v;
+  }
+}
+
+static size_t asm_build_lds_bytes(const FteDims& d) {
+  return sizeof(double) * 3 * (size_t)(4 * d.P * d.P + d.P + d.P * d.Cg);
 }
 
 static void cr_launch_build(const FteDims& d, hipStream_t s, int nblk, const FteState* st, const double* Ab,
@@ -1878,6 +1988,21 @@ static void cr_launch_top(const FteDims& d, hipStream_t s, int nlev, int a0, int
 #undef CR_TOP
 }
 
+static void cr_launch_assemble_build(const FteDims& d, hipStream_t s, const FteBuffers& b) {
+#define CR_ABUILD(nb)                                                                                          \
+  hipLaunchKernelGGL((k_cr_assemble_build<nb>), dim3(d.nblk), dim3(1024), asm_build_lds_bytes(d), s, d, b.X, \
+                     b.qinv, b.st, b.Hloc, b.gloc, b.Dc, b.Ec, b.GBc, b.gmaxp)
+  switch (d.BP >> 4) {
+    case 1: CR_ABUILD(1); break;
+    case 2: CR_ABUILD(2); break;
+    case 3: CR_ABUILD(3); break;
+    case 4: CR_ABUILD(4); break;
+    case 5: CR_ABUILD(5); break;
+    default: CR_ABUILD(6); break;
+  }
+#undef CR_ABUILD
+}
+
 static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
@@ -1893,11 +2018,15 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
   // the linearisation of X[cur] is already there (initial, or speculative at the last
-  // accepted trial): assemble the banded rows when it is new (or when the variable delays
-  // must be re-eliminated for a new damping)
-  hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, 0, 0, 0, INT_MAX,
-                     b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1);
-  cr_launch_build(d, s, d.nblk, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, 0, -1, -1, d.var ? b.Adiag : nullptr);
+  // accepted trial): assemble the banded rows and build the damped super-blocks (variable
+  // delays: assembled when new or re-eliminated for a new damping, then built)
+  if (d.var) {
+    hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, 0, 0, 0, INT_MAX,
+                       b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1);
+    cr_launch_build(d, s, d.nblk, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, 0, -1, -1, b.Adiag);
+  } else {
+    cr_launch_assemble_build(d, s, b);
+  }
   const int bend = d.nblk - 1;
   int sym = 0;
   cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad, false, &sym);
@@ -2211,23 +2340,42 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
                        b.X, b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr);
   ACS_HIP(ctx, hipGetLastError());
   // capture `chunk` iterations into one hipGraph (kernels read the LM state from device
-  // memory, so the graph is static); replay until the device reports a stop status
+  // memory, so the graph is static); replay until the device reports a stop status. The
+  // instantiated graph stays in the context for the next solve with the same key.
   const int chunk = 4;
-  hipGraph_t graph = nullptr;
+  std::string key;
+  key_put(key, d);
+  key_put(key, b);
+  key_put(key, o.max_iters);
+  key_put(key, o.ftol);
+  key_put(key, o.xtol);
+  key_put(key, o.gtol);
+  key_put(key, s);
+  key_put(key, chunk);
+  acs_ctx::GraphCache& gc = ctx->graphs[GRAPH_FTE];
   hipGraphExec_t exec = nullptr;
   bool use_graph = op.max_iters > 0;
-  if (use_graph) {
+  if (use_graph && gc.exec && gc.key == key) {
+    exec = gc.exec;
+  } else if (use_graph) {
+    if (gc.exec) (void)hipGraphExecDestroy(gc.exec);
+    gc.exec = nullptr;
+    gc.key.clear();
+    hipGraph_t graph = nullptr;
     if (hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) != hipSuccess) use_graph = false;
-  }
-  if (use_graph) {
-    for (int c = 0; c < chunk; ++c) fte_enqueue_iteration(S, s, o);
-    if (hipStreamEndCapture(s, &graph) != hipSuccess || hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) !=
-                                                            hipSuccess) {
+    if (use_graph) {
+      for (int c = 0; c < chunk; ++c) fte_enqueue_iteration(S, s, o);
+      if (hipStreamEndCapture(s, &graph) != hipSuccess ||
+          hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        exec = nullptr;
+        use_graph = false;
+      }
       if (graph) (void)hipGraphDestroy(graph);
-      (void)hipGetLastError();
-      graph = nullptr;
-      exec = nullptr;
-      use_graph = false;
+    }
+    if (exec) {
+      gc.exec = exec;
+      gc.key = key;
     }
   }
   FteState hs;
@@ -2243,8 +2391,6 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
     ACS_HIP(ctx, hipStreamSynchronize(s));
     if (hs.status != 0) break;
   }
-  if (exec) (void)hipGraphExecDestroy(exec);
-  if (graph) (void)hipGraphDestroy(graph);
   if (op.max_iters == 0) {
     ACS_HIP(ctx, hipMemcpyAsync(&hs, b.st, sizeof(hs), hipMemcpyDeviceToHost, s));
     ACS_HIP(ctx, hipStreamSynchronize(s));
