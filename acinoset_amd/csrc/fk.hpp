@@ -106,8 +106,14 @@ __device__ __forceinline__ void mat3_mul(const double* A, const double* B, doubl
 // __syncthreads() before reading sh (positions / M / om). Positions exclude any
 // shutter-delay shift (callers add it). F32_TRIG: cos / sin in float32 of the float32
 // angle (the reference EKF's numerics, src/core/ekf.py:79 + misc.py:381-420).
+// FK_MARK(slot): phase marks of thread 0 of block 0 (a profiling build defines it)
+#ifndef FK_MARK
+#define FK_MARK(slot)
+#define FK_MARK_T0
+#endif
 template <bool F32_TRIG = false>
 __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int tid, int nth) {
+  FK_MARK_T0
   for (int p = tid; p < s.P; p += nth) {
     double v = x[p];
     sh.xp[p] = v;
@@ -120,22 +126,28 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
       sincos(v, &sh.sn[p], &sh.cs[p]);
     }
   }
-  if (tid < 2) {  // translation parameters, summed once per frame instead of once per node chain
-    const int kind = tid == 0 ? PK_TRANS : PK_WORLD;
+  FK_MARK(24);
+  __syncthreads();
+  FK_MARK(25);
+  // translation parameters, summed once per frame instead of once per node chain, from the
+  // LDS copy (a loop of global loads here was a chain of cache round trips) by the last two
+  // threads, which the joint loop below leaves idle when nth >= J + 2
+  if (tid >= nth - 2) {
+    const int kind = tid == nth - 2 ? PK_TRANS : PK_WORLD;
     double t[3] = {0.0, 0.0, 0.0};
     for (int q = 0; q < s.P; ++q)
       if (s.pk[4 * q] == kind) {
         const int a = s.pk[4 * q + 1];
-        t[0] += a == 0 ? x[q] : 0.0;
-        t[1] += a == 1 ? x[q] : 0.0;
-        t[2] += a == 2 ? x[q] : 0.0;
+        const double v = sh.xp[q];
+        t[0] += a == 0 ? v : 0.0;
+        t[1] += a == 1 ? v : 0.0;
+        t[2] += a == 2 ? v : 0.0;
       }
-    double* dst = tid == 0 ? sh.root : sh.world;
+    double* dst = kind == PK_TRANS ? sh.root : sh.world;
     dst[0] = t[0];
     dst[1] = t[1];
     dst[2] = t[2];
   }
-  __syncthreads();
   for (int j = tid; j < s.J; j += nth) {
     const int* jt = s.joints + 8 * j;
     const int nrot = jt[1];
@@ -159,6 +171,7 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
 #pragma unroll
     for (int i = 0; i < 9; ++i) sh.G[j][i] = Gm[i];
   }
+  FK_MARK(26);
   __syncthreads();
   for (int j = tid; j < s.J; j += nth) {
     double Mm[9], T[9];
@@ -174,6 +187,7 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
 #pragma unroll
     for (int i = 0; i < 9; ++i) sh.M[j][i] = Mm[i];
   }
+  FK_MARK(27);
   __syncthreads();
   const int* pk = s.pk;
   for (int k = tid; k < s.K; k += nth) {
@@ -206,6 +220,7 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
     sh.pos[k][1] = p1;
     sh.pos[k][2] = p2;
   }
+  FK_MARK(28);
   for (int q = tid; q < s.P; q += nth) {
     if (pk[4 * q] != PK_ROT) {
       sh.om[q][0] = sh.om[q][1] = sh.om[q][2] = 0.0;

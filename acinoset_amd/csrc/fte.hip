@@ -26,6 +26,15 @@
 //   k_fte_lm         [1 block ]  fixed-order reduction, accept/reject, lambda, stop tests
 #include <climits>
 
+#ifdef FTE_PROFILE
+__device__ unsigned long long g_fte_prof[64];  // wall-clock ticks (100 MHz) of block 0 phases
+// fk_frame phase marks (slots 24..28): thread 0 of block 0, time since fk_frame started
+#define FK_MARK_T0 const unsigned long long fk_t0 = wall_clock64();
+#define FK_MARK(slot)                                                                  \
+  do {                                                                                 \
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fte_prof[slot], wall_clock64() - fk_t0); \
+  } while (0)
+#endif
 #include "fk.hpp"
 #include "mfma64.hpp"
 
@@ -132,7 +141,6 @@ __device__ double block_max(double v, double* s_red) {
 // touches only the 9 + C shift / delay columns and is added when H is stored.
 // ---------------------------------------------------------------------------------------
 #ifdef FTE_PROFILE
-__device__ unsigned long long g_fte_prof[64];  // wall-clock ticks (100 MHz) of block 0 phases
 // k_fte_linearize phases (block 0, thread 0, after a barrier), slots 56..61
 #define LPROF(slot)                                                          \
   do {                                                                     \
@@ -234,6 +242,7 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   __shared__ double s_tabR[3 * FK_MAXN];
   LPROF_T0
   const SkelView s = skel_stage(I, Rl, s_tabI, s_tabR, tid, blockDim.x);
+  LPROF(61);
   const int f = k + 2;
   for (int i = tid; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
   for (int i = lo.am + tid; i < lo.cf; i += blockDim.x) lds[i] = 0.0;
@@ -242,6 +251,7 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
     s_dx[tid] = (x0 - x1) / d.Ts;
     s_ddx[tid] = (x0 - 2.0 * x1 + x2) / (d.Ts * d.Ts);
   }
+  LPROF(62);
   fk_frame(s, X + f * P, fk, tid, blockDim.x);
   __syncthreads();
   LPROF(56);

@@ -21,5 +21,10 @@ ctx.lib.acs_fte_prof_read(buf)
 n = max(buf[60], 1)
 v = np.array(buf[:], np.float64) * 10e-3 / n
 print(f'linearize launches {buf[60]}; block 0, mean us since kernel start:')
-for k, nm in [(56, 'FK done'), (57, 'observations + aggregation done'), (58, 'MFMA H done'), (59, 'store done')]:
+fk = [(24, 'sincos'), (25, 'barrier 1'), (26, 'joint rotations G'), (27, 'joint frames M (chains)'),
+      (28, 'node positions')]
+print('fk_frame (thread 0, block 0), mean us since fk_frame start:')
+for k, nm in fk:
+    print(f'  {nm:32s} {v[k]:8.2f}')
+for k, nm in [(61, 'skeleton table staged'), (62, 'cams / LDS init (FK start)'), (56, 'FK done'), (57, 'observations + aggregation done'), (58, 'MFMA H done'), (59, 'store done')]:
     print(f'{nm:34s} {v[k]:8.2f}')
