@@ -31,7 +31,10 @@ struct SbaParams {
   double f_scale, ftol, xtol, gtol;
 };
 
-template <int G, int S, bool CAMID>
+// HOIST: each lane keeps its camera record in registers for the whole LM loop instead of
+// re-reading it from LDS in every projection (188 VGPRs: 2 waves per SIMD), chosen for
+// grids of at most 2 waves per SIMD, where nothing else would fill the SIMD anyway.
+template <int G, int S, bool CAMID, bool HOIST>
 __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams, int C, int K,
                                                 const double2* __restrict__ uv,
                                                 const uint8_t* __restrict__ mask,
@@ -41,39 +44,57 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
                                                 double* __restrict__ cost0, double* __restrict__ cost1,
                                                 int* __restrict__ stat) {
   extern __shared__ double s_cam[];
-  for (int i = threadIdx.x; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
-  __syncthreads();
   const int lane = threadIdx.x & (G - 1);
   const int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
-  if (p >= n_pts) return;  // whole group leaves together
+  const bool live = p < n_pts;
+  // every global load is issued before the first wait: the slot's observation, its mask and
+  // camera id, and the point (none depends on another), then the camera records for LDS.
+  // One memory round trip instead of three before the LM loop starts.
+  double2 q[S];
+  uint8_t mk[S], cid[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int slot = lane + s * G;
+    q[s] = double2{0.0, 0.0};
+    mk[s] = 0;
+    cid[s] = (uint8_t)slot;
+    if (live && slot < K) {
+      const int64_t o = p * K + slot;
+      mk[s] = mask[o];
+      q[s] = uv[o];
+      if (CAMID) cid[s] = camid[o];
+    }
+  }
+  double x0 = 0.0, x1 = 0.0, x2 = 0.0;
+  if (live) {
+    x0 = pts_in[3 * p];
+    x1 = pts_in[3 * p + 1];
+    x2 = pts_in[3 * p + 2];
+  }
+  for (int i = threadIdx.x; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
+  __syncthreads();
+  if (!live) return;  // whole group leaves together
 
   double ou[S], ov[S];
+  double cr[HOIST ? S : 1][ACS_CAM_STRIDE];
   const double* oc[S];
   bool ok[S];
   int mine = 0;
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int slot = lane + s * G;
-    ok[s] = false;
-    ou[s] = ov[s] = 0.0;
-    oc[s] = s_cam;
-    if (slot < K) {
-      const int64_t o = p * K + slot;
-      if (mask[o]) {
-        const int cam = CAMID ? (int)camid[o] : slot;
-        if (cam < C) {
-          const double2 q = uv[o];
-          ou[s] = q.x;
-          ov[s] = q.y;
-          oc[s] = s_cam + cam * ACS_CAM_STRIDE;
-          ok[s] = true;
-          ++mine;
-        }
-      }
+    const int cam = cid[s];
+    ok[s] = slot < K && mk[s] && cam < C;
+    ou[s] = ok[s] ? q[s].x : 0.0;
+    ov[s] = ok[s] ? q[s].y : 0.0;
+    oc[s] = s_cam + (ok[s] ? cam : 0) * ACS_CAM_STRIDE;
+    if constexpr (HOIST) {
+#pragma unroll
+      for (int i = 0; i < ACS_CAM_STRIDE; ++i) cr[s][i] = oc[s][i];
     }
+    mine += ok[s] ? 1 : 0;
   }
   const double nobs = group_sum<G>((double)mine);
-  double x0 = pts_in[3 * p], x1 = pts_in[3 * p + 1], x2 = pts_in[3 * p + 2];
   if (nobs == 0.0) {
     if (lane == 0) {
       pts[3 * p] = x0;
@@ -102,7 +123,10 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     for (int s = 0; s < S; ++s) {
       if (!ok[s]) continue;
       ProjOut o;
-      fisheye_project<true>(oc[s], X0, X1, X2, o);
+      if constexpr (HOIST)
+        fisheye_project<true>(cr[s], X0, X1, X2, o);
+      else
+        fisheye_project<true>(oc[s], X0, X1, X2, o);
       const double r[2] = {o.u - ou[s], o.v - ov[s]};
       const double zu = r[0] * r[0] * if2, zv = r[1] * r[1] * if2;
       Fl += log1p_pos(zu + zv + zu * zv);  // log1p(zu) + log1p(zv) with one logarithm
@@ -350,7 +374,18 @@ template <int G, int S, bool CAMID>
 static void launch_lm_t(acs_ctx* ctx, int blocks, int block, const double* cams, int C, int K, const double2* uv,
                         const uint8_t* mask, const uint8_t* camid, int64_t n_pts, const double* pts_in, double* pts,
                         SbaParams prm, double* c0, double* c1, int* st) {
-  hipLaunchKernelGGL((k_sba_lm<G, S, CAMID>), dim3(blocks), dim3(block), sizeof(double) * ACS_CAM_STRIDE * C,
+  // register-resident camera records when the grid holds at most 2 waves per SIMD
+  const int64_t waves = (n_pts * G + 63) / 64;
+  const bool hoist = S == 1 && !CAMID && G <= 16 && waves <= 8 * (int64_t)ctx->n_cu;
+  if constexpr (S == 1 && !CAMID && G <= 16) {
+    if (hoist) {
+      hipLaunchKernelGGL((k_sba_lm<G, S, CAMID, true>), dim3(blocks), dim3(block),
+                         sizeof(double) * ACS_CAM_STRIDE * C, ctx->stream, cams, C, K, uv, mask, camid, n_pts, pts_in,
+                         pts, prm, c0, c1, st);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((k_sba_lm<G, S, CAMID, false>), dim3(blocks), dim3(block), sizeof(double) * ACS_CAM_STRIDE * C,
                      ctx->stream, cams, C, K, uv, mask, camid, n_pts, pts_in, pts, prm, c0, c1, st);
 }
 
