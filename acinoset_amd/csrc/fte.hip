@@ -1924,9 +1924,15 @@ static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int 
   // workgroups per eliminated block: enough column waves (16 - NB per workgroup), and more
   // of them when few blocks are left (the deep levels are latency-bound)
   const int need = (NBB + 16 - NB - 1) / (16 - NB);
-  // one column-block per workgroup while the grid still fits the 256 CUs in one wave of
-  // workgroups (one 1024-thread workgroup per CU: the LDS is full)
-  const int want = ne * NBB + ns <= 256 ? NBB : (ne <= 32 ? 4 : (ne <= 96 ? 2 : 1));
+  // the widest split whose grid still fits the 256 CUs in one wave of workgroups (one
+  // 1024-thread workgroup per CU: the LDS is full): one column-block per workgroup when
+  // possible, else 6 / 4 / 3 / 2 column-blocks' worth of workgroups per block
+  int want = 1;
+  for (int c : {NBB, 6, 4, 3, 2})
+    if (c <= NBB && ne * c + ns <= 256) {
+      want = c;
+      break;
+    }
   const int nsplit = std::min(std::max(need, want), NBB);
   const int nwg = ne * nsplit + ns;
   const size_t lds = sizeof(double) * (2 * (16 * 17 + 16 * (size_t)d.BP + 17 * (size_t)d.BP) + (size_t)d.BP * d.GR +
