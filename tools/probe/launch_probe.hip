@@ -65,6 +65,30 @@ int main() {
       for (int fk = 0; fk < 2; ++fk)
         printf("%-7s grid %5d %-6s: %.2f us per kernel (chain of %d)\n", graph ? "graph" : "stream", grid,
                fk ? "flag" : "empty", time_chain(graph, nk, grid, fk, flag, out, s), nk);
+  // one-kernel graph launched repeatedly (a cached graph per API call)
+  for (int grid : {1, 64}) {
+    hipGraph_t g1;
+    hipGraphExec_t e1;
+    hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed);
+    hipLaunchKernelGGL(k_flag, dim3(grid), dim3(256), 0, s, flag, out);
+    hipStreamEndCapture(s, &g1);
+    hipGraphInstantiate(&e1, g1, nullptr, nullptr, 0);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; ++rep) {
+      hipEventRecord(a, s);
+      for (int i = 0; i < nk; ++i) hipGraphLaunch(e1, s);
+      hipEventRecord(b, s);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      if (ms < best) best = ms;
+    }
+    printf("graph1  grid %5d flag  : %.2f us per launch of a one-kernel graph (%d launches)\n", grid,
+           best * 1e3f / nk, nk);
+  }
   hipMemset(flag, 1, sizeof(int));
   for (int grid : {1, 1000})
     printf("graph   grid %5d early-exit (flag set): %.2f us per kernel\n", grid,
