@@ -173,7 +173,11 @@ def main():
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                      'kernel': 'k_sba_lm', 'kernel_ms': kern_ms, 'kernel_ms_launches': ngrp * every,
                      'bytes_per_launch': bytes_launch,
-                     'traffic_source': pmc['source'] if pmc else None},
+                     'traffic_source': pmc['source'] if pmc else None,
+                     'note': f'latency-bound at this size: {int(n_pts * _group(C) // 64)} waves for '
+                             f'{4 * 256} SIMDs, each a chain of up to {rep["iters_max"]} dependent LM iterations '
+                             '(~1.25 us each, profiles/r02/sba_iters.log) after a 2.4 us stream-launch floor; '
+                             'sba_at_scale carries the throughput rooflines'},
         'convergence': {'status': rep['status_counts'], 'iters_max': rep['iters_max'],
                         'gn_steps_mean': iters_mean, 'cost_before': rep['cost_before'],
                         'cost_after': rep['cost_after'], 'pos_rms_vs_truth_m': pos_rms},
