@@ -184,7 +184,8 @@ def main():
     }
 
     if args.fte and world == 1:
-        out['fte'] = bench_fte(ctx, torch, stream, n_frames=args.fte_frames)
+        out['fte'] = bench_fte(ctx, torch, stream, n_frames=args.fte_frames,
+                               cpu_seconds=0.0 if args.no_cpu_baseline else args.cpu_seconds)
     if args.ekf_seqs > 0:
         out['ekf'] = bench_ekf(ctx, torch, args.ekf_seqs, args.ekf_frames, args.ekf_cams, world, rank)
         out['ekf_head'] = bench_ekf(ctx, torch, args.ekf_seqs, args.ekf_frames, args.ekf_cams, world, rank,
@@ -423,7 +424,30 @@ def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl',
             'exchange': 'none' if world == 1 else f'torch.distributed {exchange} all-reduce x3 per LM step'}
 
 
-def bench_fte(ctx, torch, stream, n_frames=1000, steps=5):
+def fte_cpu_baseline(seq, scene, meas, w, X0, seconds, max_frames=60):
+    """Oracle FTE (oracle/fte.py: numpy + scipy sparse direct solves, 1 core) on a bounded
+    sample: the first `max_frames` frames of the same sequence from the same start,
+    solved to the same LM stop; frames/s = frames / wall time (whole solves, repeated for
+    ~`seconds`)."""
+    from oracle import fte as ofte
+    n = min(max_frames, seq.N)
+    prob = ofte.Problem('default_nolure', meas[:n], w[:n], scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=True,
+                        intermode='vel')
+    t0 = time.perf_counter()
+    reps, iters = 0, 0
+    while True:
+        _, _, info = ofte.solve(prob, X0[:n + 2])
+        reps += 1
+        iters = info['iters']
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {'value': reps * n / dt, 'unit': 'frames/s', 'cores': 1, 'kind': 'port',
+            'sample': f'{reps} full solves of the first {n} frames of the same sequence ({iters} LM iterations, '
+                      f'oracle/fte.py, numpy float64 + scipy sparse LU), {dt:.1f} s'}
+
+
+def bench_fte(ctx, torch, stream, n_frames=1000, steps=5, cpu_seconds=0.0):
     """configs[2]: 6-cam x 1000-frame FTE (20 keypoints, P = 26, shutter delay 'const',
     interpolation 'vel' = the all_optimizations defaults, src/all_optimizations.py:127-136),
     from the reference initialisation (pairwise triangulation on the GPU + nose line fit)."""
@@ -492,6 +516,7 @@ def bench_fte(ctx, torch, stream, n_frames=1000, steps=5):
             'roofline': {'bound': 'fp64', 'achieved': tfs, 'peak': FP64_PEAK_TFS, 'unit': 'TFLOP/s',
                          'frac': tfs / FP64_PEAK_TFS, 'flop_per_frame_step': flop_frame,
                          'note': 'whole solve (all kernels), algorithmic flops of SURVEY.md 8(d)'},
+            **({'cpu_baseline': fte_cpu_baseline(seq, scene, meas, w, X0, cpu_seconds)} if cpu_seconds > 0 else {}),
             }
 
 
