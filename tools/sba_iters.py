@@ -1,4 +1,6 @@
-"""kernel time of the configs[1] SBA solve vs max_iters (per-iteration slope / fixed cost)."""
+"""Kernel time of the configs[1] SBA solve (acs_sba_points_dense_io, HIP events on the
+kernel stream) against the LM iteration cap: fixed cost and per-iteration slope.
+    python tools/sba_iters.py"""
 import ctypes, os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
 import numpy as np
