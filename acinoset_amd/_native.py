@@ -37,7 +37,8 @@ SYMBOLS = (
     'acs_fte_default_opts', 'acs_fte_solve', 'acs_fte_eval', 'acs_triangulate_pairs', 'acs_triangulate_dense',
     'acs_sba_ext_default_opts', 'acs_sba_extrinsics', 'acs_sba_points_dense_io',
     'acs_fte_dist_create', 'acs_fte_dist_init', 'acs_fte_dist_phase1', 'acs_fte_dist_phase2', 'acs_fte_dist_phase3',
-    'acs_fte_dist_phase4', 'acs_fte_dist_result', 'acs_fte_dist_destroy',
+    'acs_fte_dist_phase4', 'acs_fte_dist_gather', 'acs_fte_dist_scatter', 'acs_fte_dist_result',
+    'acs_fte_dist_destroy',
     'acs_sba_ext_dist_create', 'acs_sba_ext_dist_init', 'acs_sba_ext_dist_phase1', 'acs_sba_ext_dist_phase2',
     'acs_sba_ext_dist_phase3', 'acs_sba_ext_dist_result', 'acs_sba_ext_dist_destroy', 'acs_ekf_run',
 )
@@ -136,9 +137,11 @@ def _declare(lib):
                                           C.POINTER(FteOpts), i32, i32, C.POINTER(_P), C.POINTER(i64), u32]),
         'acs_fte_dist_init': (C.c_int, [_P, _P]),
         'acs_fte_dist_phase1': (C.c_int, [_P, _P]),
-        'acs_fte_dist_phase2': (C.c_int, [_P, _P, _P]),
-        'acs_fte_dist_phase3': (C.c_int, [_P, _P, _P]),
+        'acs_fte_dist_phase2': (C.c_int, [_P, _P]),
+        'acs_fte_dist_phase3': (C.c_int, [_P, _P]),
         'acs_fte_dist_phase4': (C.c_int, [_P, _P, i32, C.POINTER(i32)]),
+        'acs_fte_dist_gather': (C.c_int, [_P, _P]),
+        'acs_fte_dist_scatter': (C.c_int, [_P, _P]),
         'acs_fte_dist_result': (C.c_int, [_P, _P, _P, C.POINTER(FteReport), u32]),
         'acs_fte_dist_destroy': (C.c_int, [_P]),
         'acs_sba_ext_dist_create': (C.c_int, [_P, _P, i32, _P, _P, _P, i64, _P, i64, C.POINTER(SbaExtOpts), i32, i32,

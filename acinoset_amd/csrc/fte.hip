@@ -1546,17 +1546,19 @@ __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int 
 // trial state X + delta, tau + dtau (clipped), norm partials per super-block. Variable
 // shutter delay: block i back-substitutes the delays of frames 3i-2..3i (X rows 3i..3i+2),
 // dtau[k, c] = -(g_c + h_c^T dx_k) / T_c over the local unknowns of frame k.
+// Blocks b0 + blockIdx.x. The (replicated) const-mode delays are stepped by the first
+// workgroup; their norm terms count only where tau_norm (once over the ranks).
 __global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __restrict__ st,
                                                   const double* __restrict__ dcv, const double* __restrict__ dtau,
                                                   const double* __restrict__ Hloc, const double* __restrict__ gloc,
                                                   double* __restrict__ Xbuf, double* __restrict__ taubuf,
-                                                  double* __restrict__ normp, int hsel) {
+                                                  double* __restrict__ normp, int hsel, int b0, int tau_norm) {
   if (st->status != 0) return;
   if (hsel) {
     Hloc += (size_t)st->cur * d.N * FTE_NZP * FTE_NZP;
     gloc += (size_t)st->cur * d.N * FTE_NZP;
   }
-  const int i = blockIdx.x;
+  const int i = blockIdx.x + b0;
   const int P = d.P, BP = d.BP;
   __shared__ double s_red[256];
   const int cur = st->cur;
@@ -1572,14 +1574,16 @@ __global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __r
     dn += dv * dv;
     xn += x * x;
   }
-  if (i == 0 && d.Cg) {
+  if (blockIdx.x == 0 && d.Cg) {
     const double* tau = taubuf + cur * d.NT;
     double* taun = taubuf + (cur ^ 1) * d.NT;
     for (int c = threadIdx.x; c < d.C; c += blockDim.x) {
       const double dv = (c == 0) ? 0.0 : dtau[c];
       taun[c] = (c == 0) ? 0.0 : fmin(fmax(tau[c] + dv, -d.Ts), d.Ts);
-      dn += dv * dv;
-      xn += tau[c] * tau[c];
+      if (tau_norm) {
+        dn += dv * dv;
+        xn += tau[c] * tau[c];
+      }
     }
   }
   if (d.var) {
@@ -1611,7 +1615,7 @@ __global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __r
   }
   dn = block_sum(dn, s_red);
   xn = block_sum(xn, s_red);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && i < d.nblk) {
     normp[2 * i] = dn;
     normp[2 * i + 1] = xn;
   }
@@ -2057,7 +2061,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
     hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, d, st, 0, bend, b.st, b.Wc, b.dtau, b.dcv);
   }
   hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
-                     b.normp, 1);
+                     b.normp, 1, 0, 1);
   // speculative linearisation at the trial state: its measurement terms and the model terms
   // are the trial cost (no separate cost pass)
   hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
@@ -2100,7 +2104,7 @@ static DistLayout dist_layout(const FteDims& d, int R) {
   L.oGmax = L.oTau + nE;
   L.n1 = L.oGmax + R;
   L.n2 = (size_t)d.nblk * BP;
-  L.n3 = 2;
+  L.n3 = 4;
   return L;
 }
 
@@ -2208,31 +2212,56 @@ __global__ void k_dist_scatter(FteDims d, const FteState* __restrict__ st, int r
   }
 }
 
-// this rank's rows of the step: blocks [a0, bend) (the last rank also its end block)
-__global__ __launch_bounds__(256) void k_dist_delta_out(FteDims d, const FteState* __restrict__ st, int b_lo,
-                                                        int b_hi, const double* __restrict__ dcv,
-                                                        double* __restrict__ p2) {
-  if (st->status != 0) return;
-  const size_t n0 = (size_t)b_lo * d.BP, n1 = (size_t)b_hi * d.BP;
-  for (size_t e = n0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n1; e += (size_t)gridDim.x * blockDim.x)
-    p2[e] = dcv[e];
-}
-
+// p3 = (measurement cost, model cost, |step|^2, |X, tau|^2) of this rank's owned terms /
+// rows (frames [k0, k1), super-blocks [n0, n1) of the trial's norm partials)
 __global__ __launch_bounds__(256) void k_dist_cost_pack(const FteState* __restrict__ st, int which, int k0, int k1,
                                                         const double* __restrict__ Fm, const double* __restrict__ Fq,
+                                                        int n0, int n1, const double* __restrict__ normp,
                                                         double* __restrict__ p3) {
   if (which == 1 && st->status != 0) return;
   __shared__ double s_red[256];
-  double a = 0.0, b = 0.0;
+  double a = 0.0, b = 0.0, dn = 0.0, xn = 0.0;
   for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
     a += Fm[k];
     b += Fq[k];
   }
+  for (int w = n0 + threadIdx.x; w < n1; w += blockDim.x) {
+    dn += normp[2 * w];
+    xn += normp[2 * w + 1];
+  }
   a = block_sum(a, s_red);
   b = block_sum(b, s_red);
+  dn = block_sum(dn, s_red);
+  xn = block_sum(xn, s_red);
   if (threadIdx.x == 0) {
     p3[0] = a;
     p3[1] = b;
+    p3[2] = dn;
+    p3[3] = xn;
+  }
+}
+
+// X[cur] rows of super-blocks [b_lo, b_hi) in the block layout of the step (BP per block)
+__global__ __launch_bounds__(256) void k_dist_x_out(FteDims d, const FteState* __restrict__ st, int b_lo, int b_hi,
+                                                    const double* __restrict__ Xbuf, double* __restrict__ p2) {
+  const double* X = Xbuf + (size_t)st->cur * d.M * d.P;
+  const int P = d.P, BP = d.BP;
+  for (size_t e = (size_t)b_lo * BP + (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)b_hi * BP;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / BP), r = (int)(e % BP), f = 3 * i + r / P;
+    if (r < 3 * P && f < d.M) p2[e] = X[(size_t)f * P + r % P];
+  }
+}
+
+// every row of X[cur] from the gathered block layout
+__global__ __launch_bounds__(256) void k_dist_x_in(FteDims d, const FteState* __restrict__ st,
+                                                   const double* __restrict__ p2, double* __restrict__ Xbuf) {
+  double* X = Xbuf + (size_t)st->cur * d.M * d.P;
+  const int P = d.P, BP = d.BP;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)d.nblk * BP;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / BP), r = (int)(e % BP), f = 3 * i + r / P;
+    if (r < 3 * P && f < d.M) X[(size_t)f * P + r % P] = p2[e];
   }
 }
 
@@ -2252,13 +2281,7 @@ __global__ __launch_bounds__(256) void k_fte_lm_dist(FteDims d, FteState* __rest
     return;
   }
   if (st->status != 0) return;
-  double dn = 0.0, xn = 0.0;
-  for (int w = tid; w < d.nblk; w += blockDim.x) {
-    dn += normp[2 * w];
-    xn += normp[2 * w + 1];
-  }
-  dn = block_sum(dn, s_red);
-  xn = block_sum(xn, s_red);
+  const double dn = p3[2], xn = p3[3];  // step / state norms summed over the ranks' owned rows
   if (tid != 0) return;
   if (st->gmax <= o.gtol) {
     st->status = ACS_STATUS_GTOL;
@@ -2666,7 +2689,8 @@ int acs_fte_dist_init(acs_fte_dist* h, double* p3) {
   if (h->c_hi > h->c_lo)
     hipLaunchKernelGGL(k_fte_cost, dim3(h->c_hi - h->c_lo), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
                        b.tau, b.qinv, b.st, 0, h->c_lo, h->own_lo, h->own_hi, b.Fm, b.Fq);
-  hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 0, h->c_lo, h->c_hi, b.Fm, b.Fq, p3);
+  hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 0, h->c_lo, h->c_hi, b.Fm, b.Fq, 0, 0,
+                     (const double*)nullptr, p3);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }
@@ -2699,7 +2723,7 @@ int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
   return ACS_OK;
 }
 
-int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
+int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
@@ -2725,35 +2749,64 @@ int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2) {
     const int ne = (dr.nblk - st + 2 * st - 1) / (2 * st);
     hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, dr, st, 0, rb, b.st, r.Wc, b.dtau, r.dcv);
   }
-  // this chain: ends from the reduced solve, interior by back substitution
-  ACS_HIP(ctx, hipMemsetAsync(p2, 0, sizeof(double) * h->Lo.n2, s));
+  // this chain: ends from the reduced solve, interior by back substitution, then the trial
+  // rows of the whole chain (its end blocks are shared: both neighbours step them alike) and
+  // the replicated delays; the norm partials of the owned blocks go to phase 3's payload
   if (h->a0 < d.nblk) {
     hipLaunchKernelGGL(k_dist_scatter, dim3(1), dim3(128), 0, s, d, b.st, h->rank, h->a0, h->bend, r.dcv, b.dcv);
     for (int lv = h->klev - 1; lv >= 0; --lv) {
       const int st = 1 << lv;
       int ne = 0;
       for (int i = h->a0 + st; i < std::min(h->bend, d.nblk); i += 2 * st) ++ne;
-      if (ne) hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, d, st, h->a0, h->bend, b.st, b.Wc, b.dtau, b.dcv);
+      if (ne)
+        hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, d, st, h->a0, h->bend, b.st, b.Wc, b.dtau, b.dcv);
     }
-    if (h->out_hi > h->out_lo)
-      hipLaunchKernelGGL(k_dist_delta_out, dim3(64), dim3(256), 0, s, d, b.st, h->out_lo, h->out_hi, b.dcv, p2);
+    const int top = std::min(h->bend, d.nblk - 1);
+    hipLaunchKernelGGL(k_cr_trial, dim3(top - h->a0 + 1), dim3(256), 0, s, d, b.st, (const double*)b.dcv, b.dtau,
+                       b.Hloc, b.gloc, b.X, b.tau, b.normp, 0, h->a0, h->rank == 0 ? 1 : 0);
+  } else {
+    // a rank past the last block still steps the replicated delays
+    hipLaunchKernelGGL(k_cr_trial, dim3(1), dim3(256), 0, s, d, b.st, (const double*)b.dcv, b.dtau, b.Hloc, b.gloc,
+                       b.X, b.tau, b.normp, 0, d.nblk, h->rank == 0 ? 1 : 0);
   }
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }
 
-int acs_fte_dist_phase3(acs_fte_dist* h, const double* p2, double* p3) {
+int acs_fte_dist_phase3(acs_fte_dist* h, double* p3) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
   hipStream_t s = ctx->stream;
-  hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, p2, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
-                     b.normp, 0);
   if (h->c_hi > h->c_lo)
     hipLaunchKernelGGL(k_fte_cost, dim3(h->c_hi - h->c_lo), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
                        b.tau, b.qinv, b.st, 1, h->c_lo, h->own_lo, h->own_hi, b.Fm, b.Fq);
-  hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 1, h->c_lo, h->c_hi, b.Fm, b.Fq, p3);
+  hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 1, h->c_lo, h->c_hi, b.Fm, b.Fq, h->out_lo,
+                     h->out_hi, b.normp, p3);
+  ACS_HIP(ctx, hipGetLastError());
+  return ACS_OK;
+}
+
+int acs_fte_dist_gather(acs_fte_dist* h, double* p2) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
+  acs_ctx* ctx = h->ctx;
+  const FteDims& d = h->S.d;
+  FteBuffers& b = h->S.b;
+  hipStream_t s = ctx->stream;
+  ACS_HIP(ctx, hipMemsetAsync(p2, 0, sizeof(double) * h->Lo.n2, s));
+  if (h->out_hi > h->out_lo)
+    hipLaunchKernelGGL(k_dist_x_out, dim3(64), dim3(256), 0, s, d, b.st, h->out_lo, h->out_hi, (const double*)b.X, p2);
+  ACS_HIP(ctx, hipGetLastError());
+  return ACS_OK;
+}
+
+int acs_fte_dist_scatter(acs_fte_dist* h, const double* p2) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
+  acs_ctx* ctx = h->ctx;
+  const FteDims& d = h->S.d;
+  FteBuffers& b = h->S.b;
+  hipLaunchKernelGGL(k_dist_x_in, dim3(64), dim3(256), 0, ctx->stream, d, b.st, p2, b.X);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }

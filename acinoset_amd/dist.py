@@ -5,15 +5,16 @@ Frame-window FTE:
 
 One process per GPU (torchrun); ranks split the trajectory's 3-frame super-blocks into
 chains that share their end blocks (include/acinoset_hip.h, acs_fte_dist_*). Every LM
-iteration exchanges three sums over the ranks:
+iteration exchanges two sums over the ranks:
 
   p1  the chain ends' reduced normal-equation blocks + tau border (~1 MB at 8 ranks)
-  p2  the step (each rank fills its own rows)
-  p3  the costs of the owned terms (2 doubles)
+  p3  the costs of the owned terms and the step / state norms of the owned rows (4 doubles)
 
 with `torch.distributed.all_reduce` (RCCL over xGMI on the "nccl" backend; gloo in the CPU
-tests). Every rank then runs the same reduced solve and the same accept/reject decision,
-so the state stays replicated without any broadcast.
+tests). Every rank then runs the same reduced solve, back-substitutes and steps its own
+chain (X lives on the chain only: the terms a rank owns never read other rows), and takes
+the same accept/reject decision. The solution rows (p2, n_blocks x BP) cross the ranks
+once, after the last iteration.
 
 `lm_loop` is the protocol, independent of the backend: the HIP ranks below, or the numpy
 restatement in oracle/fte_dist.py that the CPU tests plug in.
@@ -32,7 +33,9 @@ from . import _native
 def lm_loop(ranks, allreduce):
     """Drive the distributed LM. `ranks`: the backends living in this process (one per
     process under torch.distributed, several for the single-process emulation);
-    `allreduce(list_of_payloads)` sums the i-th payload over all ranks in place."""
+    `allreduce(list_of_payloads)` sums the i-th payload over all ranks in place.
+    Per LM iteration: the reduced system (p1) and 4 doubles (p3) cross the ranks; every
+    rank steps its own chain; the solution rows (p2) are exchanged once, at the end."""
     p3 = [r.init() for r in ranks]
     allreduce(p3)
     for r, p in zip(ranks, p3):
@@ -40,14 +43,19 @@ def lm_loop(ranks, allreduce):
     while True:
         p1 = [r.phase1() for r in ranks]
         allreduce(p1)
-        p2 = [r.phase2(a) for r, a in zip(ranks, p1)]
-        allreduce(p2)
-        p3 = [r.phase3(a) for r, a in zip(ranks, p2)]
+        for r, a in zip(ranks, p1):
+            r.phase2(a)
+        p3 = [r.phase3() for r in ranks]
         allreduce(p3)
         st = [r.phase4(a) for r, a in zip(ranks, p3)]
         assert len(set(st)) == 1, f'ranks diverged: {st}'
         if st[0] != 0:
-            return st[0]
+            break
+    p2 = [r.gather() for r in ranks]
+    allreduce(p2)
+    for r, a in zip(ranks, p2):
+        r.scatter(a)
+    return st[0]
 
 
 def lm_loop2(ranks, allreduce):
@@ -105,14 +113,18 @@ class HipFteRank:
         return self.p[0]
 
     def phase2(self, p1):
-        self.ctx.check(self.ctx.lib.acs_fte_dist_phase2(self.h, self._ptr(p1), self._ptr(self.p[1])),
-                       'acs_fte_dist_phase2')
+        self.ctx.check(self.ctx.lib.acs_fte_dist_phase2(self.h, self._ptr(p1)), 'acs_fte_dist_phase2')
+
+    def phase3(self):
+        self.ctx.check(self.ctx.lib.acs_fte_dist_phase3(self.h, self._ptr(self.p[2])), 'acs_fte_dist_phase3')
+        return self.p[2]
+
+    def gather(self):
+        self.ctx.check(self.ctx.lib.acs_fte_dist_gather(self.h, self._ptr(self.p[1])), 'acs_fte_dist_gather')
         return self.p[1]
 
-    def phase3(self, p2):
-        self.ctx.check(self.ctx.lib.acs_fte_dist_phase3(self.h, self._ptr(p2), self._ptr(self.p[2])),
-                       'acs_fte_dist_phase3')
-        return self.p[2]
+    def scatter(self, p2):
+        self.ctx.check(self.ctx.lib.acs_fte_dist_scatter(self.h, self._ptr(p2)), 'acs_fte_dist_scatter')
 
     def phase4(self, p3, init=False):
         st = C.c_int32(0)

@@ -185,17 +185,21 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
 
 /* ---- §8(e): frame-window distributed FTE (configs[3]) --------------------------------
  * One handle per rank (rank of world); every rank gets the full-size inputs of
- * acs_fte_solve and keeps the state replicated. The super-blocks of 3 frames are split
+ * acs_fte_solve. The super-blocks of 3 frames are split
  * into `world` chains that share their end blocks; a term belongs to the chain holding its
- * lowest row. One LM iteration:
- *   phase1(p1) -> all-reduce(p1, sum) -> phase2(p1, p2) -> all-reduce(p2, sum)
- *   -> phase3(p2, p3) -> all-reduce(p3, sum) -> phase4(p3, 0, &status)
- * starting with init(p3) -> all-reduce(p3) -> phase4(p3, 1, NULL). Payloads are DEVICE
- * buffers of payload_sizes[0..2] doubles (p1: chain-end blocks of the reduced system,
- * ~ (world+1) (2 BP^2 + BP GR) doubles; p2: the step, n_blocks x BP; p3: 2 costs). Every
- * rank runs the same reduced solve on the summed p1 and takes the same decisions; the
- * result equals acs_fte_solve up to summation order. Phases are asynchronous on the
- * context stream except phase4, which returns the LM status (0 = running).
+ * lowest row. X is kept only on the rank's own chain (its rows and both shared end blocks).
+ * One LM iteration, with ONE all-reduce of the reduced system and one of 4 doubles:
+ *   phase1(p1) -> all-reduce(p1, sum) -> phase2(p1) -> phase3(p3) -> all-reduce(p3, sum)
+ *   -> phase4(p3, 0, &status)
+ * starting with init(p3) -> all-reduce(p3) -> phase4(p3, 1, NULL), and after the last
+ * iteration gather(p2) -> all-reduce(p2) -> scatter(p2) before result(). Payloads are
+ * DEVICE buffers of payload_sizes[0..2] doubles (p1: chain-end blocks of the reduced
+ * system, ~ (world+1) (2 BP^2 + BP GR) doubles; p2: the solution rows, n_blocks x BP,
+ * exchanged once per solve; p3: 2 costs + step / state norms of the owned rows). Every
+ * rank runs the same reduced solve on the summed p1, back-substitutes and steps its own
+ * chain, and takes the same decisions; the result equals acs_fte_solve up to summation
+ * order. Phases are asynchronous on the context stream except phase4, which returns the
+ * LM status (0 = running).
  * shutter_delay with sd_mode 1 ('variable') is single-GPU only (ACS_E_INVALID here).   */
 typedef struct acs_fte_dist acs_fte_dist;
 int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
@@ -206,9 +210,11 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
                         acs_fte_dist** out, int64_t* payload_sizes, uint32_t flags);
 int acs_fte_dist_init(acs_fte_dist* h, double* p3);
 int acs_fte_dist_phase1(acs_fte_dist* h, double* p1);
-int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1, double* p2);
-int acs_fte_dist_phase3(acs_fte_dist* h, const double* p2, double* p3);
+int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1);
+int acs_fte_dist_phase3(acs_fte_dist* h, double* p3);
 int acs_fte_dist_phase4(acs_fte_dist* h, const double* p3, int32_t init, int32_t* status);
+int acs_fte_dist_gather(acs_fte_dist* h, double* p2);
+int acs_fte_dist_scatter(acs_fte_dist* h, const double* p2);
 int acs_fte_dist_result(acs_fte_dist* h, double* X, double* tau, acs_fte_report* report, uint32_t flags);
 int acs_fte_dist_destroy(acs_fte_dist* h);
 

@@ -16,10 +16,15 @@ monolithic oracle (oracle/fte.py solve):
   contributes the Schur complement on (chain-end rows, tau), their raw diagonals and
   gradients, and max |g| over its interior rows to payload 1 (a sum over ranks);
 * the summed reduced system is damped with the summed raw diagonals, tau_0 pinned, and
-  solved identically on every rank; interiors are back-substituted; payload 2 = the step
-  rows each rank publishes (blocks [a_r, a_r + 2^k), the last rank also its end);
-* payload 3 = the owned terms' (measurement, model) cost at the trial state; the
-  accept/reject rule is oracle/fte.py solve's.
+  solved identically on every rank; each rank back-substitutes its interior and steps its
+  own chain only (rows of the chain and its two end blocks; the terms it owns read no
+  others; the replicated delays on every rank);
+* payload 3 = the owned terms' (measurement, model) cost at the trial state and the
+  squared step / state norms of the owned rows (blocks [a_r, a_r + 2^k), the last rank
+  also its end; the delays counted on rank 0); the accept/reject rule is oracle/fte.py
+  solve's;
+* after the last iteration payload 2 = the owned rows of the solution (a sum over ranks
+  rebuilds X everywhere).
 
 The payload layouts are this module's own (dense); only their sums cross ranks.
 """
@@ -55,6 +60,7 @@ class OracleFteRank:
         var = lambda fs: np.array([f * P + q for f in fs for q in range(P)], np.int64)  # noqa: E731
         self.I = var(rows(a0 + 1, min(bend, nblk)))                      # interior unknowns
         ends = sorted(set(rows(a0, a0 + 1)) | set(rows(bend, bend + 1)))
+        self.chain = np.concatenate([var(ends), self.I]).astype(np.int64)  # rows this rank steps
         self.ntau = p.C if p.sd else 0
         tau_idx = np.arange(self.ntau) + M * P
         self.B = np.concatenate([var(ends), tau_idx]).astype(np.int64)  # border unknowns
@@ -70,7 +76,7 @@ class OracleFteRank:
         nS = len(self.S)
         self.n1 = nS * nS + 3 * nS + world
         self.n2 = M * P
-        self.n3 = 2
+        self.n3 = 4
 
     # ---- protocol ----------------------------------------------------------------------
     def init(self):
@@ -133,24 +139,21 @@ class OracleFteRank:
         if len(self.I):
             d[self.I] = np.linalg.solve(self.HII, -self.g[self.I] - self.HIB @ dS[self.Bpos])
         self.dtau = dS[nS - self.ntau:] if self.ntau else np.zeros(0)
-        out = np.zeros(self.n2)
-        out[self.out] = d[self.out]
-        return out
-
-    def phase3(self, p2):
-        p = self.prob
-        dX = p2.reshape(p.M, p.P)
-        self.Xn = self.X + dX
+        # the trial state on this chain (other rows are never read by the owned terms)
+        self.Xn = self.X.copy()
+        self.Xn.flat[self.chain] += d[self.chain]
         if p.sd:
             self.taun = np.clip(self.tau + self.dtau, -p.Ts, p.Ts)
             self.taun[0] = 0.0
         else:
             self.taun = self.tau
-        d = np.concatenate([p2, self.dtau])
-        self.dn = np.linalg.norm(d)
-        self.xn = np.linalg.norm(p.pack(self.X, self.tau))
-        _, fm, fq = p.cost(self.Xn, self.taun, self.frames, self.stencils)
-        return np.array([fm, fq])
+        own_tau = self.rank == 0
+        self.dn2 = float(np.sum(d[self.out] ** 2) + (np.sum(self.dtau ** 2) if own_tau else 0.0))
+        self.xn2 = float(np.sum(self.X.flat[self.out] ** 2) + (np.sum(self.tau ** 2) if own_tau and p.sd else 0.0))
+
+    def phase3(self):
+        _, fm, fq = self.prob.cost(self.Xn, self.taun, self.frames, self.stencils)
+        return np.array([fm, fq, self.dn2, self.xn2])
 
     def phase4(self, p3, init=False):
         o = self.opts
@@ -164,7 +167,8 @@ class OracleFteRank:
             self.status = 1
             return self.status
         self.iters += 1
-        small = self.dn <= o['xtol'] * (o['xtol'] + self.xn)
+        dn, xn = np.sqrt(p3[2]), np.sqrt(p3[3])
+        small = dn <= o['xtol'] * (o['xtol'] + xn)
         if Fn < self.F:
             fconv = (self.F - Fn) <= o['ftol'] * abs(self.F)
             self.nacc += 1
@@ -184,6 +188,14 @@ class OracleFteRank:
         if self.status == 0 and self.iters >= o['max_iters']:
             self.status = 5
         return self.status
+
+    def gather(self):
+        out = np.zeros(self.n2)
+        out[self.out] = self.X.flat[self.out]
+        return out
+
+    def scatter(self, p2):
+        self.X = np.array(p2, np.float64).reshape(self.prob.M, self.prob.P)
 
     def result(self):
         return self.X, self.tau, dict(status=self.status, iters=self.iters, n_accepted=self.nacc, cost_before=self.F0,
