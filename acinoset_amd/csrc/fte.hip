@@ -2324,7 +2324,49 @@ struct acs_fte_dist {
   FteOptsDev o;
   int R, rank, span, a0, bend, klev;
   int k_lo, k_hi, f_lo, f_hi, b_hi_build, c_lo, c_hi, own_lo, own_hi, out_lo, out_hi;
+  // phases 1-3 captured as hipGraphs on their first call (one graph launch instead of tens
+  // of kernel launches per phase); key = (payload pointer, stream)
+  struct Captured {
+    hipGraphExec_t exec = nullptr;
+    const void* ptr = nullptr;
+    hipStream_t stream = nullptr;
+  } g[3];
 };
+
+// Run `enqueue` (kernel launches on ctx->stream) through the phase's cached graph,
+// capturing it when the key changed; plain launches if capture is unavailable.
+template <typename F>
+static int dist_run_captured(acs_fte_dist* h, int which, const void* ptr, F enqueue) {
+  acs_ctx* ctx = h->ctx;
+  hipStream_t s = ctx->stream;
+  auto& c = h->g[which];
+  if (!c.exec || c.ptr != ptr || c.stream != s) {
+    if (c.exec) (void)hipGraphExecDestroy(c.exec);
+    c.exec = nullptr;
+    hipGraph_t graph = nullptr;
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) == hipSuccess) {
+      const int rc = enqueue();
+      const hipError_t e = hipStreamEndCapture(s, &graph);
+      if (rc) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc;
+      }
+      if (e == hipSuccess && graph && hipGraphInstantiate(&c.exec, graph, nullptr, nullptr, 0) == hipSuccess) {
+        c.ptr = ptr;
+        c.stream = s;
+      } else {
+        c.exec = nullptr;
+      }
+      if (graph) (void)hipGraphDestroy(graph);
+    }
+    if (!c.exec) {
+      (void)hipGetLastError();
+      return enqueue();
+    }
+  }
+  ACS_HIP(ctx, hipGraphLaunch(c.exec, s));
+  return ACS_OK;
+}
 
 static const double* dist_local_cr(acs_fte_dist* h) {
   const FteDims& d = h->S.d;
@@ -2673,6 +2715,8 @@ int acs_fte_dist_destroy(acs_fte_dist* h) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   if (!h) return ACS_OK;
   (void)hipStreamSynchronize(h->ctx->stream);
+  for (auto& c : h->g)
+    if (c.exec) (void)hipGraphExecDestroy(c.exec);
   if (h->own) (void)hipFree(h->own);
   if (h->own_red) (void)hipFree(h->own_red);
   delete h;
@@ -2695,7 +2739,7 @@ int acs_fte_dist_init(acs_fte_dist* h, double* p3) {
   return ACS_OK;
 }
 
-int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
+static int dist_phase1_body(acs_fte_dist* h, double* p1) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
@@ -2723,7 +2767,7 @@ int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
   return ACS_OK;
 }
 
-int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1) {
+static int dist_phase2_body(acs_fte_dist* h, const double* p1) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
@@ -2773,7 +2817,7 @@ int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1) {
   return ACS_OK;
 }
 
-int acs_fte_dist_phase3(acs_fte_dist* h, double* p3) {
+static int dist_phase3_body(acs_fte_dist* h, double* p3) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
@@ -2786,6 +2830,21 @@ int acs_fte_dist_phase3(acs_fte_dist* h, double* p3) {
                      h->out_hi, b.normp, p3);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
+}
+
+int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
+  return dist_run_captured(h, 0, p1, [&] { return dist_phase1_body(h, p1); });
+}
+
+int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
+  return dist_run_captured(h, 1, p1, [&] { return dist_phase2_body(h, p1); });
+}
+
+int acs_fte_dist_phase3(acs_fte_dist* h, double* p3) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
+  return dist_run_captured(h, 2, p3, [&] { return dist_phase3_body(h, p3); });
 }
 
 int acs_fte_dist_gather(acs_fte_dist* h, double* p2) {

@@ -80,23 +80,33 @@ class HipFteRank:
     tensors, so torch.distributed can reduce them in place)."""
 
     def __init__(self, ctx, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutter_delay=True, intermode=1,
-                 opts=None, rank=0, world=1):
+                 opts=None, rank=0, world=1, dev=None):
+        """`dev`: the inputs already resident in HBM, as torch device tensors
+        {'ints', 'reals', 'cams', 'meas', 'w', 'qinv', 'X', 'tau'} (copied device to device
+        into the handle; the host arrays are then only used for the shapes)."""
         import torch
         self.ctx = ctx
         self.torch = torch
-        ints, reals, cams, meas, w, qinv, N, Cn = ctx._fte_args(table, cams, meas, w, Ts, qinv, shutter_delay,
-                                                                intermode)
-        self.N, self.P, self.C = N, table.P, Cn
-        X = _native._c64(X0).reshape(N + 2, table.P)
-        tau = np.zeros(Cn) if tau0 is None else _native._c64(tau0)
         opts = opts or ctx.fte_default_opts()
         h = C.c_void_p()
         sizes = (C.c_int64 * 3)()
-        P_ = _native._ptr
-        ctx.check(ctx.lib.acs_fte_dist_create(ctx.h, P_(ints), len(ints), P_(reals), len(reals), P_(cams), Cn,
-                                              P_(meas), P_(w), N, int(bool(shutter_delay)), float(Ts), P_(qinv), 0,
-                                              int(intermode), P_(X), P_(tau), C.byref(opts), int(rank), int(world),
-                                              C.byref(h), sizes, 0), 'acs_fte_dist_create')
+        if dev is None:
+            ints, reals, cams, meas, w, qinv, N, Cn = ctx._fte_args(table, cams, meas, w, Ts, qinv, shutter_delay,
+                                                                    intermode)
+            X = _native._c64(X0).reshape(N + 2, table.P)
+            tau = np.zeros(Cn) if tau0 is None else _native._c64(tau0)
+            P_ = _native._ptr
+            ptrs = [P_(a) for a in (ints, reals, cams, meas, w, qinv, X, tau)]
+            n_ints, n_reals, flags = len(ints), len(reals), 0
+        else:
+            N, Cn = int(np.shape(meas)[0]), int(np.shape(meas)[1])
+            ptrs = [C.c_void_p(dev[k].data_ptr()) for k in ('ints', 'reals', 'cams', 'meas', 'w', 'qinv', 'X', 'tau')]
+            n_ints, n_reals, flags = dev['ints'].numel(), dev['reals'].numel(), _native.ACS_DEVICE_PTRS
+        self.N, self.P, self.C = N, table.P, Cn
+        ctx.check(ctx.lib.acs_fte_dist_create(ctx.h, ptrs[0], n_ints, ptrs[1], n_reals, ptrs[2], Cn, ptrs[3], ptrs[4], N,
+                                              int(bool(shutter_delay)), float(Ts), ptrs[5], 0, int(intermode), ptrs[6],
+                                              ptrs[7], C.byref(opts), int(rank), int(world), C.byref(h), sizes, flags),
+                  'acs_fte_dist_create')
         self.h = h
         dev = torch.device('cuda', ctx.device)
         self.p = [torch.zeros(int(n), dtype=torch.float64, device=dev) for n in sizes]

@@ -145,3 +145,30 @@ def test_sba_ext_dist_two_processes(ctx, tmp_path):
     assert np.array_equal(a['cams'], b['cams']) and np.array_equal(a['X'], b['X'])
     assert int(a['iters']) == r1['iters']
     np.testing.assert_allclose(a['X'], X1, rtol=0, atol=1e-9)
+
+
+def test_fte_dist_device_resident_inputs_match_host_inputs(ctx):
+    """HipFteRank with the inputs already in HBM (ACS_DEVICE_PTRS, copied device to device
+    into each rank) gives the solve of the host-input ranks, bit for bit."""
+    import torch
+    prob, cams, X0 = _problem(40)
+    table = pkin.build_table(prob.mode)
+    dv = torch.device('cuda', ctx.device)
+    T = lambda a, dt=torch.float64: torch.from_numpy(np.ascontiguousarray(a)).to(dv, dt)  # noqa: E731
+    dev = dict(ints=T(table.ints, torch.int32), reals=T(table.reals), cams=T(cams), meas=T(np.nan_to_num(prob.meas)),
+               w=T(prob.w), qinv=T(prob.qinv), X=T(X0), tau=torch.zeros(len(cams), dtype=torch.float64, device=dv))
+    outs = []
+    with dist._on_torch_stream(ctx):
+        for use_dev in (False, True):
+            ranks = [dist.HipFteRank(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, rank=r, world=2,
+                                     dev=dev if use_dev else None) for r in range(2)]
+            try:
+                dist.lm_loop(ranks, dist.local_allreduce)
+                outs.append(ranks[0].result())
+            finally:
+                for r in ranks:
+                    r.close()
+    (Xh, th, rh), (Xd, td, rd) = outs
+    assert rh['iters'] == rd['iters'] and rh['n_accepted'] == rd['n_accepted']
+    np.testing.assert_array_equal(Xd, Xh)
+    np.testing.assert_array_equal(td, th)
