@@ -286,3 +286,68 @@ __device__ __forceinline__ void fk_dpos(const SkelView& s, const FkShared& sh, i
     }
   }
 }
+
+// Per-parameter data of fk_dpos resolved once per frame (after fk_frame + a barrier), so
+// that a derivative needs no chain of dependent table lookups: typ 0 = constant vector
+// `vec` (translations: unit axis; neck length: M_frame e_x), 1 = rotation, d = om x (pos -
+// org). Same arithmetic as fk_dpos, so the same bits.
+struct FkDeriv {
+  int typ[FK_MAXP];
+  double vec[FK_MAXP][3];
+  double org[FK_MAXP][3];
+};
+
+__device__ __forceinline__ void fk_deriv_prep(const SkelView& s, const FkShared& sh, FkDeriv& dv, int q) {
+  const int* pk = s.pk + 4 * q;
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+  int typ = 0;
+  switch (pk[0]) {
+    case PK_TRANS:
+    case PK_WORLD:
+      v0 = pk[1] == 0 ? 1.0 : 0.0;
+      v1 = pk[1] == 1 ? 1.0 : 0.0;
+      v2 = pk[1] == 2 ? 1.0 : 0.0;
+      break;
+    case PK_LEN: {
+      const double* Mf = sh.M[s.nodes[4 * pk[1] + 1]];
+      v0 = Mf[0];
+      v1 = Mf[3];
+      v2 = Mf[6];
+      break;
+    }
+    case PK_ROT: {
+      typ = 1;
+      const int o = s.jorigin[pk[1]];
+      dv.org[q][0] = sh.pos[o][0];
+      dv.org[q][1] = sh.pos[o][1];
+      dv.org[q][2] = sh.pos[o][2];
+      v0 = sh.om[q][0];
+      v1 = sh.om[q][1];
+      v2 = sh.om[q][2];
+      break;
+    }
+  }
+  dv.typ[q] = typ;
+  dv.vec[q][0] = v0;
+  dv.vec[q][1] = v1;
+  dv.vec[q][2] = v2;
+}
+
+// fk_dpos from the resolved table (valid after fk_deriv_prep of every q + a barrier)
+__device__ __forceinline__ void fk_dpos_fast(const SkelView& s, const FkShared& sh, const FkDeriv& dv, int node, int q,
+                                             double* d) {
+  const bool on = s.deriv[node * s.P + q] != 0;
+  const double w0 = dv.vec[q][0], w1 = dv.vec[q][1], w2 = dv.vec[q][2];
+  if (dv.typ[q] == 1) {
+    const double r0 = sh.pos[node][0] - dv.org[q][0];
+    const double r1 = sh.pos[node][1] - dv.org[q][1];
+    const double r2 = sh.pos[node][2] - dv.org[q][2];
+    d[0] = on ? w1 * r2 - w2 * r1 : 0.0;
+    d[1] = on ? w2 * r0 - w0 * r2 : 0.0;
+    d[2] = on ? w0 * r1 - w1 * r0 : 0.0;
+  } else {
+    d[0] = on ? w0 : 0.0;
+    d[1] = on ? w1 : 0.0;
+    d[2] = on ? w2 : 0.0;
+  }
+}

@@ -236,6 +236,7 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   double *s_cam = lds + lo.cam, *s_am = lds + lo.am, *s_qt = lds + lo.qt, *s_ac = lds + lo.ac, *s_cf = lds + lo.cf,
          *s_u = lds + lo.uni;
   __shared__ FkShared fk;
+  __shared__ FkDeriv fkd;
   __shared__ double s_dx[3], s_ddx[3];
   __shared__ double s_red[256];
   __shared__ int s_tabI[FK_MAX_INTS];
@@ -254,6 +255,7 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   LPROF(62);
   fk_frame(s, X + f * P, fk, tid, blockDim.x);
   __syncthreads();
+  if (tid < P) fk_deriv_prep(s, fk, fkd, tid);  // read after the barriers of phase (a)
   LPROF(56);
   if (tid < C) {
     const double tc = d.Ct ? tau[tid] : 0.0;
@@ -367,17 +369,21 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   dbl4 acc[3];
   for (int q = 0; q < 3; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
   double gacc = 0.0;
+  const int gi = tid - 128;
   constexpr int RC = 3 * LIN_MC;
   double* sD = s_u;            // D_l rows
   double* sB = s_u + RC * LD;  // Z_l D_l + Q_l rows
   double* sQ = sB + RC * LD;   // Q_l rows
   for (int l0 = 0; l0 < L; l0 += LIN_MC) {
+#ifdef FTE_PROFILE
+    unsigned long long tb = wall_clock64();
+#endif
     for (int e = tid; e < LIN_MC * NZP; e += blockDim.x) {
       const int m = e / NZP, q = e - m * NZP, l = l0 + m;
       double dp[3] = {0.0, 0.0, 0.0}, qv[3] = {0.0, 0.0, 0.0};
       const double* am = s_am + 27 * (l < L ? l : 0);
       if (l < L) {
-        if (q < P) fk_dpos(s, fk, s.outn[l], q, dp);
+        if (q < P) fk_dpos_fast(s, fk, fkd, s.outn[l], q, dp);
         int i0;
         const int cls = lin_tcol(q, P, NZ, &i0);
         if (cls >= 0 && cls < 3) {
@@ -394,9 +400,18 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
       }
     }
     __syncthreads();
-    if (tid < NZP) {
+#ifdef FTE_PROFILE
+    if (blockIdx.x == 0 && tid == 0) {  // operand rows built (slot 14), MFMA + barrier (slot 15)
+      const unsigned long long t1 = wall_clock64();
+      atomicAdd(&g_fte_prof[14], t1 - tb);
+      tb = t1;
+    }
+#endif
+    // gradient column gi = tid - 128 on wave 2, which carries one MFMA tile fewer than
+    // waves 0 and 1 (NT = 3: tiles 0-5 on waves 0, 1, 2, 3, 0, 1)
+    if (gi >= 0 && gi < NZP) {
       const int nr = 3 * min(LIN_MC, L - l0);
-      for (int r = 0; r < nr; ++r) gacc = fma(sD[r * LD + tid], s_am[27 * (l0 + r / 3) + 24 + r % 3], gacc);
+      for (int r = 0; r < nr; ++r) gacc = fma(sD[r * LD + gi], s_am[27 * (l0 + r / 3) + 24 + r % 3], gacc);
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -416,6 +431,9 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
       }
     }
     __syncthreads();
+#ifdef FTE_PROFILE
+    if (blockIdx.x == 0 && tid == 0) atomicAdd(&g_fte_prof[15], wall_clock64() - tb);
+#endif
   }
 
   LPROF(58);
@@ -457,9 +475,9 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
       H[col * FTE_NZP + row] = v;
     }
   }
-  if (tid < NZP) {
+  if (gi >= 0 && gi < NZP) {
     int i;
-    const int a = lin_tcol(tid, P, NZ, &i);
+    const int a = lin_tcol(gi, P, NZ, &i);
     if (a >= 0 && a < 3) {
       for (int c = 0; c < C; ++c) gacc += s_cf[7 * c + a] * s_ac[9 * c + 6 + i];
     } else if (a == 3) {
@@ -467,7 +485,7 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
       const double* r = s_ac + 9 * i + 6;
       gacc += v[0] * r[0] + v[1] * r[1] + v[2] * r[2];
     }
-    gloc[(size_t)k * FTE_NZP + tid] = gacc;
+    gloc[(size_t)k * FTE_NZP + gi] = gacc;
   }
   const double tot = block_sum(rho, s_red);
   if (tid == 0) Floc[k] = tot;

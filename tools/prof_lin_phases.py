@@ -26,5 +26,8 @@ fk = [(24, 'sincos'), (25, 'barrier 1'), (26, 'joint rotations G'), (27, 'joint 
 print('fk_frame (thread 0, block 0), mean us since fk_frame start:')
 for k, nm in fk:
     print(f'  {nm:32s} {v[k]:8.2f}')
+print('phase (b), summed over the marker chunks:')
+for k, nm in [(14, 'operand rows (fk_dpos, Z D + Q)'), (15, 'gradient + MFMA + barrier')]:
+    print(f'  {nm:32s} {v[k]:8.2f}')
 for k, nm in [(61, 'skeleton table staged'), (62, 'cams / LDS init (FK start)'), (56, 'FK done'), (57, 'observations + aggregation done'), (58, 'MFMA H done'), (59, 'store done')]:
     print(f'{nm:34s} {v[k]:8.2f}')
