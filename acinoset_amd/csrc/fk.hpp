@@ -148,31 +148,46 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
     dst[1] = t[1];
     dst[2] = t[2];
   }
-  for (int j = tid; j < s.J; j += nth) {
+  // G = A_{n-1} ... A_0 (apply A_0 first), one thread per (joint, column): the column
+  // starts as a unit vector and takes the joint's <= 3 rotations; the joint's table entries
+  // and their sines / cosines are loaded together, and the axis is selected, not branched on
+  // (the three candidate results are act_rot_vec's expressions, so the same bits)
+  for (int jc = tid; jc < 3 * s.J; jc += nth) {
+    const int j = jc / 3, col = jc - 3 * j;
     const int* jt = s.joints + 8 * j;
     const int nrot = jt[1];
-    // G = A_{n-1} ... A_0 (apply A_0 first): build column by column from identity
-    double Gm[9];
+    int ax[3], pr[3];
+    double sr[3], cr[3];
 #pragma unroll
-    for (int col = 0; col < 3; ++col) {
-      double v[3] = {col == 0 ? 1.0 : 0.0, col == 1 ? 1.0 : 0.0, col == 2 ? 1.0 : 0.0};
-      for (int r = 0; r < nrot; ++r) {
-        double w[3];
-        const int p = jt[5 + r];
-        act_rot_vec(jt[2 + r], sh.sn[p], sh.cs[p], v, w);
-        v[0] = w[0];
-        v[1] = w[1];
-        v[2] = w[2];
-      }
-      Gm[col] = v[0];
-      Gm[3 + col] = v[1];
-      Gm[6 + col] = v[2];
+    for (int r = 0; r < 3; ++r) {
+      ax[r] = jt[2 + r];
+      pr[r] = r < nrot ? jt[5 + r] : 0;
     }
 #pragma unroll
-    for (int i = 0; i < 9; ++i) sh.G[j][i] = Gm[i];
+    for (int r = 0; r < 3; ++r) {
+      sr[r] = sh.sn[pr[r]];
+      cr[r] = sh.cs[pr[r]];
+    }
+    double v0 = col == 0 ? 1.0 : 0.0, v1 = col == 1 ? 1.0 : 0.0, v2 = col == 2 ? 1.0 : 0.0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      if (r >= nrot) break;
+      const double sv = sr[r], c = cr[r];
+      const double x0 = v0, x1 = v1, x2 = v2;
+      const int a = ax[r];
+      // axis 0: (x0, c x1 - s x2, s x1 + c x2); 1: (c x0 + s x2, x1, -s x0 + c x2);
+      // 2: (c x0 - s x1, s x0 + c x1, x2)
+      v0 = a == 0 ? x0 : (a == 1 ? c * x0 + sv * x2 : c * x0 - sv * x1);
+      v1 = a == 0 ? c * x1 - sv * x2 : (a == 1 ? x1 : sv * x0 + c * x1);
+      v2 = a == 0 ? sv * x1 + c * x2 : (a == 1 ? -sv * x0 + c * x2 : x2);
+    }
+    sh.G[j][col] = v0;
+    sh.G[j][3 + col] = v1;
+    sh.G[j][6 + col] = v2;
   }
   FK_MARK(26);
   __syncthreads();
+  constexpr int FK_D = 8;  // unrolled chain depth of the node positions below
   for (int j = tid; j < s.J; j += nth) {
     double Mm[9], T[9];
 #pragma unroll
@@ -190,31 +205,58 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
   FK_MARK(27);
   __syncthreads();
   const int* pk = s.pk;
+  // node positions: the chain of (node, frame, offset parameter) up to the root first
+  // (int loads only), then every term's M and offset loads at once; terms are added in walk
+  // order with the root / world translation last, as a walk up would
   for (int k = tid; k < s.K; k += nth) {
     double p0 = 0.0, p1 = 0.0, p2 = 0.0;
-    int node = k;
-    while (true) {
-      const int* nd = s.nodes + 4 * node;
-      const int base = nd[0];
-      if (base == -2) {  // world node (lure): params of PK_WORLD kind
-        p0 += sh.world[0];
-        p1 += sh.world[1];
-        p2 += sh.world[2];
-        break;
+    int cn[FK_D], cf[FK_D], co[FK_D];
+    bool add[FK_D];
+    int node = k, endb = 0;
+    bool live = true;
+#pragma unroll
+    for (int a = 0; a < FK_D; ++a) {
+      const int* nd = s.nodes + 4 * (live ? node : 0);
+      const int b = nd[0];
+      cn[a] = node;
+      cf[a] = nd[1];
+      co[a] = nd[2];
+      add[a] = live && b >= 0;
+      if (live && b < 0) {
+        endb = b;
+        live = false;
       }
-      if (base == -1) {  // head root: (x_0, y_0, z_0)
-        p0 += sh.root[0];
-        p1 += sh.root[1];
-        p2 += sh.root[2];
-        break;
-      }
-      const double* Mf = sh.M[nd[1]];
-      double o0 = s.off[3 * node], o1 = s.off[3 * node + 1], o2 = s.off[3 * node + 2];
-      if (nd[2] >= 0) o0 = sh.xp[nd[2]];
+      if (add[a]) node = b;
+    }
+    auto term = [&](int nn, int fr, int op) {
+      const double* Mf = sh.M[fr];
+      double o0 = s.off[3 * nn], o1 = s.off[3 * nn + 1], o2 = s.off[3 * nn + 2];
+      if (op >= 0) o0 = sh.xp[op];
       p0 += Mf[0] * o0 + Mf[1] * o1 + Mf[2] * o2;
       p1 += Mf[3] * o0 + Mf[4] * o1 + Mf[5] * o2;
       p2 += Mf[6] * o0 + Mf[7] * o1 + Mf[8] * o2;
-      node = base;
+    };
+#pragma unroll
+    for (int a = 0; a < FK_D; ++a)
+      if (add[a]) term(cn[a], cf[a], co[a]);
+    while (live) {  // chains deeper than FK_D
+      const int* nd = s.nodes + 4 * node;
+      const int b = nd[0];
+      if (b < 0) {
+        endb = b;
+        break;
+      }
+      term(node, nd[1], nd[2]);
+      node = b;
+    }
+    if (endb == -2) {  // world node (lure): params of PK_WORLD kind
+      p0 += sh.world[0];
+      p1 += sh.world[1];
+      p2 += sh.world[2];
+    } else {  // head root: (x_0, y_0, z_0)
+      p0 += sh.root[0];
+      p1 += sh.root[1];
+      p2 += sh.root[2];
     }
     sh.pos[k][0] = p0;
     sh.pos[k][1] = p1;
