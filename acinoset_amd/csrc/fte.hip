@@ -1841,10 +1841,9 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
     return o;
   };
   const size_t Cg1 = d.Cg ? d.Cg : 1;
-  // the per-frame linearisation is double-buffered only for the speculative single-GPU
-  // solve (k_fte_linearize spec = 1 writes the trial's copy); the distributed handles
-  // (`owned`) linearise in place (hsel = spec = 0) and take one copy
-  const size_t nlin = owned ? 1 : 2;
+  // the per-frame linearisation is double-buffered: the speculative linearisation of the
+  // trial state (k_fte_linearize spec = 1) writes copy cur ^ 1 (single-GPU and frame-window)
+  const size_t nlin = 2;
   const size_t oX = take((size_t)2 * M * P), oT = take(2 * (size_t)d.NT), oAd = take((size_t)M * P),
                oH = take(nlin * N * FTE_NZP * FTE_NZP), og = take(nlin * N * FTE_NZP), oF = take(nlin * N), oAb = take((size_t)M * 4 * P * P),
                ogb = take((size_t)M * P), oBt = take((size_t)M * P * Cg1), ogm = take(M),
@@ -2232,17 +2231,17 @@ __global__ void k_dist_scatter(FteDims d, const FteState* __restrict__ st, int r
 
 // p3 = (measurement cost, model cost, |step|^2, |X, tau|^2) of this rank's owned terms /
 // rows (frames [k0, k1), super-blocks [n0, n1) of the trial's norm partials)
-__global__ __launch_bounds__(256) void k_dist_cost_pack(const FteState* __restrict__ st, int which, int k0, int k1,
-                                                        const double* __restrict__ Fm, const double* __restrict__ Fq,
-                                                        int n0, int n1, const double* __restrict__ normp,
-                                                        double* __restrict__ p3) {
+// which = 1: the trial's measurement terms are in Fm's speculative copy (cur ^ 1, N each)
+__global__ __launch_bounds__(256) void k_dist_cost_pack(const FteState* __restrict__ st, int which, int N, int m0,
+                                                        int m1, int q0, int q1, const double* __restrict__ Fm,
+                                                        const double* __restrict__ Fq, int n0, int n1,
+                                                        const double* __restrict__ normp, double* __restrict__ p3) {
   if (which == 1 && st->status != 0) return;
+  if (which == 1) Fm += (size_t)(st->cur ^ 1) * N;
   __shared__ double s_red[256];
   double a = 0.0, b = 0.0, dn = 0.0, xn = 0.0;
-  for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
-    a += Fm[k];
-    b += Fq[k];
-  }
+  for (int k = m0 + threadIdx.x; k < m1; k += blockDim.x) a += Fm[k];
+  for (int k = q0 + threadIdx.x; k < q1; k += blockDim.x) b += Fq[k];
   for (int w = n0 + threadIdx.x; w < n1; w += blockDim.x) {
     dn += normp[2 * w];
     xn += normp[2 * w + 1];
@@ -2285,9 +2284,7 @@ __global__ __launch_bounds__(256) void k_dist_x_in(FteDims d, const FteState* __
 
 // k_fte_lm with the all-reduced costs (every rank takes the same decision)
 __global__ __launch_bounds__(256) void k_fte_lm_dist(FteDims d, FteState* __restrict__ st, FteOptsDev o, int init,
-                                                     const double* __restrict__ p3,
-                                                     const double* __restrict__ normp) {
-  __shared__ double s_red[256];
+                                                     const double* __restrict__ p3) {
   const int tid = threadIdx.x;
   const double fm = p3[0], fq = p3[1];
   if (init) {
@@ -2751,8 +2748,13 @@ int acs_fte_dist_init(acs_fte_dist* h, double* p3) {
   if (h->c_hi > h->c_lo)
     hipLaunchKernelGGL(k_fte_cost, dim3(h->c_hi - h->c_lo), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
                        b.tau, b.qinv, b.st, 0, h->c_lo, h->own_lo, h->own_hi, b.Fm, b.Fq);
-  hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 0, h->c_lo, h->c_hi, b.Fm, b.Fq, 0, 0,
-                     (const double*)nullptr, p3);
+  hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 0, d.N, h->c_lo, h->c_hi, h->c_lo, h->c_hi,
+                     (const double*)b.Fm, (const double*)b.Fq, 0, 0, (const double*)nullptr, p3);
+  // the linearisation of the starting state (copy 0); later ones are speculative (phase 3)
+  if (h->a0 < d.nblk && h->k_hi > h->k_lo)
+    hipLaunchKernelGGL(k_fte_linearize, dim3(h->k_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
+                       b.meas, b.w, b.X, b.tau, b.st, 1, h->k_lo, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr,
+                       (const double*)nullptr);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }
@@ -2765,17 +2767,14 @@ static int dist_phase1_body(acs_fte_dist* h, double* p1) {
   hipStream_t s = ctx->stream;
   ACS_HIP(ctx, hipMemsetAsync(p1, 0, sizeof(double) * h->Lo.n1, s));
   if (h->a0 < d.nblk) {
-    if (h->k_hi > h->k_lo)
-      hipLaunchKernelGGL(k_fte_linearize, dim3(h->k_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
-                         b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr,
-                         (const double*)nullptr);
+    // the linearisation of X[cur] is there already (init, or the speculative one of phase 3)
     hipLaunchKernelGGL(k_fte_assemble, dim3(h->f_hi - h->f_lo), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, 0,
-                       h->f_lo, h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 0);
+                       h->f_lo, h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1);
     const int top = std::min(h->bend, d.nblk - 1);
     cr_launch_build(d, s, top - h->a0 + 1, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, h->a0, h->a0, h->bend, nullptr);
     const double* Efin = dist_local_cr(h);
     hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part,
-                       h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk), 0);
+                       h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk), 1);
     hipLaunchKernelGGL(k_dist_pack, dim3(32, 2), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.Dc, Efin,
                        b.GBc, b.Ab, b.gb, p1);
     hipLaunchKernelGGL(k_dist_pack_small, dim3(1), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.part,
@@ -2841,11 +2840,17 @@ static int dist_phase3_body(acs_fte_dist* h, double* p3) {
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
   hipStream_t s = ctx->stream;
-  if (h->c_hi > h->c_lo)
-    hipLaunchKernelGGL(k_fte_cost, dim3(h->c_hi - h->c_lo), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
-                       b.tau, b.qinv, b.st, 1, h->c_lo, h->own_lo, h->own_hi, b.Fm, b.Fq);
-  hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 1, h->c_lo, h->c_hi, b.Fm, b.Fq, h->out_lo,
-                     h->out_hi, b.normp, p3);
+  // speculative linearisation of the trial rows: its measurement terms (owned frames
+  // [k_lo, k_hi)) and model stencils (owned: k - 1 in [own_lo, own_hi), so frames up to k_hi
+  // inclusive; the one extra frame's own terms are not counted) are the trial cost, and an
+  // accepted step needs no new linearisation in phase 1
+  const int l_hi = std::min(h->k_hi + 1, d.N);
+  if (h->a0 < d.nblk && l_hi > h->k_lo)
+    hipLaunchKernelGGL(k_fte_linearize, dim3(l_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
+                       b.meas, b.w, b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv);
+  const int q0 = std::max(h->k_lo + 1, 1), q1 = l_hi;
+  hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 1, d.N, h->k_lo, h->k_hi, q0,
+                     std::max(q0, q1), (const double*)b.Floc, (const double*)b.Fq, h->out_lo, h->out_hi, b.normp, p3);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }
@@ -2894,7 +2899,7 @@ int acs_fte_dist_phase4(acs_fte_dist* h, const double* p3, int32_t init, int32_t
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
   hipStream_t s = ctx->stream;
-  hipLaunchKernelGGL(k_fte_lm_dist, dim3(1), dim3(256), 0, s, d, b.st, h->o, init, p3, b.normp);
+  hipLaunchKernelGGL(k_fte_lm_dist, dim3(1), dim3(256), 0, s, d, b.st, h->o, init, p3);
   ACS_HIP(ctx, hipGetLastError());
   int32_t stv = 0;
   ACS_HIP(ctx, hipMemcpyAsync(&stv, &b.st->status, sizeof(int32_t), hipMemcpyDeviceToHost, s));
