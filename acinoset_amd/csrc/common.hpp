@@ -43,7 +43,16 @@ struct acs_ctx {
     std::string key;
   };
   GraphCache graphs[GRAPH_NSLOTS];
+  // pinned host slots for asynchronous device-state snapshots and their completion events
+  // (the FTE solve reads the LM status of iteration n while iteration n + 1 runs)
+  void* pinned = nullptr;
+  size_t pinned_bytes = 0;
+  hipEvent_t snap_ev[2] = {};
 };
+
+// Pinned host buffer of at least `bytes` (grow-only) and the two snapshot events.
+// Returns nullptr (and sets the error) on failure.
+void* acs_pinned(acs_ctx* ctx, size_t bytes);
 
 // append the bytes of a trivially copyable value to a graph-cache key
 template <typename T>

@@ -34,6 +34,33 @@ void* acs_ws(acs_ctx* ctx, int slot, size_t bytes) {
   return ctx->ws[slot];
 }
 
+void* acs_pinned(acs_ctx* ctx, size_t bytes) {
+  if (!ctx->snap_ev[0]) {
+    for (auto& e : ctx->snap_ev) {
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        e = nullptr;
+        acs_fail(ctx, ACS_E_HIP, "hipEventCreateWithFlags failed");
+        return nullptr;
+      }
+    }
+  }
+  if (ctx->pinned_bytes >= bytes) return ctx->pinned;
+  if (ctx->pinned) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipHostFree(ctx->pinned);
+    ctx->pinned = nullptr;
+    ctx->pinned_bytes = 0;
+  }
+  const size_t n = (bytes + 255) & ~size_t(255);
+  if (hipHostMalloc(&ctx->pinned, n, hipHostMallocDefault) != hipSuccess) {
+    ctx->pinned = nullptr;
+    acs_fail(ctx, ACS_E_NOMEM, "hipHostMalloc(%zu) failed", n);
+    return nullptr;
+  }
+  ctx->pinned_bytes = n;
+  return ctx->pinned;
+}
+
 int acs_stage_in(acs_ctx* ctx, int slot, const void* src, size_t bytes, uint32_t flags, void** dev) {
   if (flags & ACS_DEVICE_PTRS) {
     *dev = const_cast<void*>(src);
@@ -106,6 +133,9 @@ int acs_ctx_destroy(acs_ctx* ctx) {
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
   for (int i = 0; i < WS_NSLOTS; ++i)
     if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  for (auto& e : ctx->snap_ev)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
   return ACS_OK;

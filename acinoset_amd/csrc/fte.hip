@@ -98,16 +98,27 @@ __device__ __forceinline__ double loss_curv(double e, const LossOut& l) {
 }
 
 // fixed-order block sum (blockDim.x must be a power of two <= 256)
+// Sum over the workgroup (blockDim a power of two, 64..1024) in the fixed order of the
+// halving tree s[t] += s[t + h], h = n/2 .. 1. The levels h >= 128 go through LDS; then
+// every wave evaluates the last seven levels itself (s[l] + s[l + 64], then shuffles down
+// 32 .. 1: lane l < h adds lane l + h, the tree's own operands), so each wave ends with the
+// tree's bits in lane 0 without a broadcast round trip: 3 barriers at 256 threads, was 10.
 __device__ double block_sum(double v, double* s_red) {
-  const int t = threadIdx.x;
-  s_red[t] = v;
-  __syncthreads();
-  for (int h = blockDim.x / 2; h > 0; h >>= 1) {
-    if (t < h) s_red[t] += s_red[t + h];
+  const int t = threadIdx.x, n = blockDim.x, l = t & 63;
+  double r = v;
+  if (n > 64) {
+    s_red[t] = v;
     __syncthreads();
+    for (int h = n / 2; h >= 128; h >>= 1) {
+      if (t < h) s_red[t] += s_red[t + h];
+      __syncthreads();
+    }
+    r = s_red[l] + s_red[l + 64];
   }
-  const double r = s_red[0];
-  __syncthreads();
+#pragma unroll
+  for (int h = 32; h > 0; h >>= 1) r += __shfl_down(r, h, 64);
+  r = __shfl(r, 0, 64);
+  if (n > 64) __syncthreads();  // s_red is free for the caller's next reduction
   return r;
 }
 __device__ double block_max(double v, double* s_red) {
@@ -1713,12 +1724,21 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
                                                 const double* __restrict__ normp, int spec) {
   __shared__ double s_red[256];
   const int tid = threadIdx.x;
-  if (spec) Fm += (size_t)(st->cur ^ 1) * d.N;  // the trial's measurement terms (Floc buffer)
-  double a = 0.0, b = 0.0;
+  // every load is issued before the LM state is read: both copies of the measurement terms
+  // (spec: the trial's are in Floc copy cur ^ 1) and the step / state norm partials
+  double a0 = 0.0, a1 = 0.0, b = 0.0, dn = 0.0, xn = 0.0;
   for (int k = tid; k < d.N; k += blockDim.x) {
-    a += Fm[k];
+    a0 += Fm[k];
+    if (spec) a1 += Fm[(size_t)d.N + k];
     b += Fq[k];
   }
+  if (!init) {
+    for (int w = tid; w < d.nblk; w += blockDim.x) {
+      dn += normp[2 * w];
+      xn += normp[2 * w + 1];
+    }
+  }
+  const double a = (spec && (st->cur ^ 1)) ? a1 : a0;
   const double fm = block_sum(a, s_red), fq = block_sum(b, s_red);
   if (init) {
     if (tid == 0) {
@@ -1729,11 +1749,6 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
     return;
   }
   if (st->status != 0) return;
-  double dn = 0.0, xn = 0.0;
-  for (int w = tid; w < d.nblk; w += blockDim.x) {
-    dn += normp[2 * w];
-    xn += normp[2 * w + 1];
-  }
   dn = block_sum(dn, s_red);
   xn = block_sum(xn, s_red);
   if (tid != 0) return;
@@ -2435,10 +2450,13 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
     hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
                        b.X, b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr);
   ACS_HIP(ctx, hipGetLastError());
-  // capture `chunk` iterations into one hipGraph (kernels read the LM state from device
-  // memory, so the graph is static); replay until the device reports a stop status. The
+  // capture one iteration into a hipGraph (kernels read the LM state from device memory,
+  // so the graph is static) and replay it until the device reports a stop status, one
+  // iteration queued ahead: the host reads iteration n's status snapshot (pinned slot n & 1)
+  // while iteration n + 1 runs, so the GPU never waits for the host, and a stop costs one
+  // early-exiting iteration (was: chunks of 4 behind a full synchronisation, up to 3). The
   // instantiated graph stays in the context for the next solve with the same key.
-  const int chunk = 4;
+  const int chunk = 1;
   std::string key;
   key_put(key, d);
   key_put(key, b);
@@ -2476,18 +2494,32 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   }
   FteState hs;
   std::memset(&hs, 0, sizeof(hs));
-  for (int it = 0; it < op.max_iters + chunk; it += chunk) {
-    if (use_graph) {
-      ACS_HIP(ctx, hipGraphLaunch(exec, s));
-    } else {
-      for (int c = 0; c < chunk; ++c) fte_enqueue_iteration(S, s, o);
+  if (op.max_iters > 0) {
+    FteState* snap = (FteState*)acs_pinned(ctx, 2 * sizeof(FteState));
+    if (!snap) return ACS_E_NOMEM;
+    // max_iters + 1 launches at most: the kernel sets MAXITER in iteration max_iters
+    const int nmax = op.max_iters + 1;
+    int last = 0;
+    for (int n = 0;; ++n) {
+      if (n < nmax) {
+        if (use_graph)
+          ACS_HIP(ctx, hipGraphLaunch(exec, s));
+        else
+          fte_enqueue_iteration(S, s, o);
+        ACS_HIP(ctx, hipGetLastError());
+        ACS_HIP(ctx, hipMemcpyAsync(&snap[n & 1], b.st, sizeof(FteState), hipMemcpyDeviceToHost, s));
+        ACS_HIP(ctx, hipEventRecord(ctx->snap_ev[n & 1], s));
+        last = n;
+      }
+      if (n >= 1) {
+        ACS_HIP(ctx, hipEventSynchronize(ctx->snap_ev[(n - 1) & 1]));
+        if (snap[(n - 1) & 1].status != 0 || n >= nmax) break;
+      }
     }
-    ACS_HIP(ctx, hipGetLastError());
-    ACS_HIP(ctx, hipMemcpyAsync(&hs, b.st, sizeof(hs), hipMemcpyDeviceToHost, s));
-    ACS_HIP(ctx, hipStreamSynchronize(s));
-    if (hs.status != 0) break;
-  }
-  if (op.max_iters == 0) {
+    // the last queued iteration exits early on a stop status (the state is unchanged)
+    ACS_HIP(ctx, hipEventSynchronize(ctx->snap_ev[last & 1]));
+    hs = snap[last & 1];
+  } else {
     ACS_HIP(ctx, hipMemcpyAsync(&hs, b.st, sizeof(hs), hipMemcpyDeviceToHost, s));
     ACS_HIP(ctx, hipStreamSynchronize(s));
   }
