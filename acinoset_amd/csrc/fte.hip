@@ -121,6 +121,29 @@ __device__ double block_sum(double v, double* s_red) {
   if (n > 64) __syncthreads();  // s_red is free for the caller's next reduction
   return r;
 }
+// acc[s] += x[s][es * k] for k = k0, k0 + st, .. < k1 in that order (the plain strided
+// loop's sums, bit for bit), with eight strides' loads of every stream issued before the
+// first add instead of one dependent round trip per stride
+template <int NS>
+__device__ __forceinline__ void strided_sums(const double* const (&x)[NS], int es, int k0, int k1, int st,
+                                             double* acc) {
+  int k = k0;
+  for (; k + 7 * st < k1; k += 8 * st) {
+    double v[NS][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) v[s][j] = x[s][(size_t)es * (k + j * st)];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) acc[s] += v[s][j];
+  }
+  for (; k < k1; k += st)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc[s] += x[s][(size_t)es * k];
+}
+
 __device__ double block_max(double v, double* s_red) {
   const int t = threadIdx.x;
   s_red[t] = v;
@@ -1726,20 +1749,18 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
   const int tid = threadIdx.x;
   // every load is issued before the LM state is read: both copies of the measurement terms
   // (spec: the trial's are in Floc copy cur ^ 1) and the step / state norm partials
-  double a0 = 0.0, a1 = 0.0, b = 0.0, dn = 0.0, xn = 0.0;
-  for (int k = tid; k < d.N; k += blockDim.x) {
-    a0 += Fm[k];
-    if (spec) a1 += Fm[(size_t)d.N + k];
-    b += Fq[k];
+  double acc[3] = {0.0, 0.0, 0.0}, nrm[2] = {0.0, 0.0};
+  {
+    const double* xs[3] = {Fm, spec ? Fm + d.N : Fm, Fq};
+    strided_sums<3>(xs, 1, tid, d.N, blockDim.x, acc);
   }
   if (!init) {
-    for (int w = tid; w < d.nblk; w += blockDim.x) {
-      dn += normp[2 * w];
-      xn += normp[2 * w + 1];
-    }
+    const double* xs[2] = {normp, normp + 1};
+    strided_sums<2>(xs, 2, tid, d.nblk, blockDim.x, nrm);
   }
-  const double a = (spec && (st->cur ^ 1)) ? a1 : a0;
-  const double fm = block_sum(a, s_red), fq = block_sum(b, s_red);
+  double dn = nrm[0], xn = nrm[1];
+  const double a = (spec && (st->cur ^ 1)) ? acc[1] : acc[0];
+  const double fm = block_sum(a, s_red), fq = block_sum(acc[2], s_red);
   if (init) {
     if (tid == 0) {
       st->F = st->F0 = fm + fq;
@@ -2254,13 +2275,20 @@ __global__ __launch_bounds__(256) void k_dist_cost_pack(const FteState* __restri
   if (which == 1 && st->status != 0) return;
   if (which == 1) Fm += (size_t)(st->cur ^ 1) * N;
   __shared__ double s_red[256];
-  double a = 0.0, b = 0.0, dn = 0.0, xn = 0.0;
-  for (int k = m0 + threadIdx.x; k < m1; k += blockDim.x) a += Fm[k];
-  for (int k = q0 + threadIdx.x; k < q1; k += blockDim.x) b += Fq[k];
-  for (int w = n0 + threadIdx.x; w < n1; w += blockDim.x) {
-    dn += normp[2 * w];
-    xn += normp[2 * w + 1];
+  double a = 0.0, b = 0.0, nrm[2] = {0.0, 0.0};
+  {
+    const double* xs[1] = {Fm};
+    strided_sums<1>(xs, 1, m0 + (int)threadIdx.x, m1, blockDim.x, &a);
   }
+  {
+    const double* xs[1] = {Fq};
+    strided_sums<1>(xs, 1, q0 + (int)threadIdx.x, q1, blockDim.x, &b);
+  }
+  if (n1 > n0) {
+    const double* xs[2] = {normp, normp + 1};
+    strided_sums<2>(xs, 2, n0 + (int)threadIdx.x, n1, blockDim.x, nrm);
+  }
+  double dn = nrm[0], xn = nrm[1];
   a = block_sum(a, s_red);
   b = block_sum(b, s_red);
   dn = block_sum(dn, s_red);
