@@ -190,6 +190,9 @@ __device__ double block_max(double v, double* s_red) {
 #define LIN_OCH 128  // observations per aggregation chunk (<= blockDim)
 #define LIN_MC 4     // markers per MFMA chunk (3 * LIN_MC operand rows)
 
+// compact per-frame tau border of the local normal matrix: Cg x Cg block, then Cg gradient
+__host__ __device__ __forceinline__ int tc_stride(int Cg) { return Cg * Cg + Cg; }
+
 struct LinLds {
   int cam, am, qt, ac, cf, uni, total;
 };
@@ -247,7 +250,8 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
                                                        const FteState* __restrict__ st, int force, int k0,
                                                        double* __restrict__ Hloc, double* __restrict__ gloc,
                                                        double* __restrict__ Floc, int spec,
-                                                       double* __restrict__ Fq, const double* __restrict__ qinv) {
+                                                       double* __restrict__ Fq, const double* __restrict__ qinv,
+                                                       double* __restrict__ Tc) {
   // spec: speculative linearisation at the trial state X[cur ^ 1] into the second
   // Hloc / gloc / Floc buffer, with the model cost of the frame's stencil in Fq: it is the
   // trial cost for k_fte_lm, and an accepted step (cur ^= 1) needs no new linearisation
@@ -257,6 +261,7 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
     Hloc += hb * d.N * FTE_NZP * FTE_NZP;
     gloc += hb * d.N * FTE_NZP;
     Floc += hb * d.N;
+    Tc += hb * d.N * tc_stride(d.Cg);
   }
   const int k = blockIdx.x + k0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
@@ -507,6 +512,13 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
       const double v = acc[q][rg] + tpart(row, col);
       H[row * FTE_NZP + col] = v;
       H[col * FTE_NZP + row] = v;
+      // the tau border block again, compact (k_cr_tau_partial reads it contiguously)
+      const int tr = row - (P + 6), tq = col - (P + 6);
+      if (tr >= 0 && tq < d.Cg) {
+        double* T = Tc + (size_t)k * tc_stride(d.Cg);
+        T[tr * d.Cg + tq] = v;
+        T[tq * d.Cg + tr] = v;
+      }
     }
   }
   if (gi >= 0 && gi < NZP) {
@@ -520,6 +532,8 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
       gacc += v[0] * r[0] + v[1] * r[1] + v[2] * r[2];
     }
     gloc[(size_t)k * FTE_NZP + gi] = gacc;
+    const int ti = gi - (P + 6);
+    if (ti >= 0 && ti < d.Cg) Tc[(size_t)k * tc_stride(d.Cg) + d.Cg * d.Cg + ti] = gacc;
   }
   const double tot = block_sum(rho, s_red);
   if (tid == 0) Floc[k] = tot;
@@ -1419,13 +1433,15 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
                                                         const double* __restrict__ Hloc,
                                                         const double* __restrict__ gloc,
                                                         const double* __restrict__ Tau, double* __restrict__ part,
-                                                        int k_lo, int k_hi, int b_lo, int b_hi, int hsel) {
+                                                        int k_lo, int k_hi, int b_lo, int b_hi, int hsel,
+                                                        const double* __restrict__ Tc) {
   // frames [k_lo, k_hi) (tau blocks of their normal matrices / gradients) and eliminated
   // super-blocks [b_lo, b_hi) (tau Schur terms), each range cut into CR_NCHUNK chunks
   if (st->status != 0) return;
   if (hsel) {
     Hloc += (size_t)st->cur * d.N * FTE_NZP * FTE_NZP;
     gloc += (size_t)st->cur * d.N * FTE_NZP;
+    if (Tc) Tc += (size_t)st->cur * d.N * tc_stride(d.Cg);
   }
   const int ch = blockIdx.x;
   const int P = d.P, Cg = d.Cg, GR = d.GR;
@@ -1449,7 +1465,9 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
   };
   for (int e = threadIdx.x; e < nE; e += blockDim.x) {
     double v;
-    if (e < nH) {
+    if (Tc && e < nH + Cg) {
+      v = sum8(Tc + e, (size_t)tc_stride(Cg), k0, k1);  // compact copy from k_fte_linearize
+    } else if (e < nH) {
       const int r = e / Cg, c = e % Cg;
       v = sum8(Hloc + (P + 6 + r) * FTE_NZP + P + 6 + c, (size_t)FTE_NZP * FTE_NZP, k0, k1);
     } else if (e < nH + Cg) {
@@ -1809,7 +1827,7 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
 struct FteBuffers {
   int* I;
   double *Rl, *cams, *meas, *w, *qinv, *X, *tau;
-  double *Hloc, *gloc, *Floc, *Ab, *gb, *Bt, *gmaxp, *Dc, *Ec, *GBc, *Wc, *Tau, *dcv, *dtau, *normp, *Fm, *Fq, *part;
+  double *Hloc, *gloc, *Floc, *Tc, *Ab, *gb, *Bt, *gmaxp, *Dc, *Ec, *GBc, *Wc, *Tau, *dcv, *dtau, *normp, *Fm, *Fq, *part;
   double* Adiag;
   double *Ec2, *dL, *dR;  // second coupling buffer (levels alternate), pending Schur terms
   int* bad;
@@ -1888,7 +1906,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
                oE2 = take((size_t)n * BP * BP), odL = take((size_t)n * BP * (BP + GR)),
                odR = take((size_t)n * BP * (BP + GR)),
                odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)),
-               onp = take(2 * (size_t)n), oFm = take(N), oFq = take(N), ost = take(16), oint = take(8);
+               onp = take(2 * (size_t)n), oTc = take(nlin * N * std::max(tc_stride(d.Cg), 1)), oFm = take(N), oFq = take(N), ost = take(16), oint = take(8);
   // staged inputs (owned mode only)
   const size_t oI = take((n_ints + 1) / 2 + 1), oR = take(n_reals), oC = take((size_t)ACS_CAM_STRIDE * C),
                oMe = take((size_t)N * C * L * 2), oWt = take((size_t)N * C * L), oQ = take(P);
@@ -1937,6 +1955,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.Hloc = arena + oH;
   b.gloc = arena + og;
   b.Floc = arena + oF;
+  b.Tc = arena + oTc;
   b.Ab = arena + oAb;
   b.gb = arena + ogb;
   b.Bt = arena + oBt;
@@ -2080,7 +2099,7 @@ static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
   hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
-                     b.st, force, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr);
+                     b.st, force, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr, b.Tc);
   hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, force, 0, 0, INT_MAX,
                      b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1);
 }
@@ -2105,7 +2124,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad, false, &sym);
   cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, sym);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
-                     d.N, 0, d.nblk, 1);
+                     d.N, 0, d.nblk, 1, (const double*)b.Tc);
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, d, b.st, (const double*)b.Wc, b.part, b.gmaxp, b.tau, b.dcv,
                      b.dtau, b.bad);
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
@@ -2118,7 +2137,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   // speculative linearisation at the trial state: its measurement terms and the model terms
   // are the trial cost (no separate cost pass)
   hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
-                     b.X, b.tau, b.st, 0, 0, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv);
+                     b.X, b.tau, b.st, 0, 0, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv, b.Tc);
   hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 0, b.Floc, b.Fq, b.normp, 1);
 }
 
@@ -2476,7 +2495,7 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   // the linearisation of the initial state (buffer cur = 0); later ones are speculative
   if (op.max_iters > 0)
     hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
-                       b.X, b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr);
+                       b.X, b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr, b.Tc);
   ACS_HIP(ctx, hipGetLastError());
   // capture one iteration into a hipGraph (kernels read the LM state from device memory,
   // so the graph is static) and replay it until the device reports a stop status, one
@@ -2814,7 +2833,7 @@ int acs_fte_dist_init(acs_fte_dist* h, double* p3) {
   if (h->a0 < d.nblk && h->k_hi > h->k_lo)
     hipLaunchKernelGGL(k_fte_linearize, dim3(h->k_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
                        b.meas, b.w, b.X, b.tau, b.st, 1, h->k_lo, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr,
-                       (const double*)nullptr);
+                       (const double*)nullptr, b.Tc);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }
@@ -2834,7 +2853,8 @@ static int dist_phase1_body(acs_fte_dist* h, double* p1) {
     cr_launch_build(d, s, top - h->a0 + 1, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, h->a0, h->a0, h->bend, nullptr);
     const double* Efin = dist_local_cr(h);
     hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part,
-                       h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk), 1);
+                       h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk), 1,
+                       (const double*)b.Tc);
     hipLaunchKernelGGL(k_dist_pack, dim3(32, 2), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.Dc, Efin,
                        b.GBc, b.Ab, b.gb, p1);
     hipLaunchKernelGGL(k_dist_pack_small, dim3(1), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.part,
@@ -2860,7 +2880,7 @@ static int dist_phase2_body(acs_fte_dist* h, const double* p1) {
   cr_reduce(dr, s, b.st, r, 0, dr.nblk, rb, dr.nlev, b.bad, false, &sym);
   cr_launch_top(dr, s, dr.nlev, 0, dr.nblk, b.st, r, b.bad, sym);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, dr, b.st, r.Hloc, r.gloc, r.Tau, r.part, 0,
-                     0, 0, dr.nblk, 0);
+                     0, 0, dr.nblk, 0, (const double*)nullptr);
   const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
   hipLaunchKernelGGL(k_red_part, dim3(1), dim3(256), 0, s, nE, h->Lo, b.st, p1, r.part);
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, dr, b.st, (const double*)r.Wc, r.part, r.gmaxp, b.tau, r.dcv,
@@ -2907,7 +2927,7 @@ static int dist_phase3_body(acs_fte_dist* h, double* p3) {
   const int l_hi = std::min(h->k_hi + 1, d.N);
   if (h->a0 < d.nblk && l_hi > h->k_lo)
     hipLaunchKernelGGL(k_fte_linearize, dim3(l_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
-                       b.meas, b.w, b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv);
+                       b.meas, b.w, b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv, b.Tc);
   const int q0 = std::max(h->k_lo + 1, 1), q1 = l_hi;
   hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 1, d.N, h->k_lo, h->k_hi, q0,
                      std::max(q0, q1), (const double*)b.Floc, (const double*)b.Fq, h->out_lo, h->out_hi, b.normp, p3);
