@@ -144,6 +144,21 @@ __device__ __forceinline__ void strided_sums(const double* const (&x)[NS], int e
     for (int s = 0; s < NS; ++s) acc[s] += x[s][(size_t)es * k];
 }
 
+// max(m, x[k]) over k = k0, k0 + st, .. < k1 with eight loads in flight (max is exact, so
+// any grouping gives the same value)
+__device__ __forceinline__ double strided_max(const double* __restrict__ x, int k0, int k1, int st, double m) {
+  int k = k0;
+  for (; k + 7 * st < k1; k += 8 * st) {
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[k + j * st];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmax(m, v[j]);
+  }
+  for (; k < k1; k += st) m = fmax(m, x[k]);
+  return m;
+}
+
 __device__ double block_max(double v, double* s_red) {
   const int t = threadIdx.x;
   s_red[t] = v;
@@ -1515,7 +1530,7 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
   // gradient max (frames + free tau border)
   {
     double mx = 0.0;
-    for (int f = tid; f < d.M; f += nth) mx = fmax(mx, gmaxp[f]);
+    mx = strided_max(gmaxp, tid, d.M, nth, mx);
     for (int c = tid; c < Cg; c += nth)
       if (!s_held[c]) mx = fmax(mx, fabs(s_sum[nH + c]));
     mx = block_max(mx, s_red);
@@ -2225,7 +2240,7 @@ __global__ __launch_bounds__(256) void k_dist_pack_small(FteDims d, const FteSta
   }
   const int f0 = 3 * (a0 + 1), f1 = min(3 * min(bend, d.nblk), d.M);
   double mx = 0.0;
-  for (int f = f0 + threadIdx.x; f < f1; f += blockDim.x) mx = fmax(mx, gmaxp[f]);
+  mx = strided_max(gmaxp, f0 + (int)threadIdx.x, f1, blockDim.x, mx);
   mx = block_max(mx, s_red);
   if (threadIdx.x == 0) p1[Lo.oGmax + rank] = mx;
 }
