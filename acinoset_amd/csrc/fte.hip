@@ -1839,6 +1839,26 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
 // =======================================================================================
 // host side
 // =======================================================================================
+// both copies of X from Xsrc, tau copy 0 from tausrc (zeros if null) and copy 1 zeroed, the
+// pivot counter and the tau step zeroed (Xsrc / tausrc may be copy 0 itself)
+__global__ __launch_bounds__(256) void k_fte_init_state(double* __restrict__ X, const double* Xsrc, size_t MP,
+                                                        double* __restrict__ tau, const double* tausrc, int NT,
+                                                        int* __restrict__ bad, double* __restrict__ dtau, int GR) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < MP) {
+    const double v = Xsrc[i];
+    X[i] = v;
+    X[MP + i] = v;
+  }
+  if (i < (size_t)NT) {
+    const double v = tausrc ? tausrc[i] : 0.0;
+    tau[i] = v;
+    tau[NT + i] = 0.0;
+  }
+  if (i < (size_t)GR) dtau[i] = 0.0;
+  if (i == 0) *bad = 0;
+}
+
 struct FteBuffers {
   int* I;
   double *Rl, *cams, *meas, *w, *qinv, *X, *tau;
@@ -1991,15 +2011,21 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.Fq = arena + oFq;
   b.st = (FteState*)(arena + ost);
   b.bad = (int*)(arena + oint);
-  ACS_HIP(ctx, hipMemcpyAsync(b.X, X, sizeof(double) * M * P, kin, s));
-  if (tau)
-    ACS_HIP(ctx, hipMemcpyAsync(b.tau, tau, sizeof(double) * d.NT, kin, s));
-  else
-    ACS_HIP(ctx, hipMemsetAsync(b.tau, 0, sizeof(double) * d.NT, s));
-  ACS_HIP(ctx, hipMemsetAsync(b.tau + d.NT, 0, sizeof(double) * d.NT, s));
-  ACS_HIP(ctx, hipMemcpyAsync(b.X + (size_t)M * P, b.X, sizeof(double) * M * P, hipMemcpyDeviceToDevice, s));
-  ACS_HIP(ctx, hipMemsetAsync(b.bad, 0, sizeof(int), s));
-  ACS_HIP(ctx, hipMemsetAsync(b.dtau, 0, sizeof(double) * GR, s));
+  // state buffers in one launch (was six copies / fills): host inputs are copied into copy 0
+  // first and the kernel then works in place
+  const double* Xs = X;
+  const double* ts = tau;
+  if (!(flags & ACS_DEVICE_PTRS)) {
+    ACS_HIP(ctx, hipMemcpyAsync(b.X, X, sizeof(double) * M * P, hipMemcpyHostToDevice, s));
+    if (tau) ACS_HIP(ctx, hipMemcpyAsync(b.tau, tau, sizeof(double) * d.NT, hipMemcpyHostToDevice, s));
+    Xs = b.X;
+    ts = tau ? b.tau : nullptr;
+  }
+  const size_t MP = (size_t)M * P;
+  const size_t nI = std::max(MP, (size_t)std::max(d.NT, GR));
+  hipLaunchKernelGGL(k_fte_init_state, dim3(acs_grid((int64_t)nI, 256)), dim3(256), 0, s, b.X, Xs, MP, b.tau, ts,
+                     d.NT, b.bad, b.dtau, GR);
+  ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }
 
