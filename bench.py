@@ -182,6 +182,19 @@ def main():
                         'gn_steps_mean': iters_mean, 'cost_before': rep['cost_before'],
                         'cost_after': rep['cost_after'], 'pos_rms_vs_truth_m': pos_rms},
     }
+    if pmc and pmc.get('fp64_flops') and pmc.get('valu_insts') and pmc.get('waves'):
+        # the same kernel against the FP64 VALU peak, and the issue rate of one wave: VALU
+        # instructions per wave (PMC) over the kernel's time in 2.4 GHz clocks
+        tfs = pmc['fp64_flops'] / (kern_ms * 1e-3) / 1e12
+        ipw = pmc['valu_insts'] / pmc['waves']
+        out['roofline_fp64'] = {'bound': 'fp64-valu', 'achieved': tfs, 'peak': FP64_VALU_PEAK_TFS,
+                                'unit': 'TFLOP/s', 'frac': tfs / FP64_VALU_PEAK_TFS,
+                                'flops_per_launch': pmc['fp64_flops'], 'valu_insts_per_wave': ipw,
+                                'clocks_per_valu_inst': kern_ms * 1e-3 * 2.4e9 / ipw,
+                                'source': pmc['source'],
+                                'note': 'one wave per busy SIMD: each wave issues its VALU stream serially, '
+                                        'so time ~ instructions per wave x issue interval (f64 FMA: 8 clocks '
+                                        'dependent latency, profiles/r01d/probes)'}
 
     if args.fte and world == 1:
         out['fte'] = bench_fte(ctx, torch, stream, n_frames=args.fte_frames,
@@ -221,7 +234,9 @@ def pmc_per_launch(kernel, grid):
     if r is None:
         return None, None
     root = os.path.dirname(os.path.abspath(__file__))
-    return r.get('hbm_bytes'), dict(fp64_flops=r.get('fp64_flops'), source=os.path.relpath(files[-1], root))
+    c = r.get('counters', {})
+    return r.get('hbm_bytes'), dict(fp64_flops=r.get('fp64_flops'), valu_insts=r.get('valu_insts'),
+                                    waves=c.get('SQ_WAVES'), source=os.path.relpath(files[-1], root))
 
 
 def _group(C):
