@@ -500,8 +500,8 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     // barrier per pivot. Thread (row gr = tid & 31, column group cg = tid >> 5) holds
     // aug[gr][cg + 16 j]; pivoting is implicit (rows stay in place, a row is "used" once it
     // has been a pivot). Step k: the 32 lanes owning column k pick the unused row with the
-    // largest |a[r][k]| (ties: lowest row), publish column k and the pivot row index in LDS;
-    // after the barrier every other row subtracts f_r = a[r][k] / a[pv][k] times the pivot
+    // largest |a[r][k]| (ties: lowest row), publish the row factors and the pivot row index
+    // in LDS; after the barrier every other row subtracts f_r = a[r][k] / a[pv][k] times the pivot
     // row (read from the owning lane of the same wave by v_readlane). Columns <= k of the
     // P x P block are finished and left stale. At the end row pv_k, divided by its pivot,
     // is the solution row k.
@@ -552,18 +552,21 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
             bi = (int)bx[0];
             take(b1, (int)bx[1]);
           }
-          colb[buf * 32 + gr] = colv;
+          // the column owner forms the row factors f_r = a[r][k] / a[pv][k] itself (slot
+          // pv carries the pivot), so after the barrier every lane needs two independent
+          // LDS reads and no division
+          const double p = read_lane_f64(colv, bi + 32 * half);
+          colb[buf * 32 + gr] = gr == bi ? p : colv / p;
           if (gr == 0) pvb[buf] = bi;
         }
         __syncthreads();
         const int pv = pvb[buf];
-        const double p = colb[buf * 32 + pv];
-        const double f = colb[buf * 32 + gr] / p;
+        const double f = colb[buf * 32 + gr];
         const bool piv = gr == pv;
         if (piv) {
           used = true;
           myk = k;
-          myp = p;
+          myp = f;
         }
         const bool upd = !piv && gr < P;
         const int src0 = pv, src1 = pv + 32;
