@@ -502,7 +502,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     // has been a pivot). Step k: the 32 lanes owning column k pick the unused row with the
     // largest |a[r][k]| (ties: lowest row), publish the row factors and the pivot row index
     // in LDS; after the barrier every other row subtracts f_r = a[r][k] / a[pv][k] times the pivot
-    // row (read from the owning lane of the same wave by v_readlane). Columns <= k of the
+    // row (read from the owning lane of the same wave by ds_bpermute). Columns <= k of the
     // P x P block are finished and left stale. At the end row pv_k, divided by its pivot,
     // is the solution row k.
     {
@@ -569,11 +569,11 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
           myp = f;
         }
         const bool upd = !piv && gr < P;
-        const int src0 = pv, src1 = pv + 32;
+        const int src = (pv + 32 * half) << 2;  // the pivot row's lane of this half-wave
 #pragma unroll
         for (int j = 0; j < NCG; ++j) {
-          const double r0 = read_lane_f64(av[j], src0), r1 = read_lane_f64(av[j], src1);
-          const double prow = half ? r1 : r0;
+          const double prow = __hiloint2double(__builtin_amdgcn_ds_bpermute(src, __double2hiint(av[j])),
+                                               __builtin_amdgcn_ds_bpermute(src, __double2loint(av[j])));
           const int c = cg + 16 * j;
           if (upd && (c > k)) av[j] = fma(-f, prow, av[j]);
         }
