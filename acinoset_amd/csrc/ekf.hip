@@ -532,7 +532,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
           double best = used ? -1.0 : fabs(colv);
           int bi = gr;
           auto take = [&](double ob, int oi) {
-            const bool t = ob > best || (ob == best && oi < bi);
+            const bool t = (ob > best) | ((ob == best) & (oi < bi));  // no short-circuit branches
             best = t ? ob : best;
             bi = t ? oi : bi;
           };
@@ -570,12 +570,17 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
         }
         const bool upd = !piv && gr < P;
         const int src = (pv + 32 * half) << 2;  // the pivot row's lane of this half-wave
+        // every permute is issued before the first wait, and the update is a select (a
+        // branch per column put one LDS round trip per column on the critical path)
+        double prow[NCG];
+#pragma unroll
+        for (int j = 0; j < NCG; ++j)
+          prow[j] = __hiloint2double(__builtin_amdgcn_ds_bpermute(src, __double2hiint(av[j])),
+                                     __builtin_amdgcn_ds_bpermute(src, __double2loint(av[j])));
 #pragma unroll
         for (int j = 0; j < NCG; ++j) {
-          const double prow = __hiloint2double(__builtin_amdgcn_ds_bpermute(src, __double2hiint(av[j])),
-                                               __builtin_amdgcn_ds_bpermute(src, __double2loint(av[j])));
-          const int c = cg + 16 * j;
-          if (upd && (c > k)) av[j] = fma(-f, prow, av[j]);
+          const double nv = fma(-f, prow[j], av[j]);
+          av[j] = (upd && (cg + 16 * j > k)) ? nv : av[j];
         }
       }
       __syncthreads();  // every thread past its last read of aug
