@@ -184,6 +184,27 @@ __device__ void ekf_fk_batch(const SkelView& sk, const double* ss, double eps, d
   __syncthreads();
 }
 
+// Row / column of the flat index e = tid, tid + nth, ... over rows of nc columns, stepped
+// without an integer division per element (nth / nc and nth % nc once per loop).
+struct Walk2 {
+  int e, r, c, de, dr, dc, nc;
+  __device__ Walk2(int tid, int nth, int nc_) : e(tid), de(nth), nc(nc_) {
+    r = tid / nc;
+    c = tid - r * nc;
+    dr = nth / nc;
+    dc = nth - dr * nc;
+  }
+  __device__ void next() {
+    e += de;
+    r += dr;
+    c += dc;
+    if (c >= nc) {
+      c -= nc;
+      ++r;
+    }
+  }
+};
+
 template <bool F32>
 __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __restrict__ I,
                                                     const double* __restrict__ Rl, const double* __restrict__ cams,
@@ -272,29 +293,31 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     }
     // F X: row block 0 += sT block 1 + sT^2/2 block 2, then block 1 += sT block 2 (each pass
     // reads only rows not yet updated); then the same on the columns for (F X) F^T
-    for (int e = tid; e < P * n; e += nth) {
-      const int r = e / n, c = e % n;
+    for (Walk2 w(tid, nth, n); w.e < P * n; w.next()) {
+      const int r = w.r, c = w.c;
       sP[r * LDP + c] += sT * sP[(r + P) * LDP + c] + h2 * sP[(r + 2 * P) * LDP + c];
     }
     __syncthreads();
-    for (int e = tid; e < P * n; e += nth) {
-      const int r = P + e / n, c = e % n;
+    for (Walk2 w(tid, nth, n); w.e < P * n; w.next()) {
+      const int r = P + w.r, c = w.c;
       sP[r * LDP + c] += sT * sP[(r + P) * LDP + c];
     }
     __syncthreads();
-    for (int e = tid; e < P * n; e += nth) {
-      const int r = e / P, c = e % P;
+    for (Walk2 w(tid, nth, P); w.e < P * n; w.next()) {
+      const int r = w.r, c = w.c;
       sP[r * LDP + c] += sT * sP[r * LDP + c + P] + h2 * sP[r * LDP + c + 2 * P];
     }
     __syncthreads();
-    for (int e = tid; e < P * n; e += nth) {
-      const int r = e / P, c = P + e % P;
+    for (Walk2 w(tid, nth, P); w.e < P * n; w.next()) {
+      const int r = w.r, c = P + w.c;
       sP[r * LDP + c] += sT * sP[r * LDP + c + P];
     }
     __syncthreads();
-    for (int e = tid; e < n * n; e += nth) sP[(e / n) * LDP + e % n] += Q[e];
-    __syncthreads();
-    for (int e = tid; e < n * n; e += nth) Ppred[fo * n * n + e] = sP[(e / n) * LDP + e % n];
+    for (Walk2 w(tid, nth, n); w.e < n * n; w.next()) {  // + Q, stored as P_pred (own elements)
+      const double v = sP[w.r * LDP + w.c] + Q[w.e];
+      sP[w.r * LDP + w.c] = v;
+      Ppred[fo * n * n + w.e] = v;
+    }
 
     EKF_TICK(1);
     // ---- 2. poses of the forward-difference Jacobian --------------------------------
@@ -604,7 +627,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     wg_mgemm<false, false>(sP, LDP, sPx, Pp, aug + Pp, AW, d.npad, d.npad, Pp, -1.0, 1.0);
     EKF_TICK(7);
     if (tid < n) xest[fo * n + tid] = ss[tid];
-    for (int e = tid; e < n * n; e += nth) Pest[fo * n * n + e] = sP[(e / n) * LDP + e % n];
+    for (Walk2 w(tid, nth, n); w.e < n * n; w.next()) Pest[fo * n * n + w.e] = sP[w.r * LDP + w.c];
     __syncthreads();
   }
 #ifdef EKF_PROFILE
