@@ -546,10 +546,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       for (int k = 0; k < P; ++k) {
         const int buf = k & 1;
         if (cg == (k & 15)) {
-          const int jk = k >> 4;
-          double colv = av[0];
-#pragma unroll
-          for (int j = 1; j < NCG; ++j) colv = (j == jk) ? av[j] : colv;
+          const double colv = (k >> 4) ? av[1] : av[0];  // k < P <= FK_MAXP = 32 (checked on entry)
           // arg max over the 32 lanes on the VALU: DPP inside each 16-lane row, then the
           // row pair by v_permlane16_swap ((max, lowest row) is commutative and associative)
           double best = used ? -1.0 : fabs(colv);
