@@ -98,6 +98,8 @@ class SbaExtReport(C.Structure):
         return d
 
 
+# must equal ACS_ABI_VERSION in include/acinoset_hip.h (checked when the library loads)
+ABI_VERSION = 2
 _lib = None
 _lock = threading.Lock()
 _P = C.c_void_p
@@ -176,6 +178,10 @@ def load_library():
                     '(hipcc --offload-arch=gfx950). There is no CPU fallback.')
             lib = C.CDLL(LIB_PATH)
             _declare(lib)
+            got = lib.acs_abi_version()
+            if got != ABI_VERSION:
+                raise NativeUnavailable(f'{LIB_PATH} has C ABI version {got}, this package needs {ABI_VERSION} '
+                                        '(include/acinoset_hip.h ACS_ABI_VERSION): rebuild the library')
             _lib = lib
     return _lib
 

@@ -35,13 +35,14 @@ void* acs_ws(acs_ctx* ctx, int slot, size_t bytes) {
 }
 
 void* acs_pinned(acs_ctx* ctx, size_t bytes) {
-  if (!ctx->snap_ev[0]) {
-    for (auto& e : ctx->snap_ev) {
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-        e = nullptr;
-        acs_fail(ctx, ACS_E_HIP, "hipEventCreateWithFlags failed");
-        return nullptr;
-      }
+  // every snapshot event is checked on its own: a partial failure on an earlier call
+  // leaves the missing ones null and they are created here on the next call
+  for (auto& e : ctx->snap_ev) {
+    if (e) continue;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      e = nullptr;
+      acs_fail(ctx, ACS_E_HIP, "hipEventCreateWithFlags failed");
+      return nullptr;
     }
   }
   if (ctx->pinned_bytes >= bytes) return ctx->pinned;

@@ -131,7 +131,9 @@ __device__ void fk_frame(const SkelView& s, const double* x, FkShared& sh, int t
   FK_MARK(25);
   // translation parameters, summed once per frame instead of once per node chain, from the
   // LDS copy (a loop of global loads here was a chain of cache round trips) by the last two
-  // threads, which the joint loop below leaves idle when nth >= J + 2
+  // threads; the joint loop below runs over 3*J (joint, column) items, so these two are
+  // idle there only when nth >= 3*J + 2 (with fewer threads they take joint items too, after
+  // their sums, which is still correct)
   if (tid >= nth - 2) {
     const int kind = tid == nth - 2 ? PK_TRANS : PK_WORLD;
     double t[3] = {0.0, 0.0, 0.0};

@@ -75,6 +75,26 @@ def lm_loop2(ranks, allreduce):
             return st[0]
 
 
+def _check_dev(torch, dev, device, table, N, Cn):
+    """The HBM-resident inputs of a rank go to the C ABI as raw pointers: check what the
+    kernels assume (device, dtype, contiguity, element counts) before handing them over."""
+    want = {'ints': (torch.int32, len(table.ints)), 'reals': (torch.float64, len(table.reals)),
+            'cams': (torch.float64, Cn * _native.ACS_CAM_STRIDE), 'meas': (torch.float64, N * Cn * table.L * 2),
+            'w': (torch.float64, N * Cn * table.L), 'qinv': (torch.float64, table.P),
+            'X': (torch.float64, (N + 2) * table.P), 'tau': (torch.float64, Cn)}
+    for k, (dt, n) in want.items():
+        t = dev.get(k)
+        if t is None:
+            raise ValueError(f'dev[{k!r}] missing')
+        if t.device.type != 'cuda' or t.device.index != device:
+            raise ValueError(f'dev[{k!r}] is on {t.device}, the context is on cuda:{device}')
+        if t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f'dev[{k!r}] must be a contiguous {dt} tensor (got {t.dtype}, '
+                             f'contiguous={t.is_contiguous()})')
+        if t.numel() != n:
+            raise ValueError(f'dev[{k!r}] has {t.numel()} elements, expected {n}')
+
+
 class HipFteRank:
     """One rank of the distributed solve on a HIP context (payloads are torch device
     tensors, so torch.distributed can reduce them in place)."""
@@ -100,6 +120,7 @@ class HipFteRank:
             n_ints, n_reals, flags = len(ints), len(reals), 0
         else:
             N, Cn = int(np.shape(meas)[0]), int(np.shape(meas)[1])
+            _check_dev(torch, dev, ctx.device, table, N, Cn)
             ptrs = [C.c_void_p(dev[k].data_ptr()) for k in ('ints', 'reals', 'cams', 'meas', 'w', 'qinv', 'X', 'tau')]
             n_ints, n_reals, flags = dev['ints'].numel(), dev['reals'].numel(), _native.ACS_DEVICE_PTRS
         self.N, self.P, self.C = N, table.P, Cn

@@ -22,18 +22,21 @@ from .utils import get_pairwise_3d_points_from_df, load_manual_points, load_poin
 
 def create_bundle_adjustment_jacobian_sparsity_matrix(n_cams, n_params_per_camera, camera_indices, n_points,
                                                       point_indices):
-    """`src/lib/sba.py:11-22` (sparsity metadata; the GPU solver does not need it)."""
-    from scipy.sparse import lil_matrix
-    m = camera_indices.size * 2
-    n = n_cams * n_params_per_camera + n_points * 3
-    A = lil_matrix((m, n), dtype=int)
-    i = np.arange(camera_indices.size)
-    for s in range(n_params_per_camera):
-        A[2 * i, camera_indices * n_params_per_camera + s] = 1
-        A[2 * i + 1, camera_indices * n_params_per_camera + s] = 1
-    for s in range(3):
-        A[2 * i, n_cams * n_params_per_camera + point_indices * 3 + s] = 1
-        A[2 * i + 1, n_cams * n_params_per_camera + point_indices * 3 + s] = 1
+    """The Jacobian sparsity pattern of `src/lib/sba.py:11-22` as metadata (the GPU solver
+    works on the per-point blocks directly and never builds it): residual rows 2i, 2i+1 of
+    observation i touch its camera's parameter columns and its point's 3 columns, laid
+    out [cameras | points]. Built in one COO pass and returned as a lil matrix of ints."""
+    from scipy.sparse import coo_matrix
+    cam = np.asarray(camera_indices, np.int64)
+    pt = np.asarray(point_indices, np.int64)
+    n_obs = cam.size
+    cols_per_obs = np.concatenate([cam[:, None] * n_params_per_camera + np.arange(n_params_per_camera),
+                                   n_cams * n_params_per_camera + pt[:, None] * 3 + np.arange(3)], 1)
+    k = cols_per_obs.shape[1]
+    rows = (2 * np.arange(n_obs)[:, None, None] + np.arange(2)[None, :, None]).repeat(k, 2)
+    cols = np.broadcast_to(cols_per_obs[:, None, :], rows.shape)
+    shape = (2 * n_obs, n_cams * n_params_per_camera + 3 * n_points)
+    A = coo_matrix((np.ones(rows.size, int), (rows.ravel(), cols.ravel())), shape=shape).tolil()
     return A
 
 

@@ -127,30 +127,66 @@ def _read_dlc(path):
                           'or install tables') from e
 
 
+# the head-detector outputs (`dlc_head` in the first path, src/lib/utils.py:84-103): three
+# generic body parts renamed, a fourth ('objectA') dropped, markers kept in this order
+DLC_HEAD_PARTS = {'bodypart1': 'r_eye', 'bodypart2': 'l_eye', 'bodypart3': 'nose'}
+DLC_HEAD_ORDER = ('nose', 'r_eye', 'l_eye')
+
+
+def _frame_from_label(label):
+    """DLC image-path row label 'labeled-data/.../img0042.png' -> 42 (`int(s[-7:-4])`). An
+    integer label (a video-analysis row number) is kept; the reference would fail on it."""
+    if isinstance(label, (int, np.integer)):
+        return int(label)
+    return int(str(label)[-7:-4])
+
+
 def load_dlc_points_as_df(dlc_df_fpaths, frame_shifts=None, verbose=False):
-    """`src/lib/utils.py:77-151` for standard DLC outputs (scorer/bodyparts/coords columns):
+    """`src/lib/utils.py:77-151`: per-camera DLC tables (scorer/bodyparts/coords columns) ->
     long DataFrame [frame, camera, marker, x, y, likelihood], camera-major, then frame, then
-    marker in sorted order (the reference's `.T.unstack().T` sorts the bodyparts level,
-    :115). A missing likelihood column becomes 1 where x is finite (:98-110). A frame shift
-    moves every marker's (x, y, likelihood) by that many frames; the frames shifted in are
-    NaN with likelihood 0 and the frame column is not shifted (:118-132)."""
-    assert frame_shifts is None or len(dlc_df_fpaths) == len(frame_shifts)
+    marker. Pinned to the reference function itself by `tests/golden/dlc.npz`. Three input
+    branches, as in the reference:
+    * a likelihood column present: rows keep their index as the frame, markers sorted (the
+      reference's `.T.unstack().T` orders the bodyparts level, :120);
+    * no likelihood column (:104-117): likelihood = 1 where y is present, 0 where it is NaN;
+      the frame is parsed from the image-path row label;
+    * `dlc_head` in the FIRST path (:84-103, applied to every file): bodypart1/2/3 renamed
+      r_eye/l_eye/nose, objectA dropped, likelihood = 1 where x is present, markers in the
+      order nose, r_eye, l_eye, frames from the row labels.
+    A frame shift moves every marker's (x, y, likelihood) by that many frames; the frames
+    shifted in are NaN with likelihood 0 and the frame column is not shifted (:124-137)."""
+    assert frame_shifts is None or len(dlc_df_fpaths) == len(frame_shifts), \
+        '`frame_shifts` should be the same size with `dlc_df_fpaths`'
+    head = len(dlc_df_fpaths) > 0 and 'dlc_head' in dlc_df_fpaths[0]
     out = []
     for i, path in enumerate(dlc_df_fpaths):
         df = _read_dlc(path)
         df = df.droplevel(0, axis=1)                        # scorer
-        parts = sorted(dict.fromkeys(df.columns.get_level_values(0)))
         coords = set(df.columns.get_level_values(1))
         idx = df.index
-        frames = np.array([int(str(s)[-7:-4]) if not np.issubdtype(type(s), np.integer) else int(s) for s in idx])
+        if head:
+            df = df.rename(columns=DLC_HEAD_PARTS, level=0)
+            parts = list(DLC_HEAD_ORDER)
+            lik_from = 'x'
+            frames = np.array([_frame_from_label(s) for s in idx])
+        elif 'likelihood' not in coords:
+            parts = sorted(dict.fromkeys(df.columns.get_level_values(0)))
+            lik_from = 'y'
+            frames = np.array([_frame_from_label(s) for s in idx])
+        else:
+            parts = sorted(dict.fromkeys(df.columns.get_level_values(0)))
+            lik_from = None
+            frames = np.asarray(idx)
         shift = 0 if frame_shifts is None else int(frame_shifts[i])
         n, L = len(frames), len(parts)
         vals = np.full((3, n, L), np.nan)
         for j, bp in enumerate(parts):
-            x = df[(bp, 'x')].to_numpy(np.float64)
-            vals[0, :, j] = x
+            vals[0, :, j] = df[(bp, 'x')].to_numpy(np.float64)
             vals[1, :, j] = df[(bp, 'y')].to_numpy(np.float64)
-            vals[2, :, j] = df[(bp, 'likelihood')].to_numpy(np.float64) if 'likelihood' in coords else np.isfinite(x)
+            if lik_from is None:
+                vals[2, :, j] = df[(bp, 'likelihood')].to_numpy(np.float64)
+            else:
+                vals[2, :, j] = np.isfinite(vals[0 if lik_from == 'x' else 1, :, j])
         if shift:
             sh = np.full_like(vals, np.nan)
             if shift > 0:

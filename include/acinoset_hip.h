@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ACS_ABI_VERSION 1
+#define ACS_ABI_VERSION 2
 #define ACS_CAM_STRIDE 20
 
 /* status codes */

@@ -518,8 +518,80 @@ def fte_fixture(name, mode, n_frames, cams, sd, sd_mode, intermode, start_frame=
           f'objective {rec["pt0"]["obj"]:.6f}, reference build+eval {dt:.1f}s')
 
 
+def _dlc_frames(seed, parts, n, scorer, coords=('x', 'y', 'likelihood'), str_index=False, nan_frac=0.15):
+    """A synthetic DLC output table: MultiIndex columns (scorer, bodyparts, coords), rows =
+    frames (int) or DLC image paths ('labeled-data/.../img0042.png')."""
+    import pandas as pd
+    rng = np.random.default_rng(seed)
+    cols = pd.MultiIndex.from_tuples([(scorer, bp, c) for bp in parts for c in coords],
+                                     names=['scorer', 'bodyparts', 'coords'])
+    v = np.empty((n, len(cols)))
+    for j, (_, bp, c) in enumerate(cols):
+        v[:, j] = rng.uniform(0.0, 1.0, n) if c == 'likelihood' else rng.uniform(0, 2000, n)
+    # x and y go missing together mostly, alone sometimes (the reference derives a missing
+    # likelihood from y in the plain branch, :111-113, and from x in the dlc_head branch, :88-91)
+    miss = rng.uniform(size=(n, len(parts))) < nan_frac
+    alone = rng.integers(0, 4, size=(n, len(parts)))          # 0: only x, 1: only y, else both
+    for k, bp in enumerate(parts):
+        for j, (_, b, c) in enumerate(cols):
+            if b == bp and c in ('x', 'y'):
+                drop = miss[:, k] & ((alone[:, k] >= 2) | (alone[:, k] == (0 if c == 'x' else 1)))
+                v[drop, j] = np.nan
+    idx = [f'labeled-data/cam/img{i + 3:04d}.png' for i in range(n)] if str_index else np.arange(n)
+    return pd.DataFrame(v, index=idx, columns=cols)
+
+
+def dlc_fixture():
+    """`load_dlc_points_as_df` (src/lib/utils.py:77-151), the reference function itself, on
+    synthetic DLC tables handed to it through a patched `pandas.read_hdf` (PyTables is not
+    installed, and the reference ships no .h5 file). Cases: standard 3-coord files,
+    files without a likelihood column (image-path index), the `dlc_head` branch
+    (:84-103) and frame shifts (:124-135). The fixture holds each case's input tables and
+    the reference's output columns."""
+    import pandas as pd
+    parts = ['nose', 'r_eye', 'l_eye', 'neck_base', 'spine', 'tail_base']
+    cases = {
+        'standard': ([_dlc_frames(1, parts, 9, 'DLC_resnet50'), _dlc_frames(2, parts, 9, 'DLC_resnet50')],
+                     ['cam1DLC.h5', 'cam2DLC.h5'], None),
+        'nolik': ([_dlc_frames(3, parts, 7, 'DLC_x', coords=('x', 'y'), str_index=True),
+                   _dlc_frames(4, parts, 7, 'DLC_x', coords=('x', 'y'), str_index=True)],
+                  ['cam1.h5', 'cam2.h5'], None),
+        'shifted': ([_dlc_frames(5, parts, 8, 'DLC_resnet50') for _ in range(3)],
+                    ['cam1DLC.h5', 'cam2DLC.h5', 'cam3DLC.h5'], [2, 0, -1]),
+        'head': ([_dlc_frames(6 + c, ['bodypart1', 'bodypart2', 'bodypart3', 'objectA'], 6, '2019-03-09_lily_run',
+                              coords=('x', 'y'), str_index=True) for c in range(2)],
+                 ['/data/dlc_head/cam1.h5', '/data/dlc_head/cam2.h5'], None),
+    }
+    out = {}
+    orig = pd.read_hdf
+    for name, (tables, paths, shifts) in cases.items():
+        by_path = dict(zip(paths, tables))
+        pd.read_hdf = lambda p, *a, **k: by_path[p].copy()
+        try:
+            ref = ref_utils.load_dlc_points_as_df(paths, frame_shifts=shifts)
+        finally:
+            pd.read_hdf = orig
+        for c, (p, t) in enumerate(zip(paths, tables)):
+            out[f'{name}_in{c}_values'] = t.to_numpy(np.float64)
+            out[f'{name}_in{c}_columns'] = np.array(['|'.join(col) for col in t.columns])
+            out[f'{name}_in{c}_index'] = np.array([str(s) for s in t.index])
+            out[f'{name}_in{c}_int_index'] = np.array(not isinstance(t.index[0], str))
+            out[f'{name}_in{c}_path'] = np.array(p)
+        out[f'{name}_ncams'] = np.array(len(paths))
+        out[f'{name}_shifts'] = np.array(shifts if shifts is not None else [], np.int64)
+        out[f'{name}_out_frame'] = np.array([str(f) for f in ref['frame']])
+        out[f'{name}_out_camera'] = ref['camera'].to_numpy(np.int64)
+        out[f'{name}_out_marker'] = np.array([str(m) for m in ref['marker']])
+        for k in ('x', 'y', 'likelihood'):
+            out[f'{name}_out_{k}'] = ref[k].to_numpy(np.float64)
+        print(f'dlc {name}: {len(ref)} rows, cams {len(paths)}, shifts {shifts}')
+    np.savez_compressed(os.path.join(HERE, 'dlc.npz'), **out)
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['loss', 'fk', 'tri', 'cfg1', 'cfg2', 'ext']
+    if 'dlc' in which:
+        dlc_fixture()
     if 'fte' in which:
         fte_fixture('fte_head_const', 'head', 8, range(6), True, 'const', 'vel')
         fte_fixture('fte_default_const', 'default', 5, range(6), True, 'const', 'vel')

@@ -109,58 +109,24 @@ def test_states_variable_shutter_delay_layout():
     assert np.array_equal(np.asarray(st['shutter_delay']), tau.T)
 
 
-def _dlc_csv(path, parts, n, seed, likelihood=True, str_index=False):
-    """A DLC-style export: 3 header rows (scorer / bodyparts / coords), one row per frame."""
-    rng = np.random.default_rng(seed)
-    coords = ['x', 'y', 'likelihood'] if likelihood else ['x', 'y']
-    cols = pd.MultiIndex.from_product([['DLC_resnet50_cheetahOct1shuffle1_200000'], parts, coords],
-                                      names=['scorer', 'bodyparts', 'coords'])
-    v = rng.uniform(0, 1000, (n, len(cols)))
-    v[rng.random(v.shape) < 0.05] = np.nan
-    idx = [f'labeled-data/run/img{k:03d}.png' for k in range(n)] if str_index else np.arange(n)
-    df = pd.DataFrame(v, index=idx, columns=cols)
-    df.to_csv(path)
-    return df
-
-
-def _expected_long(df, cam, shift):
-    """Row-by-row restatement of src/lib/utils.py:77-151 on one file: markers in sorted order
-    within a frame (the `.T.unstack().T` reshape sorts the bodyparts level, :115), rows moved
-    by `shift` frames with NaN / likelihood 0 shifted in (:118-132), frame column unshifted."""
-    d = df.droplevel(0, axis=1)
-    parts = sorted(set(d.columns.get_level_values(0)))
-    has_lk = 'likelihood' in set(d.columns.get_level_values(1))
-    n = len(d)
-    frames = [int(str(s)[-7:-4]) if isinstance(s, str) else int(s) for s in d.index]
-    rows = []
-    for k in range(n):
-        src = k - shift
-        for bp in parts:
-            if 0 <= src < n:
-                x, y = d[(bp, 'x')].iloc[src], d[(bp, 'y')].iloc[src]
-                lk = d[(bp, 'likelihood')].iloc[src] if has_lk else (0.0 if np.isnan(x) else 1.0)
-            else:
-                x = y = lk = np.nan
-            rows.append((frames[k], cam, bp, x, y, 0.0 if np.isnan(lk) else lk))
-    return pd.DataFrame(rows, columns=['frame', 'camera', 'marker', 'x', 'y', 'likelihood'])
-
-
-@pytest.mark.parametrize('shifts', [None, [0, 2, -3]])
-def test_load_dlc_points_as_df_matches_reference_reshape(tmp_path, shifts):
+@pytest.mark.parametrize('name', ['standard', 'shifted'])
+def test_load_dlc_csv_route_matches_reference(tmp_path, name):
+    """DLC's .csv export of the same tables (the route on boxes without PyTables) gives what
+    the reference function made of the .h5 tables (tests/golden/dlc.npz)."""
     from acinoset_amd.lib import utils as lu
-    parts = ['nose', 'r_eye', 'l_eye', 'neck_base', 'tail_tip']
-    paths, dfs = [], []
-    for c in range(3):
-        p = str(tmp_path / f'cam{c + 1}DLC.csv')
-        dfs.append(_dlc_csv(p, parts, 12, seed=c, likelihood=(c != 1), str_index=(c == 2)))
-        paths.append(p)
-    got = lu.load_dlc_points_as_df(paths, frame_shifts=shifts)
-    exp = pd.concat([_expected_long(df, c, 0 if shifts is None else shifts[c]) for c, df in enumerate(dfs)],
-                    ignore_index=True)
-    assert list(got.columns) == ['frame', 'camera', 'marker', 'x', 'y', 'likelihood']
-    assert got[['frame', 'camera', 'marker']].astype(str).equals(exp[['frame', 'camera', 'marker']].astype(str))
+    from tests.test_dlc_reference import GOLD, _inputs
+    d = np.load(GOLD)
+    tables, paths, shifts = _inputs(d, name)
+    csvs = []
+    for k, p in enumerate(paths):
+        q = str(tmp_path / f'cam{k + 1}DLC.csv')
+        tables[p].to_csv(q)
+        csvs.append(q)
+    got = lu.load_dlc_points_as_df(csvs, frame_shifts=shifts)
+    np.testing.assert_array_equal(np.array([str(f) for f in got['frame']]), d[f'{name}_out_frame'])
+    np.testing.assert_array_equal(np.array([str(m) for m in got['marker']]), d[f'{name}_out_marker'])
     for col in ('x', 'y', 'likelihood'):
-        np.testing.assert_allclose(got[col].to_numpy(float), exp[col].to_numpy(float), rtol=0, atol=1e-9,
+        np.testing.assert_allclose(got[col].to_numpy(float), d[f'{name}_out_{col}'], rtol=0, atol=1e-9,
                                    equal_nan=True)
 
 
@@ -197,3 +163,22 @@ def test_all_optimizations_frame_range_matches_reference(seed):
     df['likelihood'] = lik
     filt = df.query('likelihood > 0.8')
     assert ao.auto_frame_range(filt, get_markers('head')) == _reference_frame_range(filt, get_markers('head'))
+
+
+def test_sparsity_pattern_metadata():
+    """`create_bundle_adjustment_jacobian_sparsity_matrix` (src/lib/sba.py:11-22): rows 2i,
+    2i+1 touch observation i's camera block and its point's 3 columns, [cameras | points]."""
+    from acinoset_amd.lib.sba import create_bundle_adjustment_jacobian_sparsity_matrix as sparsity
+    rng = np.random.default_rng(5)
+    n_cams, n_pts, n_obs, pc = 4, 7, 25, 6
+    cam = rng.integers(0, n_cams, n_obs)
+    pt = rng.integers(0, n_pts, n_obs)
+    A = sparsity(n_cams, pc, cam, n_pts, pt)
+    D = np.zeros((2 * n_obs, n_cams * pc + 3 * n_pts), int)
+    for i in range(n_obs):
+        for r in (2 * i, 2 * i + 1):
+            D[r, cam[i] * pc:(cam[i] + 1) * pc] = 1
+            D[r, n_cams * pc + 3 * pt[i]:n_cams * pc + 3 * pt[i] + 3] = 1
+    assert A.shape == D.shape
+    np.testing.assert_array_equal(A.toarray(), D)
+    assert sparsity(n_cams, 0, cam, n_pts, pt).shape == (2 * n_obs, 3 * n_pts)
