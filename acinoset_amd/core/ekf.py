@@ -58,6 +58,14 @@ def process_covariance(P, sT):
                      [sT ** 2 / 2 * qb, sT * qb, qb]])
 
 
+def ring_cal_covs(n_cams):
+    """Calibration covariances for a rig of `n_cams` cameras: the reference's six values
+    (src/core/ekf.py:210) for six cameras; for other rigs (the synthetic 12-camera ring of
+    configs[4], which has no calibration of its own) camera c takes the reference's value of
+    camera c mod 6. The reference itself asserts six cameras (:213)."""
+    return [CAL_COVS[c % len(CAL_COVS)] for c in range(n_cams)]
+
+
 def measurement_std(n_cams, cal_covs=None):
     """Per-camera pixel std of R (src/core/ekf.py:244-248): dlc_cov + 2 cov_c / min(cov).
     The reference hard-codes 6 cameras (:213); other rigs pass their own `cal_covs`."""
@@ -126,8 +134,10 @@ def run(meas, likelihood, camera_params, mode, fps, s0, dlc_thresh=0.5, ref_nume
 
 
 def ekf(DATA_DIR, points_2d_df, marker_mode, camera_params, start_frame, end_frame, dlc_thresh, scene_fpath,
-        params: Dict = {}, ref_numerics=True) -> str:
-    """`src/core/ekf.py:26` signature and outputs (OUT_DIR/ekf/ekf.pickle)."""
+        params: Dict = {}, ref_numerics=True, cal_covs=None) -> str:
+    """`src/core/ekf.py:26` signature and outputs (OUT_DIR/ekf/ekf.pickle). `cal_covs`
+    (extension): per-camera calibration covariances; None = the reference's six values,
+    or `ring_cal_covs(n_cams)` for a rig that is not six cameras."""
     OUT_DIR = os.path.join(DATA_DIR, 'ekf')
     os.makedirs(OUT_DIR, exist_ok=True)
     app.start_logging(os.path.join(OUT_DIR, 'ekf.log'))
@@ -145,8 +155,11 @@ def ekf(DATA_DIR, points_2d_df, marker_mode, camera_params, start_frame, end_fra
     n_total = int(points_2d_df['frame'].max()) + 1
     meas, lik = dense_observations(points_2d_df, markers, n_cams, max(n_total, end_frame + 1))
     t0 = time()
+    if cal_covs is None and n_cams != len(CAL_COVS):
+        cal_covs = ring_cal_covs(n_cams)
+        print(f'\t{n_cams} cameras: calibration covariances {cal_covs} (reference values by camera mod 6)')
     out = run(meas[start_frame:end_frame + 1], lik[start_frame:end_frame + 1], camera_params, marker_mode, fps, s0,
-              dlc_thresh, ref_numerics)
+              dlc_thresh, ref_numerics, cal_covs=cal_covs)
     opt_time = time() - t0
     app.stop_logging()
     xe, xs = out['x_est'], out['x_smooth']

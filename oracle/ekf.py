@@ -120,9 +120,12 @@ def initial_state(mode, frames, markers_idx, xyz, start_frame, sT):
     return s
 
 
-def ekf(meas, likelihood, K, D, R, t, mode, fps, s0, thresh=0.5, max_pixel_err=2704.0, ref_numerics=True):
+def ekf(meas, likelihood, K, D, R, t, mode, fps, s0, thresh=0.5, max_pixel_err=2704.0, ref_numerics=True,
+        cal_covs=None):
     """meas (N, C, L, 2) pixels (NaN = missing), likelihood (N, C, L). Returns a dict with
-    the filtered / predicted / smoothed states and covariances and the outlier count."""
+    the filtered / predicted / smoothed states and covariances and the outlier count.
+    `cal_covs`: per-camera calibration covariances (default: the reference's six, :210;
+    the reference asserts six cameras, :213, other rigs pass their own)."""
     N, C, L, _ = meas.shape
     P = len(POSE[mode])
     n = 3 * P
@@ -130,8 +133,9 @@ def ekf(meas, likelihood, K, D, R, t, mode, fps, s0, thresh=0.5, max_pixel_err=2
     F = transition(P, sT)
     Q = process_noise(P, sT)
     Pm = initial_covariance(mode)
-    assert C == len(CAL_COVS)
-    base = np.repeat([2 * c / min(CAL_COVS) for c in CAL_COVS], 2 * L)
+    covs = CAL_COVS if cal_covs is None else list(cal_covs)
+    assert C == len(covs), (C, len(covs))
+    base = np.repeat([2 * c / min(covs) for c in covs], 2 * L)
     s = np.asarray(s0, np.float64)
     out = dict(x_est=np.zeros((N, n)), x_pred=np.zeros((N, n)), P_est=np.zeros((N, n, n)), P_pred=np.zeros((N, n, n)))
     outliers = 0

@@ -38,6 +38,7 @@ LM spec (shared with the GPU):
 """
 import numpy as np
 import scipy.sparse as sp
+import scipy.linalg as sla
 import scipy.sparse.linalg as spla
 
 from . import kinematics as okin
@@ -280,8 +281,45 @@ def active_bounds(prob, tau, g):
     return prob.M * prob.P + np.flatnonzero(act)
 
 
+def _solve_step(prob, A, b):
+    """Solve the damped normal equations A d = b (A SPD). Unknowns are ordered [X rows frame
+    by frame | tau]. With a per-camera tau the X block is banded (a frame couples frames up
+    to 3 away: half-bandwidth 4P - 1) with a C-column border, so it is a banded Cholesky
+    (LAPACK pbtrf/pbtrs) plus a C x C Schur complement; with a per-frame tau (N*C border
+    columns) a sparse LU."""
+    if prob.var or not prob.sd:
+        if not prob.sd:
+            return sla.solveh_banded(_upper_band(A, prob.M * prob.P, 4 * prob.P - 1), b)
+        return spla.spsolve(A, b)
+    nx = prob.M * prob.P
+    ab = _upper_band(A, nx, 4 * prob.P - 1)
+    Axt = A[:nx, nx:].toarray()
+    Z = sla.solveh_banded(ab, np.column_stack([b[:nx], Axt]))
+    S = A[nx:, nx:].toarray() - Axt.T @ Z[:, 1:]
+    dt = np.linalg.solve(S, b[nx:] - Axt.T @ Z[:, 0])
+    return np.concatenate([Z[:, 0] - Z[:, 1:] @ dt, dt])
+
+
+def _upper_band(A, n, u):
+    """Upper band storage ab[u + i - j, j] = A[i, j] (i <= j) of A[:n, :n]."""
+    c = A[:n, :n].tocoo()
+    m = c.row <= c.col
+    if m.any() and int((c.col[m] - c.row[m]).max()) > u:
+        raise ValueError('normal matrix wider than the assumed time band')
+    ab = np.zeros((u + 1, n))
+    np.add.at(ab, (u + c.row[m] - c.col[m], c.col[m]), c.data[m])
+    return ab
+
+
 def solve(prob, X0, tau0=None, max_iters=200, ftol=1e-12, xtol=1e-12, gtol=1e-8, lam0=1e-3, verbose=False):
-    """LM of the module docstring. Returns (X, tau, info)."""
+    """LM of the module docstring. Returns (X, tau, info). BLAS runs on one thread: the
+    banded factorisation of a 104-wide band is 10x slower with a thread team (OpenBLAS)."""
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(1, user_api='blas'):
+        return _solve(prob, X0, tau0, max_iters, ftol, xtol, gtol, lam0, verbose)
+
+
+def _solve(prob, X0, tau0, max_iters, ftol, xtol, gtol, lam0, verbose):
     X = np.array(X0, np.float64).reshape(prob.M, prob.P)
     tau = np.zeros(prob.tau_shape) if tau0 is None else np.array(tau0, np.float64).reshape(prob.tau_shape)
     tau[..., 0] = 0.0
@@ -304,12 +342,14 @@ def solve(prob, X0, tau0=None, max_iters=200, ftol=1e-12, xtol=1e-12, gtol=1e-8,
             status = 'gtol'
             break
         dg = H.diagonal()
-        A = (H + sp.diags(lam * np.maximum(dg, 1e-12))).tolil()
+        A = (H + sp.diags(lam * np.maximum(dg, 1e-12))).tocsc()
         if pin is not None:
-            A[pin, :] = 0.0
-            A[:, pin] = 0.0
-            A[pin, pin] = 1.0
-        d = spla.spsolve(A.tocsc(), -gp)
+            # pinned unknowns: their rows and columns replaced by the identity (a diagonal
+            # mask on both sides, so the matrix stays in CSC)
+            keep = np.ones(prob.nv)
+            keep[pin] = 0.0
+            A = (sp.diags(keep) @ A @ sp.diags(keep) + sp.diags(1.0 - keep)).tocsc()
+        d = _solve_step(prob, A, -gp)
         dX, dtau = prob.unpack(d)
         Xn = X + dX
         taun = np.clip(tau + dtau, -prob.Ts, prob.Ts) if prob.sd else tau

@@ -112,3 +112,67 @@ def test_core_ekf_dropin_writes_pickle(ctx, tmp_path):
     pos = np.array(d['smoothed_positions'])[:, :3]
     err = np.sqrt(np.mean(np.sum((pos - seq.pos3d[:, 0, :3]) ** 2, -1)))
     assert err < 0.05, err
+
+
+# ---- 12-camera ring (configs[4]): the reference's filter generalised to C cameras --------
+def _setup_ring(mode, N, n_cams=12, seed=61):
+    from acinoset_amd import synth
+    scene = synth.ring_scene(n_cams)
+    seq = synth.make_sequence(N, scene, mode=mode, seed=seed)
+    uv, lik = seq.uv, seq.likelihood
+    L = uv.shape[2]
+    valid = (lik > 0.5) & np.isfinite(uv).all(-1)
+    fr, ca, mk = np.nonzero(valid)
+    fr_, mk_, xyz = fisheye.pairwise_points(fr, ca, mk, uv[fr, ca, mk, 0], uv[fr, ca, mk, 1], scene.K, scene.D,
+                                            scene.R, scene.t)
+    s0 = oekf.initial_state(mode, fr_, mk_, xyz, 0, 1 / 90.0)
+    cp = (scene.K, scene.D, scene.R, scene.t, tuple(scene.res), n_cams)
+    assert L == len(pkin.get_markers(mode))
+    return scene, seq, s0, cp, cekf.ring_cal_covs(n_cams)
+
+
+@pytest.mark.parametrize('mode,N', [('head', 40), ('default', 8)])
+def test_ekf_12cam_float64_matches_oracle(ctx, mode, N):
+    scene, seq, s0, cp, covs = _setup_ring(mode, N)
+    out = cekf.run(seq.uv, seq.likelihood, cp, mode, 90.0, s0, ref_numerics=False, cal_covs=covs, covariances=True,
+                   ctx=ctx)
+    o = oekf.ekf(seq.uv, seq.likelihood, scene.K, scene.D, scene.R, scene.t, mode, 90.0, s0, 0.5,
+                 float(scene.res[0]), ref_numerics=False, cal_covs=covs)
+    P = len(pkin.get_pose_params(mode))
+    _check(out, P, o['x_est'][:, :P], o['x_est'][:, P:2 * P], o['x_est'][:, 2 * P:], o['x_smooth'][:, :P],
+           scale=1.0 if mode == 'head' else 10.0)
+    assert abs(int(out["outliers"]) - o["outliers"]) <= 1
+    sc = np.abs(o['P_est'][:3]).max()
+    np.testing.assert_allclose(out['P_est'][:3], o['P_est'][:3], atol=(1e-7 if mode == 'head' else 1e-4) * sc, rtol=0)
+
+
+@pytest.mark.parametrize('mode,N', [('head', 40), ('default', 10)])
+def test_ekf_12cam_reference_numerics_matches_oracle(ctx, mode, N):
+    """The reference's float32 state rounding and float32 Jacobian perturbation (the
+    drop-in default) at 12 cameras, against the oracle's restatement of the same
+    roundings: head at the reference-run tolerances, default over its first 10 frames at
+    1e-3 (as test_ekf_matches_reference_default_early_frames)."""
+    scene, seq, s0, cp, covs = _setup_ring(mode, N)
+    out = cekf.run(seq.uv, seq.likelihood, cp, mode, 90.0, s0, cal_covs=covs, ctx=ctx)
+    o = oekf.ekf(seq.uv, seq.likelihood, scene.K, scene.D, scene.R, scene.t, mode, 90.0, s0, 0.5,
+                 float(scene.res[0]), ref_numerics=True, cal_covs=covs)
+    P = len(pkin.get_pose_params(mode))
+    if mode == 'head':
+        _check(out, P, o['x_est'][:, :P], o['x_est'][:, P:2 * P], o['x_est'][:, 2 * P:], o['x_smooth'][:, :P])
+        assert abs(int(out['outliers']) - o['outliers']) <= 1
+    else:
+        np.testing.assert_allclose(out['x_est'][:, :P], o['x_est'][:, :P], atol=1e-3, rtol=0)
+        np.testing.assert_allclose(out['x_est'][0, :P], o['x_est'][0, :P], atol=1e-9, rtol=0)
+
+
+def test_core_ekf_dropin_12cam(ctx, tmp_path):
+    """The drop-in on a 12-camera rig: calibration covariances by camera mod 6, head model
+    tracks the synthetic truth."""
+    import pickle
+    scene, seq, s0, cp, covs = _setup_ring('head', 30, seed=62)
+    path = cekf.ekf(str(tmp_path), seq.to_df(), 'head', cp, 0, 29, 0.5, '', params={'vid_fps': 90.0})
+    with open(path, 'rb') as f:          # written by this test
+        d = pickle.load(f)
+    pos = np.array(d['smoothed_positions'])[:, :3]
+    err = np.sqrt(np.mean(np.sum((pos - seq.pos3d[:, 0, :3]) ** 2, -1)))
+    assert err < 0.05, err
