@@ -41,6 +41,7 @@ SYMBOLS = (
     'acs_fte_dist_destroy',
     'acs_sba_ext_dist_create', 'acs_sba_ext_dist_init', 'acs_sba_ext_dist_phase1', 'acs_sba_ext_dist_phase2',
     'acs_sba_ext_dist_phase3', 'acs_sba_ext_dist_result', 'acs_sba_ext_dist_destroy', 'acs_ekf_run',
+    'acs_sba_ekf_pipeline',
 )
 
 
@@ -63,6 +64,21 @@ class Report(C.Structure):
                     status_counts={STATUS_NAMES[i]: int(self.status_counts[i]) for i in range(7)},
                     iters_max=self.iters_max, iters_sum=self.iters_sum, nfev_sum=self.nfev_sum,
                     cost_before=self.cost_before, cost_after=self.cost_after)
+
+
+class EkfInitSpec(C.Structure):
+    """acs_ekf_init_spec: what the EKF's initial state is fitted on (src/core/ekf.py:121-157)."""
+    _fields_ = [(k, C.c_int32) for k in ('nose', 'lure', 'x0', 'y0', 'psi0', 'xl', 'yl', 'from_sba')]
+
+
+def ekf_init_spec(table, obs_markers, from_sba=True):
+    """The pipeline's init descriptor for EKF skeleton `table` on observations whose marker
+    order is `obs_markers`."""
+    obs = list(obs_markers)
+    pidx = {p: i for i, p in enumerate(table.params)}
+    lure = obs.index('lure') if ('lure' in table.markers and 'lure' in obs) else -1
+    return EkfInitSpec(obs.index('nose'), lure, pidx['x_0'], pidx['y_0'], pidx['psi_0'], pidx.get('x_l', -1),
+                       pidx.get('y_l', -1), int(bool(from_sba)))
 
 
 class FteOpts(C.Structure):
@@ -156,6 +172,9 @@ def _declare(lib):
         'acs_sba_ext_dist_destroy': (C.c_int, [_P]),
         'acs_ekf_run': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, dbl, dbl, dbl, _P, _P, _P, _P, i32,
                                   dbl, _P, _P, _P, _P, _P, _P, u32]),
+        'acs_sba_ekf_pipeline': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, i32, _P, dbl, dbl, dbl,
+                                           _P, _P, _P, C.POINTER(SbaOpts), C.POINTER(EkfInitSpec), i32, dbl, _P, _P,
+                                           _P, _P, C.POINTER(Report), u32]),
         'acs_sba_extrinsics': (C.c_int, [_P, _P, i32, _P, _P, _P, i64, _P, i64, C.POINTER(SbaExtOpts), _P, _P,
                                          C.POINTER(SbaExtReport), u32]),
     }
@@ -384,6 +403,58 @@ class Context:
         if single:
             out = {k: v[0] for k, v in out.items()}
         return out
+
+    # ---- configs[4]: SBA + EKF fused ------------------------------------------------
+    def sba_ekf_pipeline(self, table, cams, meas, likelihood, obs_markers, fps, thresh, max_pixel_err, r_std_base, Q,
+                         P0, sba_opts=None, from_sba=True, ref_numerics=True, eps=1e-3):
+        """acs_sba_ekf_pipeline on host arrays: meas (S, N, C, Lobs, 2), likelihood (S, N, C,
+        Lobs) with markers `obs_markers`; the EKF runs skeleton `table` (its markers a subset of
+        obs_markers). Returns dict pts (S, N, Lobs, 3), x_est, x_smooth (S, N, 3P), outliers
+        (S,), sba (report dict)."""
+        cams = _c64(cams)
+        meas = _c64(meas)
+        S, N, Cn, Lo, _ = meas.shape
+        assert Lo == len(obs_markers) and Cn == len(cams), (meas.shape, len(obs_markers), len(cams))
+        lik = _c64(likelihood).reshape(S, N, Cn, Lo)
+        obs = list(obs_markers)
+        emap = np.array([obs.index(m) for m in table.markers], np.int32)
+        n = 3 * table.P
+        pts = np.empty((S, N, Lo, 3))
+        xe = np.empty((S, N, n))
+        xs = np.empty((S, N, n))
+        outl = np.zeros(S, np.int64)
+        rep = Report()
+        opts = sba_opts or self.sba_opts()
+        spec = ekf_init_spec(table, obs, from_sba)
+        ints = np.ascontiguousarray(table.ints, np.int32)
+        reals = np.ascontiguousarray(table.reals, np.float64)
+        self.check(self.lib.acs_sba_ekf_pipeline(
+            self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), _ptr(cams), Cn, _ptr(meas), _ptr(lik), S, N, Lo,
+            _ptr(emap), float(fps), float(thresh), float(max_pixel_err), _ptr(_c64(r_std_base)), _ptr(_c64(Q)),
+            _ptr(_c64(P0)), C.byref(opts), C.byref(spec), int(bool(ref_numerics)), float(eps), _ptr(pts), _ptr(xe),
+            _ptr(xs), _ptr(outl), C.byref(rep), 0), 'acs_sba_ekf_pipeline')
+        return dict(pts=pts, x_est=xe, x_smooth=xs, outliers=outl, sba=rep.as_dict())
+
+    def sba_ekf_pipeline_dev(self, table, obs_markers, cams_p, n_cams, meas_p, lik_p, S, N, fps, thresh,
+                             max_pixel_err, rstd_p, Q_p, P0_p, pts_p, xe_p, xs_p, sba_opts=None, from_sba=True,
+                             ref_numerics=True, eps=1e-3, report=False):
+        """acs_sba_ekf_pipeline on HBM-resident arrays (device pointers, asynchronous unless
+        `report`: then waits and returns (sba report dict, outliers (S,)))."""
+        obs = list(obs_markers)
+        emap = np.array([obs.index(m) for m in table.markers], np.int32)
+        spec = ekf_init_spec(table, obs, from_sba)
+        opts = sba_opts or self.sba_opts()
+        ints = np.ascontiguousarray(table.ints, np.int32)
+        reals = np.ascontiguousarray(table.reals, np.float64)
+        rep = Report() if report else None
+        outl = np.zeros(S, np.int64) if report else None
+        P_ = C.c_void_p
+        self.check(self.lib.acs_sba_ekf_pipeline(
+            self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), P_(cams_p), n_cams, P_(meas_p), P_(lik_p), S, N,
+            len(obs), _ptr(emap), float(fps), float(thresh), float(max_pixel_err), P_(rstd_p), P_(Q_p), P_(P0_p),
+            C.byref(opts), C.byref(spec), int(bool(ref_numerics)), float(eps), P_(pts_p), P_(xe_p), P_(xs_p),
+            _ptr(outl), C.byref(rep) if report else None, ACS_DEVICE_PTRS), 'acs_sba_ekf_pipeline')
+        return (rep.as_dict(), outl) if report else None
 
     # ---- a9 -------------------------------------------------------------------------
     def redescending_loss(self, err, a=3.0, b=10.0, c=20.0, deriv=False):

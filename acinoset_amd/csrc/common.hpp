@@ -23,6 +23,7 @@ enum WsSlot {
   WS_TMP0, WS_TMP1, WS_TMP2, WS_TMP3, WS_TMP4, WS_TMP5, WS_TMP6, WS_TMP7,
   WS_FTE0, WS_FTE1, WS_FTE2, WS_FTE3, WS_FTE4, WS_FTE5, WS_FTE6, WS_FTE7, WS_FTE8, WS_FTE9,
   WS_FTE10, WS_FTE11, WS_FTE12, WS_FTE13, WS_FTE14, WS_FTE15,
+  WS_PIPE0, WS_PIPE1, WS_PIPE2, WS_PIPE3, WS_PIPE4, WS_PIPE5, WS_PIPE6, WS_PIPE7,
   WS_NSLOTS
 };
 enum GraphSlot { GRAPH_FTE = 0, GRAPH_NSLOTS };
@@ -111,6 +112,26 @@ static inline int acs_grid(int64_t n, int block) { return (int)((n + block - 1) 
 // deterministic (stable radix sort by point id). Defined in sba.hip. *K_out = max obs/pt.
 int acs_obs_to_slots(acs_ctx* ctx, const double* duv, const int32_t* dpi, const int32_t* dci, int64_t n_obs,
                      int64_t n_pts, int n_cams, double2** uv_pad, uint8_t** mask, uint8_t** camid, int* K_out);
+
+// ---- device-buffer stages shared by the entry points and the fused pipeline -------------
+// Dense points-only SBA (sba.hip): the fused LM over (n_pts, C) observation slots; with a
+// report, waits for it (else asynchronous on the context stream).
+int acs_sba_dense_enqueue(acs_ctx* ctx, const double* dcams, int C, const double2* duv, const uint8_t* dmask,
+                          int64_t n_pts, const double* dpts_in, double* dpts_out, const acs_sba_opts* opts,
+                          acs_report* report);
+// Pairwise fisheye triangulation of the dense slots (tri.hip): mean over adjacent pairs.
+int acs_tri_dense_enqueue(acs_ctx* ctx, const double* dcams, int C, const double* duv, const uint8_t* dmask,
+                          int64_t n_pts, double* dout, int32_t* dcnt);
+// EKF + RTS smoother (ekf.hip) on device buffers.
+struct EkfIo {
+  const int* I = nullptr;
+  const double *R = nullptr, *cams = nullptr, *meas = nullptr, *lik = nullptr, *rstd = nullptr, *Q = nullptr,
+               *P0 = nullptr, *s0 = nullptr;
+  double *x_pred = nullptr, *x_est = nullptr, *x_smooth = nullptr, *P_est = nullptr, *P_smooth = nullptr;
+  long long* outliers = nullptr;  // set by acs_ekf_enqueue (device, one per sequence)
+};
+int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n_cams, int n_seq, int n_frames,
+                    double fps, double thresh, double max_pixel_err, double eps, int ref_numerics, EkfIo& io);
 
 #include "fastmath.hpp"
 

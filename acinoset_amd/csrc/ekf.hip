@@ -819,28 +819,19 @@ __global__ __launch_bounds__(256) void k_ekf_smooth_x(EkfDims d, const double* _
 }
 
 unsigned long long* g_ekf_prof = nullptr;
-extern "C" {
-void acs_ekf_prof(unsigned long long* p) { g_ekf_prof = p; }
 
-int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals, int64_t n_reals,
-                const double* cams, int32_t n_cams, const double* meas, const double* likelihood, int32_t n_seq,
-                int32_t n_frames, double fps, double thresh, double max_pixel_err, const double* r_std_base,
-                const double* Q, const double* P0, const double* s0, int32_t ref_numerics, double eps,
-                double* x_pred, double* x_est, double* x_smooth, double* P_est, double* P_smooth,
-                int64_t* outliers, uint32_t flags) {
-  ACS_DEVICE_GUARD(ctx);
-  int hdr[FK_HDR];
-  if (flags & ACS_DEVICE_PTRS)
-    ACS_HIP(ctx, hipMemcpy(hdr, skel_ints, sizeof(hdr), hipMemcpyDeviceToHost));
-  else
-    std::memcpy(hdr, skel_ints, sizeof(hdr));
+// Filter + smoother on device buffers (common.hpp). hdr = the skeleton table header. x_pred
+// may be null (workspace then), P_est null = workspace, P_smooth null = no covariance
+// smoother (gains in parallel, then the state recursion). Sets io.outliers (device,
+// n_seq long longs) and io.x_pred / io.P_est to the buffers used.
+int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n_cams, int n_seq, int n_frames,
+                    double fps, double thresh, double max_pixel_err, double eps, int ref_numerics, EkfIo& io) {
   const int Jn = hdr[0], K = hdr[1], P = hdr[2], L = hdr[3];
   ACS_CHECK(ctx, Jn > 0 && Jn <= FK_MAXJ && K <= FK_MAXN && P >= 3 && P <= FK_MAXP && L >= 1 && L <= K,
             "ekf: skeleton table out of range");
   ACS_CHECK(ctx, n_ints == FK_HDR + 9 * Jn + 4 * K + L + 4 * P + K * P && n_reals == 3 * K, "ekf: blob sizes");
   ACS_CHECK(ctx, n_seq >= 1 && n_frames >= 1 && n_cams >= 1 && n_cams <= 64 && fps > 0 && eps > 0,
             "ekf: n_seq=%d n_frames=%d n_cams=%d", n_seq, n_frames, n_cams);
-  ACS_CHECK(ctx, x_est && x_smooth, "ekf: x_est and x_smooth are required");
   EkfDims d;
   d.N = n_frames;
   d.C = n_cams;
@@ -852,8 +843,8 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
   d.Ppad = ((P + 15) / 16) * 16;
   d.m = 2 * n_cams * L;
   d.mpad = ((d.m + 15) / 16) * 16;
-  d.n_ints = (int)n_ints;
-  d.n_reals = (int)n_reals;
+  d.n_ints = n_ints;
+  d.n_reals = n_reals;
   d.S = n_seq;
   d.sT = 1.0 / fps;
   d.thresh = thresh;
@@ -862,32 +853,17 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
   const int n = d.n;
   const size_t NF = (size_t)n_seq * n_frames;
   hipStream_t s = ctx->stream;
-  int rc;
-  void *dI, *dR, *dC, *dM, *dL, *dRb, *dQ, *dP0, *dS0;
-  if ((rc = acs_stage_in(ctx, WS_FTE0, skel_ints, sizeof(int32_t) * n_ints, flags, &dI))) return rc;
-  if ((rc = acs_stage_in(ctx, WS_FTE1, skel_reals, sizeof(double) * n_reals, flags, &dR))) return rc;
-  if ((rc = acs_stage_in(ctx, WS_CAMS, cams, sizeof(double) * ACS_CAM_STRIDE * n_cams, flags, &dC))) return rc;
-  if ((rc = acs_stage_in(ctx, WS_FTE2, meas, sizeof(double) * NF * n_cams * L * 2, flags, &dM))) return rc;
-  if ((rc = acs_stage_in(ctx, WS_FTE3, likelihood, sizeof(double) * NF * n_cams * L, flags, &dL))) return rc;
-  if ((rc = acs_stage_in(ctx, WS_FTE4, r_std_base, sizeof(double) * n_cams, flags, &dRb))) return rc;
-  if ((rc = acs_stage_in(ctx, WS_FTE7, Q, sizeof(double) * n * n, flags, &dQ))) return rc;
-  if ((rc = acs_stage_in(ctx, WS_FTE8, P0, sizeof(double) * n * n, flags, &dP0))) return rc;
-  if ((rc = acs_stage_in(ctx, WS_FTE9, s0, sizeof(double) * n_seq * n, flags, &dS0))) return rc;
-  double* dxp = (double*)acs_out_buf(ctx, WS_FTE10, x_pred, sizeof(double) * NF * n, flags);
-  double* dxe = (double*)acs_out_buf(ctx, WS_FTE11, x_est, sizeof(double) * NF * n, flags);
-  double* dxs = (double*)acs_out_buf(ctx, WS_FTE12, x_smooth, sizeof(double) * NF * n, flags);
-  if (!x_pred) dxp = (double*)acs_ws(ctx, WS_FTE10, sizeof(double) * NF * n);
-  // covariance histories: always needed by the smoother; the caller's buffers when given
-  double* dPe = (flags & ACS_DEVICE_PTRS) && P_est ? P_est : (double*)acs_ws(ctx, WS_FTE13, sizeof(double) * NF * n * n);
+  if (!io.x_pred) io.x_pred = (double*)acs_ws(ctx, WS_FTE10, sizeof(double) * NF * n);
+  // covariance histories: always needed by the smoother; the caller's buffer when given
+  if (!io.P_est) io.P_est = (double*)acs_ws(ctx, WS_FTE13, sizeof(double) * NF * n * n);
   double* dPp = (double*)acs_ws(ctx, WS_FTE14, sizeof(double) * NF * n * n);
-  double* dPs = P_smooth ? ((flags & ACS_DEVICE_PTRS) ? P_smooth
-                                                      : (double*)acs_ws(ctx, WS_FTE15, sizeof(double) * NF * n * n))
-                         : nullptr;
   const size_t scr_f = (size_t)n_seq * ((size_t)(P + 1) * d.m + 2 * (size_t)d.mpad * d.Ppad + 2 * d.mpad);
   const size_t scr_s = (size_t)n_seq * 5 * d.npad * d.npad;
   double* scr = (double*)acs_ws(ctx, WS_FTE6, sizeof(double) * std::max(scr_f, scr_s) + 64 * (size_t)n_seq * 8);
-  if (!dxp || !dxe || !dxs || !dPe || !dPp || !scr || (P_smooth && !dPs)) return ACS_E_NOMEM;
+  if (!io.x_pred || !io.P_est || !dPp || !scr) return ACS_E_NOMEM;
+  double *dxp = io.x_pred, *dxe = io.x_est, *dxs = io.x_smooth, *dPe = io.P_est, *dPs = io.P_smooth;
   long long* dout = (long long*)(scr + std::max(scr_f, scr_s));
+  io.outliers = dout;
   int* dbad = (int*)(dout + n_seq);
   ACS_HIP(ctx, hipMemsetAsync(dbad, 0, sizeof(int), s));
   const size_t U = std::max(ekf_fk_lds(P, Jn, L),
@@ -896,13 +872,11 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
                                           n_reals + (n_ints + 1) / 2 + 1);
   ACS_CHECK(ctx, lds_f <= 160 * 1024, "ekf: P = %d needs %zu bytes of LDS", P, lds_f);
   if (ref_numerics)
-    hipLaunchKernelGGL(k_ekf_filter<true>, dim3(n_seq), dim3(512), lds_f, s, d, (const int*)dI, (const double*)dR,
-                       (const double*)dC, (const double*)dM, (const double*)dL, (const double*)dRb, (const double*)dQ,
-                       (const double*)dP0, (const double*)dS0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof);
+    hipLaunchKernelGGL(k_ekf_filter<true>, dim3(n_seq), dim3(512), lds_f, s, d, io.I, io.R, io.cams, io.meas, io.lik,
+                       io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof);
   else
-    hipLaunchKernelGGL(k_ekf_filter<false>, dim3(n_seq), dim3(512), lds_f, s, d, (const int*)dI, (const double*)dR,
-                       (const double*)dC, (const double*)dM, (const double*)dL, (const double*)dRb, (const double*)dQ,
-                       (const double*)dP0, (const double*)dS0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof);
+    hipLaunchKernelGGL(k_ekf_filter<false>, dim3(n_seq), dim3(512), lds_f, s, d, io.I, io.R, io.cams, io.meas, io.lik,
+                       io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof);
   ACS_HIP(ctx, hipGetLastError());
   const size_t lds_s = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + 512 + d.npad);
   if (dPs) {
@@ -920,17 +894,74 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
                        (const double*)dPp, dxs);
   }
   ACS_HIP(ctx, hipGetLastError());
-  if (x_pred && (rc = acs_stage_out(ctx, x_pred, dxp, sizeof(double) * NF * n, flags))) return rc;
-  if ((rc = acs_stage_out(ctx, x_est, dxe, sizeof(double) * NF * n, flags))) return rc;
-  if ((rc = acs_stage_out(ctx, x_smooth, dxs, sizeof(double) * NF * n, flags))) return rc;
-  if (P_est && !(flags & ACS_DEVICE_PTRS) && (rc = acs_stage_out(ctx, P_est, dPe, sizeof(double) * NF * n * n, flags)))
+  return ACS_OK;
+}
+
+extern "C" {
+void acs_ekf_prof(unsigned long long* p) { g_ekf_prof = p; }
+
+int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals, int64_t n_reals,
+                const double* cams, int32_t n_cams, const double* meas, const double* likelihood, int32_t n_seq,
+                int32_t n_frames, double fps, double thresh, double max_pixel_err, const double* r_std_base,
+                const double* Q, const double* P0, const double* s0, int32_t ref_numerics, double eps,
+                double* x_pred, double* x_est, double* x_smooth, double* P_est, double* P_smooth,
+                int64_t* outliers, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
+  int hdr[FK_HDR];
+  if (flags & ACS_DEVICE_PTRS)
+    ACS_HIP(ctx, hipMemcpy(hdr, skel_ints, sizeof(hdr), hipMemcpyDeviceToHost));
+  else
+    std::memcpy(hdr, skel_ints, sizeof(hdr));
+  ACS_CHECK(ctx, x_est && x_smooth, "ekf: x_est and x_smooth are required");
+  const int P = hdr[2], L = hdr[3], n = 3 * P;
+  ACS_CHECK(ctx, P >= 3 && P <= FK_MAXP && L >= 1 && n_seq >= 1 && n_frames >= 1 && n_cams >= 1 && n_cams <= 64,
+            "ekf: P=%d L=%d n_seq=%d n_frames=%d n_cams=%d", P, L, n_seq, n_frames, n_cams);
+  const size_t NF = (size_t)n_seq * n_frames;
+  int rc;
+  void *dI, *dR, *dC, *dM, *dL, *dRb, *dQ, *dP0, *dS0;
+  if ((rc = acs_stage_in(ctx, WS_FTE0, skel_ints, sizeof(int32_t) * n_ints, flags, &dI))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_FTE1, skel_reals, sizeof(double) * n_reals, flags, &dR))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_CAMS, cams, sizeof(double) * ACS_CAM_STRIDE * n_cams, flags, &dC))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_FTE2, meas, sizeof(double) * NF * n_cams * L * 2, flags, &dM))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_FTE3, likelihood, sizeof(double) * NF * n_cams * L, flags, &dL))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_FTE4, r_std_base, sizeof(double) * n_cams, flags, &dRb))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_FTE7, Q, sizeof(double) * n * n, flags, &dQ))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_FTE8, P0, sizeof(double) * n * n, flags, &dP0))) return rc;
+  if ((rc = acs_stage_in(ctx, WS_FTE9, s0, sizeof(double) * n_seq * n, flags, &dS0))) return rc;
+  EkfIo io;
+  io.I = (const int*)dI;
+  io.R = (const double*)dR;
+  io.cams = (const double*)dC;
+  io.meas = (const double*)dM;
+  io.lik = (const double*)dL;
+  io.rstd = (const double*)dRb;
+  io.Q = (const double*)dQ;
+  io.P0 = (const double*)dP0;
+  io.s0 = (const double*)dS0;
+  io.x_pred = x_pred ? (double*)acs_out_buf(ctx, WS_FTE10, x_pred, sizeof(double) * NF * n, flags) : nullptr;
+  io.x_est = (double*)acs_out_buf(ctx, WS_FTE11, x_est, sizeof(double) * NF * n, flags);
+  io.x_smooth = (double*)acs_out_buf(ctx, WS_FTE12, x_smooth, sizeof(double) * NF * n, flags);
+  io.P_est = (flags & ACS_DEVICE_PTRS) ? P_est : nullptr;
+  io.P_smooth = P_smooth ? ((flags & ACS_DEVICE_PTRS) ? P_smooth
+                                                      : (double*)acs_ws(ctx, WS_FTE15, sizeof(double) * NF * n * n))
+                         : nullptr;
+  if ((x_pred && !io.x_pred) || !io.x_est || !io.x_smooth || (P_smooth && !io.P_smooth)) return ACS_E_NOMEM;
+  if ((rc = acs_ekf_enqueue(ctx, (int)n_ints, (int)n_reals, hdr, n_cams, n_seq, n_frames, fps, thresh, max_pixel_err,
+                            eps, ref_numerics, io)))
+    return rc;
+  hipStream_t s = ctx->stream;
+  if (x_pred && (rc = acs_stage_out(ctx, x_pred, io.x_pred, sizeof(double) * NF * n, flags))) return rc;
+  if ((rc = acs_stage_out(ctx, x_est, io.x_est, sizeof(double) * NF * n, flags))) return rc;
+  if ((rc = acs_stage_out(ctx, x_smooth, io.x_smooth, sizeof(double) * NF * n, flags))) return rc;
+  if (P_est && !(flags & ACS_DEVICE_PTRS) &&
+      (rc = acs_stage_out(ctx, P_est, io.P_est, sizeof(double) * NF * n * n, flags)))
     return rc;
   if (P_smooth && !(flags & ACS_DEVICE_PTRS) &&
-      (rc = acs_stage_out(ctx, P_smooth, dPs, sizeof(double) * NF * n * n, flags)))
+      (rc = acs_stage_out(ctx, P_smooth, io.P_smooth, sizeof(double) * NF * n * n, flags)))
     return rc;
   if (outliers) {
     std::vector<long long> ho(n_seq);
-    ACS_HIP(ctx, hipMemcpyAsync(ho.data(), dout, sizeof(long long) * n_seq, hipMemcpyDeviceToHost, s));
+    ACS_HIP(ctx, hipMemcpyAsync(ho.data(), io.outliers, sizeof(long long) * n_seq, hipMemcpyDeviceToHost, s));
     ACS_HIP(ctx, hipStreamSynchronize(s));
     for (int q = 0; q < n_seq; ++q) outliers[q] = ho[q];
   } else if (!(flags & ACS_DEVICE_PTRS)) {

@@ -464,6 +464,21 @@ static int run_report(acs_ctx* ctx, const double* c0, const double* c1, const in
   return ACS_OK;
 }
 
+int acs_sba_dense_enqueue(acs_ctx* ctx, const double* dcams, int C, const double2* duv, const uint8_t* dmask,
+                          int64_t n_pts, const double* dpts_in, double* dpts_out, const acs_sba_opts* opts,
+                          acs_report* report) {
+  if (n_pts == 0) {
+    if (report) std::memset(report, 0, sizeof(*report));
+    return ACS_OK;
+  }
+  double *c0, *c1;
+  int* st;
+  int rc;
+  if ((rc = run_lm(ctx, dcams, C, C, duv, dmask, nullptr, n_pts, dpts_in, dpts_out, opts, &c0, &c1, &st))) return rc;
+  if (report) return run_report(ctx, c0, c1, st, n_pts, report);
+  return ACS_OK;
+}
+
 int acs_obs_to_slots(acs_ctx* ctx, const double* duv, const int32_t* dpi, const int32_t* dci, int64_t n_obs,
                      int64_t n_pts, int n_cams, double2** uv_pad, uint8_t** mask, uint8_t** camid, int* K_out) {
   hipStream_t s = ctx->stream;

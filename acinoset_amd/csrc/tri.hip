@@ -155,6 +155,15 @@ __global__ __launch_bounds__(256) void k_tri_dense(const double* __restrict__ ca
   if (cnt) cnt[p] = n;
 }
 
+int acs_tri_dense_enqueue(acs_ctx* ctx, const double* dcams, int C, const double* duv, const uint8_t* dmask,
+                          int64_t n_pts, double* dout, int32_t* dcnt) {
+  if (n_pts == 0) return ACS_OK;
+  hipLaunchKernelGGL(k_tri_dense, dim3(acs_grid(n_pts, 256)), dim3(256), 0, ctx->stream, dcams, C, duv, dmask, n_pts,
+                     dout, dcnt);
+  ACS_HIP(ctx, hipGetLastError());
+  return ACS_OK;
+}
+
 extern "C" {
 
 int acs_triangulate_pairs(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv_a, const double* uv_b,
@@ -193,9 +202,9 @@ int acs_triangulate_dense(acs_ctx* ctx, const double* cams, int32_t n_cams, cons
   int32_t* dcnt = n_pairs_out ? (int32_t*)acs_out_buf(ctx, WS_OUT1, n_pairs_out, sizeof(int32_t) * n_pts, flags)
                               : nullptr;
   if (!dout || (n_pairs_out && !dcnt)) return ACS_E_NOMEM;
-  hipLaunchKernelGGL(k_tri_dense, dim3(acs_grid(n_pts, 256)), dim3(256), 0, ctx->stream, (const double*)dc, n_cams,
-                     (const double*)duv, (const uint8_t*)dm, n_pts, dout, dcnt);
-  ACS_HIP(ctx, hipGetLastError());
+  if ((rc = acs_tri_dense_enqueue(ctx, (const double*)dc, n_cams, (const double*)duv, (const uint8_t*)dm, n_pts, dout,
+                                   dcnt)))
+    return rc;
   if ((rc = acs_stage_out(ctx, xyz_out, dout, sizeof(double) * 3 * n_pts, flags))) return rc;
   if (n_pairs_out && (rc = acs_stage_out(ctx, n_pairs_out, dcnt, sizeof(int32_t) * n_pts, flags))) return rc;
   if (!(flags & ACS_DEVICE_PTRS)) ACS_HIP(ctx, hipStreamSynchronize(ctx->stream));

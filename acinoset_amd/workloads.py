@@ -118,10 +118,13 @@ def sba_reference_workload() -> SbaWorkload:
     d = np.load(REF_SBA_FIXTURE, allow_pickle=False)
     K, D, R, t = d['K'], d['D'], d['R'], d['t']
     C = len(K)
-    p2 = d['points_2d']
-    pi = d['point_indices'].astype(np.int64)
-    ci = d['camera_indices'].astype(np.int64)
-    pts0 = d['points_3d']
+    # C order throughout: the fixture's arrays came out of DataFrames (column-major) and the
+    # bench hands their device copies to the C ABI as raw pointers
+    c64 = lambda a: np.ascontiguousarray(a, np.float64)  # noqa: E731
+    p2 = c64(d['points_2d'])
+    pi = np.ascontiguousarray(d['point_indices'], np.int64)
+    ci = np.ascontiguousarray(d['camera_indices'], np.int64)
+    pts0 = c64(d['points_3d'])
     n = len(pts0)
     uv = np.zeros((n, C, 2))
     mask = np.zeros((n, C), np.uint8)
@@ -133,8 +136,8 @@ def sba_reference_workload() -> SbaWorkload:
     scene = synth.Scene(K, D, R, t, tuple(int(v) for v in d['res']))
     seq = synth.make_sequence(n_frames, scene, mode='default_nolure', seed=0)
     truth = seq.pos3d[:, 0][d['pts_frame'], d['pts_marker']]
-    return SbaWorkload(K, D, R, t, _native.pack_cameras(K, D, R, t), p2, pi, ci, pts0, uv, mask, d['pts_out'],
-                       d['resid_after'], truth, n_frames)
+    return SbaWorkload(c64(K), c64(D), c64(R), c64(t), _native.pack_cameras(K, D, R, t), p2, pi, ci, pts0, uv, mask,
+                       c64(d['pts_out']), c64(d['resid_after']), c64(truth), n_frames)
 
 
 def reproj_rms(resid):

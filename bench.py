@@ -44,6 +44,9 @@ def parse():
     ap.add_argument('--ekf-seqs', type=int, default=64, help='EKF + RTS leg: sequences per rank (0 = skip)')
     ap.add_argument('--ekf-frames', type=int, default=500)
     ap.add_argument('--ekf-cams', type=int, default=12)
+    ap.add_argument('--pipeline-seqs', type=int, default=80,
+                    help='configs[4] fused SBA+EKF leg: clips per rank (0 = skip)')
+    ap.add_argument('--pipeline-frames', type=int, default=250)
     ap.add_argument('--exchange', default='nccl', choices=('nccl', 'gloo'),
                     help='backend of the FTE window all-reduces (nccl = RCCL over xGMI)')
     ap.add_argument('--scale-frames', type=int, default=20000,
@@ -86,10 +89,9 @@ def main():
     uv, mask, pts0, cams = wl.uv, wl.mask, wl.pts0, wl.cams
     n_pts, C = mask.shape
     dev = torch.device('cuda', local)
-    d_cams = torch.from_numpy(cams).to(dev)
-    d_uv = torch.from_numpy(uv).to(dev)
-    d_mask = torch.from_numpy(mask).to(dev)
-    d_pts0 = torch.from_numpy(pts0).to(dev)
+    # raw device pointers go to the C ABI: contiguous device copies
+    d_cams, d_uv, d_mask, d_pts0 = (torch.from_numpy(np.ascontiguousarray(a)).to(dev).contiguous()
+                                    for a in (cams, uv, mask, pts0))
     d_pts = d_pts0.clone()
     opts = _native.Context.sba_opts()
 
@@ -222,6 +224,9 @@ def main():
                                mode='head')
         out['ekf_default_model_diverges'] = bench_ekf(ctx, torch, args.ekf_seqs, args.ekf_frames, args.ekf_cams,
                                                       world, rank, mode='default')
+    if args.pipeline_seqs > 0:
+        out['sba_ekf_pipeline'] = bench_pipeline(ctx, torch, stream, world, rank, args.pipeline_seqs,
+                                                 args.pipeline_frames)
     if args.window_frames > 0:
         out['fte_window'] = bench_fte_window(ctx, torch, stream, args.window_frames, world, rank, args.exchange)
     if args.scale_frames > 0 and world == 1:
@@ -447,6 +452,93 @@ def bench_ekf(ctx, torch, n_seq, n_frames, n_cams, world, rank, mode='default', 
             'smoothed_rms_vs_truth_m': rms, 'filter': 'tracks' if rms < 0.05 else 'diverged',
             'outliers_frac': float(np.mean(out['outliers'])) / max(1.0, float(np.sum(lik > 0.5)) * 2 / n_seq),
             'numerics': 'reference (float32 state rounding, FD Jacobian eps 1e-3)'}
+
+
+def bench_pipeline(ctx, torch, stream, world, rank, n_seq=80, n_frames=250, n_cams=12, steps=3):
+    """configs[4]: "12-cam 20k-frame synthetic SBA+EKF fused" - per rank n_seq clips of n_frames
+    frames (80 x 250 = 20,000 frames, ~2.8 s clips at 90 fps) on the synthesised 12-camera ring,
+    20 DLC keypoints per frame. One step = acs_sba_ekf_pipeline on the HBM-resident observation
+    tensor: pairwise triangulation + points-only SBA of every keypoint (core.sba), the EKF initial
+    state fitted on the SBA points, and the EKF + RTS smoother (core.ekf) with the head model on
+    its three markers (the 29-parameter 'default' model loses these sequences; see the ekf legs).
+    Weak scaling: every rank runs its own clips (the EKF is sequential in time; clips are the
+    parallel unit, no collective)."""
+    import importlib
+    import torch.distributed as tdist
+    from acinoset_amd import _native, synth
+    from acinoset_amd.kinematics import build_table
+    cekf = importlib.import_module('acinoset_amd.core.ekf')
+    scene = synth.ring_scene(n_cams)
+    seqs = [synth.make_sequence(n_frames, scene, mode='default_nolure', seed=3000 + 131 * rank + k)
+            for k in range(n_seq)]
+    obs_markers = seqs[0].markers
+    table = build_table('head')
+    P = table.P
+    covs = cekf.ring_cal_covs(n_cams)
+    dv = torch.device('cuda', torch.cuda.current_device())
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(dv).contiguous()  # noqa: E731
+    d_cams = T(_native.pack_cameras(scene.K, scene.D, scene.R, scene.t))
+    d_meas = T(np.stack([q.uv for q in seqs]))
+    d_lik = T(np.stack([q.likelihood for q in seqs]))
+    d_rstd = T(cekf.measurement_std(n_cams, covs))
+    d_Q = T(cekf.process_covariance(P, 1 / 90.0))
+    d_P0 = T(cekf.initial_covariance('head'))
+    L = len(obs_markers)
+    d_pts = torch.empty((n_seq, n_frames, L, 3), dtype=torch.float64, device=dv)
+    d_xe = torch.empty((n_seq, n_frames, 3 * P), dtype=torch.float64, device=dv)
+    d_xs = torch.empty_like(d_xe)
+    args = (table, obs_markers, d_cams.data_ptr(), n_cams, d_meas.data_ptr(), d_lik.data_ptr(), n_seq, n_frames,
+            90.0, 0.5, float(scene.res[0]), d_rstd.data_ptr(), d_Q.data_ptr(), d_P0.data_ptr(), d_pts.data_ptr(),
+            d_xe.data_ptr(), d_xs.data_ptr())
+    rep, outl = ctx.sba_ekf_pipeline_dev(*args, report=True)          # warm-up + convergence report
+    torch.cuda.synchronize()
+    pts = d_pts.cpu().numpy()
+    xs = d_xs.cpu().numpy()
+    truth = np.stack([q.pos3d[:, 0] for q in seqs])                   # (S, N, L, 3)
+    ok = np.isfinite(pts).all(-1)
+    sba_rms = float(np.sqrt(np.mean(np.sum((pts[ok] - truth[ok]) ** 2, -1))))
+    head_err = []
+    for k in range(min(8, n_seq)):
+        pe = ctx.fk(table, np.ascontiguousarray(xs[k][:, :P]))
+        head_err.append(np.sqrt(np.mean(np.sum((pe - truth[k][:, :3]) ** 2, -1))))
+    if world > 1:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        ctx.sba_ekf_pipeline_dev(*args)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    dt = (time.perf_counter() - t0) / steps
+    gpu_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    frames = n_seq * n_frames
+    # algorithmic HBM bytes per frame of the fused pass: the observation tensor read once
+    # (pixels 16 B + likelihood 8 B per camera and keypoint), the SBA points and the filtered
+    # and smoothed EKF states written once
+    b_frame = n_cams * L * 24 + L * 3 * 8 + 2 * 3 * P * 8
+    achieved = frames * b_frame / (gpu_ms * 1e-3) / 1e9
+    return {'workload': f'sba+ekf fused C={n_cams} L={L} (EKF head model P={P}) {n_seq} clips x {n_frames} frames/rank '
+                        f'(configs[4])',
+            'frames_per_s': world * frames / dt, 'ms_per_step': dt * 1e3, 'gpu_ms_per_step': gpu_ms,
+            'scaling': 'weak (clips per rank)',
+            'sba': {'status': rep['status_counts'], 'iters_max': rep['iters_max'], 'points': int(rep['n_problems']),
+                    'pos_rms_vs_truth_m': sba_rms},
+            'ekf': {'smoothed_head_rms_vs_truth_m': float(np.median(head_err)),
+                    'filter': 'tracks' if np.median(head_err) < 0.05 else 'diverged',
+                    'outliers_per_clip': float(np.mean(outl))},
+            'roofline': {'bound': 'latency (sequential EKF frames per clip)', 'achieved': achieved,
+                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                         'bytes_per_frame': b_frame,
+                         'note': 'HBM-equivalent rate of the whole fused step; the EKF walks each clip\'s frames in '
+                                 'order on one CU, so the step is bound by the per-frame update latency, not HBM'}}
 
 
 def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl', steps=3):

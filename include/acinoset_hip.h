@@ -295,6 +295,38 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
                 const double* s0, int32_t ref_numerics, double eps, double* x_pred, double* x_est,
                 double* x_smooth, double* P_est, double* P_smooth, int64_t* outliers, uint32_t flags);
 
+/* ---- configs[4]: SBA + EKF fused on one observation tensor ------------------------------
+ * core.sba (src/core/sba.py:27-70) and core.ekf (src/core/ekf.py:26-298) of the same
+ * DLC observations as one device-resident enqueue: pairwise triangulation and points-only
+ * SBA of every (sequence, frame, marker) with likelihood > thresh (src/core/sba.py:41;
+ * points no adjacent camera pair saw are left out, as the reference's inner merge does,
+ * src/lib/sba.py:299), then per sequence the initial state of src/core/ekf.py:121-157 (nose /
+ * lure line fits; init->from_sba = 1: on the SBA points, 0: on the triangulated points as
+ * core.ekf does) and the EKF + RTS smoother of acs_ekf_run on the EKF model's markers.
+ * meas (n_seq, n_frames, n_cams, n_markers, 2), likelihood (n_seq, n_frames, n_cams,
+ * n_markers); ekf_markers (L of the skeleton table): observation marker index of every EKF
+ * model marker. skel_ints / skel_reals / ekf_markers / sba_opts / init are HOST descriptors
+ * whatever `flags` says; the arrays follow `flags`.
+ * Outputs: pts_out (n_seq, n_frames, n_markers, 3) SBA points (NaN where not triangulated),
+ * x_est, x_smooth (n_seq, n_frames, 3P); outliers (n_seq, may be NULL); sba_report (may be
+ * NULL; waits for the SBA). Without ACS_DEVICE_PTRS (or with outliers) the call waits and
+ * fails if a sequence's nose was seen in fewer than two frames.                        */
+typedef struct {
+  int32_t nose;      /* observation marker index of the nose */
+  int32_t lure;      /* ... of the lure, -1 if the model has none */
+  int32_t x0, y0, psi0;  /* pose parameter indices of x_0, y_0, psi_0 */
+  int32_t xl, yl;    /* ... of x_l, y_l (-1: no lure states) */
+  int32_t from_sba;  /* 1: line fits on the SBA points, 0: on the triangulated points */
+} acs_ekf_init_spec;
+int acs_sba_ekf_pipeline(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
+                         int64_t n_reals, const double* cams, int32_t n_cams, const double* meas,
+                         const double* likelihood, int32_t n_seq, int32_t n_frames, int32_t n_markers,
+                         const int32_t* ekf_markers, double fps, double thresh, double max_pixel_err,
+                         const double* r_std_base, const double* Q, const double* P0, const acs_sba_opts* sba_opts,
+                         const acs_ekf_init_spec* init, int32_t ref_numerics, double eps, double* pts_out,
+                         double* x_est, double* x_smooth, int64_t* outliers, acs_report* sba_report,
+                         uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif
