@@ -5,7 +5,9 @@ run one after the other on the same observations:
   (src/core/ekf.py:121-157) on the SBA (or triangulated) points -> oracle/ekf.ekf (:26-298).
 
 Tolerances: SBA points 1e-7 m (as test_gpu_core's SBA parity), the NaN pattern (points no
-adjacent pair saw) identical; the EKF initial state 1e-9; the EKF states at the
+adjacent pair saw) identical; the first filtered state 1e-9 (head) / 1e-7 (the 87-state
+default model, whose initial state is fitted on SBA points that agree to ~4e-9 m); the EKF
+states at the
 test_gpu_ekf tolerances (x 5e-5, dx 5e-4, ddx 5e-3, smoothed x 2e-5; x10 for the 29-state
 default model); outlier counts within 1 per sequence.
 """
@@ -96,7 +98,9 @@ def test_pipeline_6cam_default_model_matches_oracle(ctx):
     m = ~np.isnan(pts)
     np.testing.assert_allclose(g[m], pts[m], rtol=0, atol=1e-7)
     xe = out['x_est'][0]
-    np.testing.assert_allclose(xe[0], o['x_est'][0], rtol=0, atol=1e-9)
+    # the initial state is fitted on SBA points that agree with the oracle's to ~4e-9 m; the
+    # first 87-state update carries that into x_est[0] at the 1e-8 level
+    np.testing.assert_allclose(xe[0], o['x_est'][0], rtol=0, atol=1e-7)
     np.testing.assert_allclose(xe[:, :P], o['x_est'][:, :P], rtol=0, atol=10 * TOL['x'])
     np.testing.assert_allclose(out['x_smooth'][0][:, :P], o['x_smooth'][:, :P], rtol=0, atol=10 * TOL['smoothed_x'])
 
