@@ -36,8 +36,8 @@ SYMBOLS = (
     'acs_sba_residuals', 'acs_sba_points', 'acs_sba_points_dense', 'acs_redescending_loss', 'acs_fk',
     'acs_fte_default_opts', 'acs_fte_solve', 'acs_fte_eval', 'acs_triangulate_pairs', 'acs_triangulate_dense',
     'acs_sba_ext_default_opts', 'acs_sba_extrinsics', 'acs_sba_points_dense_io',
-    'acs_fte_dist_create', 'acs_fte_dist_init', 'acs_fte_dist_phase1', 'acs_fte_dist_phase2', 'acs_fte_dist_phase3',
-    'acs_fte_dist_phase4', 'acs_fte_dist_gather', 'acs_fte_dist_scatter', 'acs_fte_dist_result',
+    'acs_fte_dist_create', 'acs_fte_dist_init', 'acs_fte_dist_round', 'acs_fte_dist_poll',
+    'acs_fte_dist_gather', 'acs_fte_dist_scatter', 'acs_fte_dist_result',
     'acs_fte_dist_destroy',
     'acs_sba_ext_dist_create', 'acs_sba_ext_dist_init', 'acs_sba_ext_dist_phase1', 'acs_sba_ext_dist_phase2',
     'acs_sba_ext_dist_phase3', 'acs_sba_ext_dist_result', 'acs_sba_ext_dist_destroy', 'acs_ekf_run',
@@ -115,7 +115,7 @@ class SbaExtReport(C.Structure):
 
 
 # must equal ACS_ABI_VERSION in include/acinoset_hip.h (checked when the library loads)
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lib = None
 _lock = threading.Lock()
 _P = C.c_void_p
@@ -154,10 +154,8 @@ def _declare(lib):
         'acs_fte_dist_create': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, dbl, _P, i32, i32, _P, _P,
                                           C.POINTER(FteOpts), i32, i32, C.POINTER(_P), C.POINTER(i64), u32]),
         'acs_fte_dist_init': (C.c_int, [_P, _P]),
-        'acs_fte_dist_phase1': (C.c_int, [_P, _P]),
-        'acs_fte_dist_phase2': (C.c_int, [_P, _P]),
-        'acs_fte_dist_phase3': (C.c_int, [_P, _P]),
-        'acs_fte_dist_phase4': (C.c_int, [_P, _P, i32, C.POINTER(i32)]),
+        'acs_fte_dist_round': (C.c_int, [_P, _P, _P]),
+        'acs_fte_dist_poll': (C.c_int, [_P, i64, C.POINTER(i32)]),
         'acs_fte_dist_gather': (C.c_int, [_P, _P]),
         'acs_fte_dist_scatter': (C.c_int, [_P, _P]),
         'acs_fte_dist_result': (C.c_int, [_P, _P, _P, C.POINTER(FteReport), u32]),

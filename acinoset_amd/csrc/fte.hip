@@ -56,7 +56,14 @@ struct FteDims {
 struct FteState {
   double F, F0, lam, gmax, Fmeas, Fmodel, dnorm, xnorm;
   int cur, status, iters, nacc, relin, bad, pad0, pad1;
+  // frame-window rounds (acs_fte_dist_round): a step awaiting its summed trial cost, the
+  // first round (initial cost), and the state swapped for the speculative reduced system
+  int pending, first, spec_on, save_cur;
+  double save_lam;
 };
+// transient status of a round whose step was rejected: its solve / step / trial kernels
+// (which all stop on status != 0) are skipped, then the status returns to 0
+#define FTE_STATUS_SKIP 100
 
 struct FteOptsDev {
   int max_iters;
@@ -2328,7 +2335,7 @@ __global__ void k_dist_scatter(FteDims d, const FteState* __restrict__ st, int r
 // p3 = (measurement cost, model cost, |step|^2, |X, tau|^2) of this rank's owned terms /
 // rows (frames [k0, k1), super-blocks [n0, n1) of the trial's norm partials)
 // which = 1: the trial's measurement terms are in Fm's speculative copy (cur ^ 1, N each)
-__global__ __launch_bounds__(256) void k_dist_cost_pack(const FteState* __restrict__ st, int which, int N, int m0,
+__global__ __launch_bounds__(256) void k_dist_cost_pack(FteState* __restrict__ st, int which, int N, int m0,
                                                         int m1, int q0, int q1, const double* __restrict__ Fm,
                                                         const double* __restrict__ Fq, int n0, int n1,
                                                         const double* __restrict__ normp, double* __restrict__ p3) {
@@ -2358,6 +2365,7 @@ __global__ __launch_bounds__(256) void k_dist_cost_pack(const FteState* __restri
     p3[1] = b;
     p3[2] = dn;
     p3[3] = xn;
+    if (which == 1) st->pending = 1;  // this round took a step: its cost travels in p3
   }
 }
 
@@ -2385,27 +2393,23 @@ __global__ __launch_bounds__(256) void k_dist_x_in(FteDims d, const FteState* __
   }
 }
 
-// k_fte_lm with the all-reduced costs (every rank takes the same decision)
-__global__ __launch_bounds__(256) void k_fte_lm_dist(FteDims d, FteState* __restrict__ st, FteOptsDev o, int init,
-                                                     const double* __restrict__ p3) {
-  const int tid = threadIdx.x;
+// Round control (one thread). On the summed payload of the previous round: the first round
+// takes the initial cost; otherwise a pending step is accepted or rejected (oracle/fte.py
+// solve; every rank takes the same decision). A rejection marks the round SKIP: its solve
+// is stale (formed for the trial state) and the round only re-forms the reduced system.
+__global__ void k_dist_decide(FteState* __restrict__ st, FteOptsDev o, const double* __restrict__ p3) {
+  if (threadIdx.x != 0) return;
   const double fm = p3[0], fq = p3[1];
-  if (init) {
-    if (tid == 0) {
-      st->F = st->F0 = fm + fq;
-      st->Fmeas = fm;
-      st->Fmodel = fq;
-    }
+  if (st->first) {
+    st->first = 0;
+    st->F = st->F0 = fm + fq;
+    st->Fmeas = fm;
+    st->Fmodel = fq;
     return;
   }
-  if (st->status != 0) return;
-  const double dn = p3[2], xn = p3[3];  // step / state norms summed over the ranks' owned rows
-  if (tid != 0) return;
-  if (st->gmax <= o.gtol) {
-    st->status = ACS_STATUS_GTOL;
-    return;
-  }
-  const double Fn = fm + fq;
+  if (st->status != 0 || !st->pending) return;
+  st->pending = 0;
+  const double Fn = fm + fq, dn = p3[2], xn = p3[3];  // step / state norms summed over the owned rows
   st->iters += 1;
   st->dnorm = sqrt(dn);
   st->xnorm = sqrt(xn);
@@ -2429,6 +2433,33 @@ __global__ __launch_bounds__(256) void k_fte_lm_dist(FteDims d, FteState* __rest
     if (st->lam > 1e16) st->status = ACS_STATUS_STALLED;
   }
   if (st->status == 0 && st->iters >= o.max_iters) st->status = ACS_STATUS_MAXITER;
+  if (st->status == 0 && !st->relin) st->status = FTE_STATUS_SKIP;
+}
+
+// after the reduced solve of a live round: the gradient test on the summed gradient
+__global__ void k_dist_gtol(FteState* __restrict__ st, FteOptsDev o) {
+  if (threadIdx.x == 0 && st->status == 0 && st->gmax <= o.gtol) st->status = ACS_STATUS_GTOL;
+}
+
+// before / after the round's reduced system: a round that took a step forms it at the trial
+// state (copy cur ^ 1, linearised there for the trial cost) with the damping an acceptance
+// sets; the LM state is swapped for those kernels and restored after them
+__global__ void k_dist_spec(FteState* __restrict__ st, int enter) {
+  if (threadIdx.x != 0) return;
+  if (enter) {
+    if (st->status == FTE_STATUS_SKIP) st->status = 0;
+    if (st->status == 0 && st->pending) {
+      st->spec_on = 1;
+      st->save_cur = st->cur;
+      st->save_lam = st->lam;
+      st->cur ^= 1;
+      st->lam = fmax(st->lam * 0.1, 1e-15);
+    }
+  } else if (st->spec_on) {
+    st->spec_on = 0;
+    st->cur = st->save_cur;
+    st->lam = st->save_lam;
+  }
 }
 
 struct acs_fte_dist {
@@ -2442,23 +2473,33 @@ struct acs_fte_dist {
   FteOptsDev o;
   int R, rank, span, a0, bend, klev;
   int k_lo, k_hi, f_lo, f_hi, b_hi_build, c_lo, c_hi, own_lo, own_hi, out_lo, out_hi;
-  // phases 1-3 captured as hipGraphs on their first call (one graph launch instead of tens
-  // of kernel launches per phase); key = (payload pointer, stream)
+  // rounds captured as hipGraphs (one graph launch instead of ~60 kernel launches); key =
+  // (input payload, output payload, stream): two graphs for the two payload buffers
   struct Captured {
     hipGraphExec_t exec = nullptr;
     const void* ptr = nullptr;
+    const void* ptr2 = nullptr;
     hipStream_t stream = nullptr;
-  } g[3];
+  } g[2];
+  // status after each round: pinned ring of ACS_DIST_RING slots with completion events
+  int32_t* snap = nullptr;
+  hipEvent_t snap_ev[4] = {};
+  int64_t rounds = 0;
 };
+#define ACS_DIST_RING 4
 
 // Run `enqueue` (kernel launches on ctx->stream) through the phase's cached graph,
 // capturing it when the key changed; plain launches if capture is unavailable.
 template <typename F>
-static int dist_run_captured(acs_fte_dist* h, int which, const void* ptr, F enqueue) {
+static int dist_run_captured(acs_fte_dist* h, const void* ptr, const void* ptr2, F enqueue) {
   acs_ctx* ctx = h->ctx;
   hipStream_t s = ctx->stream;
+  int which = 0;
+  for (; which < 2; ++which)
+    if (h->g[which].exec && h->g[which].ptr == ptr && h->g[which].ptr2 == ptr2 && h->g[which].stream == s) break;
+  if (which == 2) which = (h->g[0].exec && !h->g[1].exec) ? 1 : 0;
   auto& c = h->g[which];
-  if (!c.exec || c.ptr != ptr || c.stream != s) {
+  if (!c.exec || c.ptr != ptr || c.ptr2 != ptr2 || c.stream != s) {
     if (c.exec) (void)hipGraphExecDestroy(c.exec);
     c.exec = nullptr;
     hipGraph_t graph = nullptr;
@@ -2471,6 +2512,7 @@ static int dist_run_captured(acs_fte_dist* h, int which, const void* ptr, F enqu
       }
       if (e == hipSuccess && graph && hipGraphInstantiate(&c.exec, graph, nullptr, nullptr, 0) == hipSuccess) {
         c.ptr = ptr;
+        c.ptr2 = ptr2;
         c.stream = s;
       } else {
         c.exec = nullptr;
@@ -2835,10 +2877,21 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
   std::memset(&st0, 0, sizeof(st0));
   st0.lam = op.lambda0;
   st0.relin = 1;
+  st0.first = 1;
   ACS_HIP(ctx, hipMemcpyAsync(h->S.b.st, &st0, sizeof(st0), hipMemcpyHostToDevice, ctx->stream));
   ACS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  bool snap_ok = hipHostMalloc((void**)&h->snap, sizeof(int32_t) * ACS_DIST_RING, hipHostMallocDefault) == hipSuccess;
+  for (auto& e : h->snap_ev)
+    if (snap_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      e = nullptr;
+      snap_ok = false;
+    }
+  if (!snap_ok) {
+    acs_fte_dist_destroy(h);
+    return acs_fail(ctx, ACS_E_HIP, "fte_dist: pinned status ring allocation failed");
+  }
   if (payload_sizes) {
-    payload_sizes[0] = (int64_t)h->Lo.n1;
+    payload_sizes[0] = (int64_t)(h->Lo.n1 + h->Lo.n3);
     payload_sizes[1] = (int64_t)h->Lo.n2;
     payload_sizes[2] = (int64_t)h->Lo.n3;
   }
@@ -2852,19 +2905,25 @@ int acs_fte_dist_destroy(acs_fte_dist* h) {
   (void)hipStreamSynchronize(h->ctx->stream);
   for (auto& c : h->g)
     if (c.exec) (void)hipGraphExecDestroy(c.exec);
+  for (auto& e : h->snap_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->snap) (void)hipHostFree(h->snap);
   if (h->own) (void)hipFree(h->own);
   if (h->own_red) (void)hipFree(h->own_red);
   delete h;
   return ACS_OK;
 }
 
-// cost of the owned terms at the current state -> p3 (before the first phase 4, init = 1)
-int acs_fte_dist_init(acs_fte_dist* h, double* p3) {
+static int dist_phase1_body(acs_fte_dist* h, double* p1);
+
+// payload of the starting state: the reduced system at X0 and the owned terms' cost
+int acs_fte_dist_init(acs_fte_dist* h, double* payload) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
   hipStream_t s = ctx->stream;
+  double* p3 = payload + h->Lo.n1;
   if (h->c_hi > h->c_lo)
     hipLaunchKernelGGL(k_fte_cost, dim3(h->c_hi - h->c_lo), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
                        b.tau, b.qinv, b.st, 0, h->c_lo, h->own_lo, h->own_hi, b.Fm, b.Fq);
@@ -2876,7 +2935,7 @@ int acs_fte_dist_init(acs_fte_dist* h, double* p3) {
                        b.meas, b.w, b.X, b.tau, b.st, 1, h->k_lo, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr,
                        (const double*)nullptr, b.Tc);
   ACS_HIP(ctx, hipGetLastError());
-  return ACS_OK;
+  return dist_phase1_body(h, payload);
 }
 
 static int dist_phase1_body(acs_fte_dist* h, double* p1) {
@@ -2926,6 +2985,7 @@ static int dist_phase2_body(acs_fte_dist* h, const double* p1) {
   hipLaunchKernelGGL(k_red_part, dim3(1), dim3(256), 0, s, nE, h->Lo, b.st, p1, r.part);
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, dr, b.st, (const double*)r.Wc, r.part, r.gmaxp, b.tau, r.dcv,
                      b.dtau, b.bad);
+  hipLaunchKernelGGL(k_dist_gtol, dim3(1), dim3(64), 0, s, b.st, h->o);
   for (int lv = dr.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (dr.nblk - st + 2 * st - 1) / (2 * st);
@@ -2976,19 +3036,44 @@ static int dist_phase3_body(acs_fte_dist* h, double* p3) {
   return ACS_OK;
 }
 
-int acs_fte_dist_phase1(acs_fte_dist* h, double* p1) {
+// one LM step: decide on the pending step (summed cost in `in`), solve the summed reduced
+// system of `in`, step the chain, the new trial cost -> `out`, then the reduced system at the
+// trial state (or, after a rejection, at the unchanged state) -> `out`
+int acs_fte_dist_round(acs_fte_dist* h, const double* in, double* out) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
-  return dist_run_captured(h, 0, p1, [&] { return dist_phase1_body(h, p1); });
+  ACS_CHECK(h ? h->ctx : nullptr, h && in && out && in != out, "fte_dist_round: two distinct payload buffers");
+  acs_ctx* ctx = h->ctx;
+  FteBuffers& b = h->S.b;
+  hipStream_t s = ctx->stream;
+  const size_t n1 = h->Lo.n1;
+  int rc = dist_run_captured(h, in, out, [&] {
+    hipLaunchKernelGGL(k_dist_decide, dim3(1), dim3(64), 0, s, b.st, h->o, in + n1);
+    int r2 = dist_phase2_body(h, in);
+    if (r2) return r2;
+    if ((r2 = dist_phase3_body(h, out + n1))) return r2;
+    hipLaunchKernelGGL(k_dist_spec, dim3(1), dim3(64), 0, s, b.st, 1);
+    if ((r2 = dist_phase1_body(h, out))) return r2;
+    hipLaunchKernelGGL(k_dist_spec, dim3(1), dim3(64), 0, s, b.st, 0);
+    ACS_HIP(ctx, hipGetLastError());
+    return ACS_OK;
+  });
+  if (rc) return rc;
+  const int slot = (int)(h->rounds % ACS_DIST_RING);
+  ACS_HIP(ctx, hipMemcpyAsync(h->snap + slot, &b.st->status, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  ACS_HIP(ctx, hipEventRecord(h->snap_ev[slot], s));
+  h->rounds++;
+  return ACS_OK;
 }
 
-int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1) {
+// LM status after round r (waits for that round only)
+int acs_fte_dist_poll(acs_fte_dist* h, int64_t round, int32_t* status) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
-  return dist_run_captured(h, 1, p1, [&] { return dist_phase2_body(h, p1); });
-}
-
-int acs_fte_dist_phase3(acs_fte_dist* h, double* p3) {
-  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
-  return dist_run_captured(h, 2, p3, [&] { return dist_phase3_body(h, p3); });
+  ACS_CHECK(h ? h->ctx : nullptr, h && status && round >= 0 && round < h->rounds && round >= h->rounds - ACS_DIST_RING,
+            "fte_dist_poll: round %lld not among the last %d enqueued", (long long)round, ACS_DIST_RING);
+  const int slot = (int)(round % ACS_DIST_RING);
+  ACS_HIP(h->ctx, hipEventSynchronize(h->snap_ev[slot]));
+  *status = h->snap[slot];
+  return ACS_OK;
 }
 
 int acs_fte_dist_gather(acs_fte_dist* h, double* p2) {
@@ -3011,21 +3096,6 @@ int acs_fte_dist_scatter(acs_fte_dist* h, const double* p2) {
   FteBuffers& b = h->S.b;
   hipLaunchKernelGGL(k_dist_x_in, dim3(64), dim3(256), 0, ctx->stream, d, b.st, p2, b.X);
   ACS_HIP(ctx, hipGetLastError());
-  return ACS_OK;
-}
-
-int acs_fte_dist_phase4(acs_fte_dist* h, const double* p3, int32_t init, int32_t* status) {
-  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
-  acs_ctx* ctx = h->ctx;
-  const FteDims& d = h->S.d;
-  FteBuffers& b = h->S.b;
-  hipStream_t s = ctx->stream;
-  hipLaunchKernelGGL(k_fte_lm_dist, dim3(1), dim3(256), 0, s, d, b.st, h->o, init, p3);
-  ACS_HIP(ctx, hipGetLastError());
-  int32_t stv = 0;
-  ACS_HIP(ctx, hipMemcpyAsync(&stv, &b.st->status, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  ACS_HIP(ctx, hipStreamSynchronize(s));
-  if (status) *status = stv;
   return ACS_OK;
 }
 

@@ -5,16 +5,18 @@ Frame-window FTE:
 
 One process per GPU (torchrun); ranks split the trajectory's 3-frame super-blocks into
 chains that share their end blocks (include/acinoset_hip.h, acs_fte_dist_*). Every LM
-iteration exchanges two sums over the ranks:
-
-  p1  the chain ends' reduced normal-equation blocks + tau border (~1 MB at 8 ranks)
-  p3  the costs of the owned terms and the step / state norms of the owned rows (4 doubles)
-
-with `torch.distributed.all_reduce` (RCCL over xGMI on the "nccl" backend; gloo in the CPU
-tests). Every rank then runs the same reduced solve, back-substitutes and steps its own
-chain (X lives on the chain only: the terms a rank owns never read other rows), and takes
-the same accept/reject decision. The solution rows (p2, n_blocks x BP) cross the ranks
-once, after the last iteration.
+step is ONE all-reduce (sum) of one payload: the chain ends' reduced normal-equation blocks +
+tau border (~1 MB at 8 ranks) and the previous step's trial cost and step / state norms (4
+doubles), with `torch.distributed.all_reduce` (RCCL over xGMI on the "nccl" backend; gloo in
+the CPU tests). A round, on the summed payload: every rank takes the same accept / reject
+decision on the pending step, runs the same reduced solve, back-substitutes and steps its
+own chain (X lives on the chain only: the terms a rank owns never read other rows), and
+packs the new step's cost and the reduced system at its trial state - formed speculatively
+with the damping an acceptance gives; a rejected step costs one extra round that re-forms
+the reduced system at the unchanged state. Decisions are taken on the device and the host
+reads a round's status one round late (`poll`), so the next round and its all-reduce are
+queued before the previous one has finished. The solution rows (n_blocks x BP) cross the
+ranks once, after the last round.
 
 `lm_loop` is the protocol, independent of the backend: the HIP ranks below, or the numpy
 restatement in oracle/fte_dist.py that the CPU tests plug in.
@@ -34,23 +36,20 @@ def lm_loop(ranks, allreduce):
     """Drive the distributed LM. `ranks`: the backends living in this process (one per
     process under torch.distributed, several for the single-process emulation);
     `allreduce(list_of_payloads)` sums the i-th payload over all ranks in place.
-    Per LM iteration: the reduced system (p1) and 4 doubles (p3) cross the ranks; every
-    rank steps its own chain; the solution rows (p2) are exchanged once, at the end."""
-    p3 = [r.init() for r in ranks]
-    allreduce(p3)
-    for r, p in zip(ranks, p3):
-        r.phase4(p, init=True)
+    One all-reduce per round; round k's status is read after round k + 1 is queued (a
+    round after the stop is a no-op on every rank). Returns the final status."""
+    P = [r.init() for r in ranks]
+    allreduce(P)
+    k = 0
     while True:
-        p1 = [r.phase1() for r in ranks]
-        allreduce(p1)
-        for r, a in zip(ranks, p1):
-            r.phase2(a)
-        p3 = [r.phase3() for r in ranks]
-        allreduce(p3)
-        st = [r.phase4(a) for r, a in zip(ranks, p3)]
-        assert len(set(st)) == 1, f'ranks diverged: {st}'
-        if st[0] != 0:
-            break
+        P = [r.round(p) for r, p in zip(ranks, P)]
+        allreduce(P)
+        if k >= 1:
+            st = [r.poll(k - 1) for r in ranks]
+            assert len(set(st)) == 1, f'ranks diverged: {st}'
+            if st[0] != 0:
+                break
+        k += 1
     p2 = [r.gather() for r in ranks]
     allreduce(p2)
     for r, a in zip(ranks, p2):
@@ -130,38 +129,36 @@ class HipFteRank:
                   'acs_fte_dist_create')
         self.h = h
         dev = torch.device('cuda', ctx.device)
-        self.p = [torch.zeros(int(n), dtype=torch.float64, device=dev) for n in sizes]
+        # two round payloads (a round reads one and writes the other) and the solution rows
+        self.bufs = [torch.zeros(int(sizes[0]), dtype=torch.float64, device=dev) for _ in range(2)]
+        self.p2 = torch.zeros(int(sizes[1]), dtype=torch.float64, device=dev)
+        self.which = 0
 
     def _ptr(self, t):
         return C.c_void_p(t.data_ptr())
 
     def init(self):
-        self.ctx.check(self.ctx.lib.acs_fte_dist_init(self.h, self._ptr(self.p[2])), 'acs_fte_dist_init')
-        return self.p[2]
+        self.which = 0
+        self.ctx.check(self.ctx.lib.acs_fte_dist_init(self.h, self._ptr(self.bufs[0])), 'acs_fte_dist_init')
+        return self.bufs[0]
 
-    def phase1(self):
-        self.ctx.check(self.ctx.lib.acs_fte_dist_phase1(self.h, self._ptr(self.p[0])), 'acs_fte_dist_phase1')
-        return self.p[0]
+    def round(self, pin):
+        out = self.bufs[self.which ^ 1]
+        self.ctx.check(self.ctx.lib.acs_fte_dist_round(self.h, self._ptr(pin), self._ptr(out)), 'acs_fte_dist_round')
+        self.which ^= 1
+        return out
 
-    def phase2(self, p1):
-        self.ctx.check(self.ctx.lib.acs_fte_dist_phase2(self.h, self._ptr(p1)), 'acs_fte_dist_phase2')
-
-    def phase3(self):
-        self.ctx.check(self.ctx.lib.acs_fte_dist_phase3(self.h, self._ptr(self.p[2])), 'acs_fte_dist_phase3')
-        return self.p[2]
+    def poll(self, k):
+        st = C.c_int32(0)
+        self.ctx.check(self.ctx.lib.acs_fte_dist_poll(self.h, int(k), C.byref(st)), 'acs_fte_dist_poll')
+        return st.value
 
     def gather(self):
-        self.ctx.check(self.ctx.lib.acs_fte_dist_gather(self.h, self._ptr(self.p[1])), 'acs_fte_dist_gather')
-        return self.p[1]
+        self.ctx.check(self.ctx.lib.acs_fte_dist_gather(self.h, self._ptr(self.p2)), 'acs_fte_dist_gather')
+        return self.p2
 
     def scatter(self, p2):
         self.ctx.check(self.ctx.lib.acs_fte_dist_scatter(self.h, self._ptr(p2)), 'acs_fte_dist_scatter')
-
-    def phase4(self, p3, init=False):
-        st = C.c_int32(0)
-        self.ctx.check(self.ctx.lib.acs_fte_dist_phase4(self.h, self._ptr(p3), int(bool(init)), C.byref(st)),
-                       'acs_fte_dist_phase4')
-        return st.value
 
     def result(self):
         X = np.empty((self.N + 2, self.P))

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ACS_ABI_VERSION 2
+#define ACS_ABI_VERSION 3
 #define ACS_CAM_STRIDE 20
 
 /* status codes */
@@ -185,21 +185,26 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
 
 /* ---- §8(e): frame-window distributed FTE (configs[3]) --------------------------------
  * One handle per rank (rank of world); every rank gets the full-size inputs of
- * acs_fte_solve. The super-blocks of 3 frames are split
- * into `world` chains that share their end blocks; a term belongs to the chain holding its
- * lowest row. X is kept only on the rank's own chain (its rows and both shared end blocks).
- * One LM iteration, with ONE all-reduce of the reduced system and one of 4 doubles:
- *   phase1(p1) -> all-reduce(p1, sum) -> phase2(p1) -> phase3(p3) -> all-reduce(p3, sum)
- *   -> phase4(p3, 0, &status)
- * starting with init(p3) -> all-reduce(p3) -> phase4(p3, 1, NULL), and after the last
- * iteration gather(p2) -> all-reduce(p2) -> scatter(p2) before result(). Payloads are
- * DEVICE buffers of payload_sizes[0..2] doubles (p1: chain-end blocks of the reduced
- * system, ~ (world+1) (2 BP^2 + BP GR) doubles; p2: the solution rows, n_blocks x BP,
- * exchanged once per solve; p3: 2 costs + step / state norms of the owned rows). Every
- * rank runs the same reduced solve on the summed p1, back-substitutes and steps its own
- * chain, and takes the same decisions; the result equals acs_fte_solve up to summation
- * order. Phases are asynchronous on the context stream except phase4, which returns the
- * LM status (0 = running).
+ * acs_fte_solve. The super-blocks of 3 frames are split into `world` chains that share their
+ * end blocks; a term belongs to the chain holding its lowest row. X is kept only on the
+ * rank's own chain (its rows and both shared end blocks).
+ * ONE all-reduce (sum) per LM step, of one DEVICE payload of payload_sizes[0] doubles: the
+ * chain ends' reduced system (~ (world+1) (2 BP^2 + BP GR) doubles) followed by the pending
+ * step's trial cost and step / state norms (4 doubles):
+ *   init(P0) -> all-reduce(P0) -> round(P0, P1) -> all-reduce(P1) -> round(P1, P0) -> ...
+ * round(in, out), on the summed `in`: every rank takes the same accept / reject decision on
+ * the pending step (its cost is in `in`), solves the reduced system of `in`, back-substitutes
+ * and steps its own chain, and writes into `out` the new step's trial cost and the reduced
+ * system at the trial state, formed speculatively with the damping an acceptance gives
+ * (linearised there already for the trial cost). After a rejection the round writes the
+ * reduced system at the unchanged state with the new damping instead, and no step: a
+ * rejection costs one extra round. Decisions are taken on the device; a round never waits
+ * for the host. poll(h, r, &status) waits for round r (0-based) only and returns the LM
+ * status after it (0 = running), so a host can queue round r + 1 first (a round after the
+ * stop changes nothing). Then gather(p2) -> all-reduce(p2) -> scatter(p2) (the solution
+ * rows, n_blocks x BP doubles = payload_sizes[1], once per solve) before result(). Every
+ * rank runs the same reduced solve and takes the same decisions; the result equals
+ * acs_fte_solve up to summation order.
  * shutter_delay with sd_mode 1 ('variable') is single-GPU only (ACS_E_INVALID here).   */
 typedef struct acs_fte_dist acs_fte_dist;
 int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
@@ -208,11 +213,9 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
                         const double* qinv, int32_t sd_mode, int32_t intermode, const double* X,
                         const double* tau, const acs_fte_opts* opts, int32_t rank, int32_t world,
                         acs_fte_dist** out, int64_t* payload_sizes, uint32_t flags);
-int acs_fte_dist_init(acs_fte_dist* h, double* p3);
-int acs_fte_dist_phase1(acs_fte_dist* h, double* p1);
-int acs_fte_dist_phase2(acs_fte_dist* h, const double* p1);
-int acs_fte_dist_phase3(acs_fte_dist* h, double* p3);
-int acs_fte_dist_phase4(acs_fte_dist* h, const double* p3, int32_t init, int32_t* status);
+int acs_fte_dist_init(acs_fte_dist* h, double* payload);
+int acs_fte_dist_round(acs_fte_dist* h, const double* in, double* out);
+int acs_fte_dist_poll(acs_fte_dist* h, int64_t round, int32_t* status);
 int acs_fte_dist_gather(acs_fte_dist* h, double* p2);
 int acs_fte_dist_scatter(acs_fte_dist* h, const double* p2);
 int acs_fte_dist_result(acs_fte_dist* h, double* X, double* tau, acs_fte_report* report, uint32_t flags);

@@ -23,7 +23,12 @@ monolithic oracle (oracle/fte.py solve):
   squared step / state norms of the owned rows (blocks [a_r, a_r + 2^k), the last rank
   also its end; the delays counted on rank 0); the accept/reject rule is oracle/fte.py
   solve's;
-* after the last iteration payload 2 = the owned rows of the solution (a sum over ranks
+* rounds (one all-reduce per LM step): payloads 1 and 3 travel together. A round decides
+  on the pending step (its summed cost), solves the summed reduced system, steps the chain
+  and returns the new step's cost with the reduced system at the trial state, formed with
+  the damping an acceptance gives (lam / 10, floor 1e-15). After a rejection (lam * 10) the
+  round skips the solve and returns the reduced system at the unchanged state instead;
+* after the last round payload 2 = the owned rows of the solution (a sum over ranks
   rebuilds X everywhere).
 
 The payload layouts are this module's own (dense); only their sums cross ranks.
@@ -78,17 +83,48 @@ class OracleFteRank:
         self.n2 = M * P
         self.n3 = 4
 
-    # ---- protocol ----------------------------------------------------------------------
+    # ---- protocol (one payload per round: [p1 | p3]) --------------------------------------
     def init(self):
         _, fm, fq = self.prob.cost(self.X, self.tau, self.frames, self.stencils)
-        return np.array([fm, fq])
+        _, H, g = self.prob.linearize(self.X, self.tau, self.frames, self.stencils)
+        self.H, self.g = H.toarray(), g
+        self.first, self.pending, self.statuses = True, False, []
+        return np.concatenate([self.phase1(self.H, self.g, self.lam), [fm, fq, 0.0, 0.0]])
 
-    def phase1(self):
+    def round(self, P):
+        p1, p3 = P[:self.n1], P[self.n1:]
+        out = np.zeros(self.n1 + self.n3)
+        skip = False
+        if self.first:
+            self.first = False
+            self.F = self.F0 = float(p3[0] + p3[1])
+        elif self.status == 0 and self.pending:
+            self.pending = False
+            skip = self.phase4(p3) == 0 and not self.relin          # rejected: re-form only
+        if self.status == 0 and not skip:
+            self.phase2(p1)
+            if self.gmax <= self.opts['gtol']:
+                self.status = 1
+        if self.status == 0:
+            if not skip:
+                out[self.n1:] = self.phase3()
+                self.pending = True
+                # speculative: the reduced system at the trial state, damped as after an
+                # acceptance (linearised there for the trial cost)
+                _, Hn, gn = self.prob.linearize(self.Xn, self.taun, self.frames, self.stencils)
+                self.Hn, self.gn = Hn.toarray(), gn
+                out[:self.n1] = self.phase1(self.Hn, self.gn, max(self.lam * 0.1, 1e-15))
+            else:
+                out[:self.n1] = self.phase1(self.H, self.g, self.lam)
+        self.statuses.append(self.status)
+        return out
+
+    def poll(self, k):
+        return self.statuses[k]
+
+    def phase1(self, H, g, lam):
         p = self.prob
-        if self.relin:
-            _, H, g = p.linearize(self.X, self.tau, self.frames, self.stencils)
-            self.H, self.g = H.toarray(), g
-        H, g, I, B, lam = self.H, self.g, self.I, self.B, self.lam
+        I, B = self.I, self.B
         HII = H[np.ix_(I, I)].copy()
         HII[np.diag_indices_from(HII)] += lam * np.maximum(np.diag(HII), 1e-12)
         HIB, HBB = H[np.ix_(I, B)], H[np.ix_(B, B)]
@@ -155,17 +191,10 @@ class OracleFteRank:
         _, fm, fq = self.prob.cost(self.Xn, self.taun, self.frames, self.stencils)
         return np.array([fm, fq, self.dn2, self.xn2])
 
-    def phase4(self, p3, init=False):
+    def phase4(self, p3):
+        """Accept / reject the pending step on its summed cost (oracle/fte.py solve)."""
         o = self.opts
         Fn = float(p3[0] + p3[1])
-        if init:
-            self.F = self.F0 = Fn
-            return 0
-        if self.status:
-            return self.status
-        if self.gmax <= o['gtol']:
-            self.status = 1
-            return self.status
         self.iters += 1
         dn, xn = np.sqrt(p3[2]), np.sqrt(p3[3])
         small = dn <= o['xtol'] * (o['xtol'] + xn)
@@ -174,6 +203,7 @@ class OracleFteRank:
             self.nacc += 1
             self.F = Fn
             self.X, self.tau = self.Xn, self.taun
+            self.H, self.g = self.Hn, self.gn
             self.lam = max(self.lam * 0.1, 1e-15)
             self.relin = True
             if fconv:

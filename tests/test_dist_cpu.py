@@ -53,6 +53,47 @@ def test_dist_protocol_matches_monolithic(mode, N, sd, inter, world):
     _check(outs[0], ref)
 
 
+@pytest.mark.parametrize('reject_at', [None, 3])
+def test_dist_one_allreduce_per_lm_step(reject_at):
+    """The round protocol: one all-reduce per LM step (init and the final gather aside),
+    one more per rejected step, one more for the round queued before the stop was read.
+    These problems never reject a step on their own, so `reject_at` inflates the 4th step's
+    trial cost on every rank: the rejection, its re-formed round and the recovery run, and
+    the solve still lands on the monolithic solution."""
+    prob, X0 = _problem('head', 40, True, 'vel')
+    world = 3
+    ref = ofte.solve(prob, X0, max_iters=30)
+    ranks = [odist.OracleFteRank(prob, X0, None, r, world, max_iters=30) for r in range(world)]
+    if reject_at is not None:
+        for r in ranks:
+            def ph3(_orig=r.phase3, _r=r):
+                p3 = _orig()
+                if _r.iters == reject_at:
+                    p3 = p3.copy()
+                    p3[0] += 1e6 / world
+                return p3
+            r.phase3 = ph3
+    sizes = []
+
+    def counting(payloads):
+        sizes.append(len(payloads[0]))
+        dist.local_allreduce(payloads)
+    dist.lm_loop(ranks, counting)
+    X, tau, info = ranks[0].result()
+    n_rej = info['iters'] - info['n_accepted']
+    rounds = len(sizes) - 2                       # minus init and the final gather
+    assert all(n == ranks[0].n1 + ranks[0].n3 for n in sizes[:-1])
+    # round 0 forms step 1, round k decides step k and forms step k + 1 (a rejected step
+    # adds the round that re-forms the system); plus the round queued before the stop was read
+    assert rounds == info['iters'] + n_rej + 2, (rounds, info)
+    if reject_at is None:
+        _check((X, tau, info), ref)
+    else:
+        assert n_rej == 1 and info['status'] in (2, 3)
+        np.testing.assert_allclose(X, ref[0], rtol=0, atol=1e-8)
+        assert abs(info['cost_after'] - ref[2]['cost_after']) <= 1e-10 * ref[2]['cost_after']
+
+
 def test_dist_chain_partition_covers_every_term():
     """Every frame and stencil is owned by exactly one rank; chains tile the blocks."""
     prob, X0 = _problem('head', 50)
