@@ -901,6 +901,10 @@ __global__ __launch_bounds__(1024) void k_cr_build(FteDims d, const FteState* __
 // make an HBM round trip. Same arithmetic and order as the two kernels, so the same bits.
 // Runs every iteration (the damping changes on a rejected step; the rows are then
 // re-assembled from the unchanged linearisation).
+// Frame-window ranks (dist path): blocks b0 + blockIdx.x of the chain, only the terms the
+// rank owns (lowest row in [lo, hi)), the chain ends end_l / end_r left undamped (they are
+// damped in the reduced system with the summed raw diagonals), and the raw diagonal and
+// gradient of every row written to rdiag / graw (row layout f P + p) for the payload.
 template <int NB>
 __global__ __launch_bounds__(1024) void k_cr_assemble_build(FteDims d, const double* __restrict__ Xbuf,
                                                             const double* __restrict__ qinv,
@@ -908,10 +912,13 @@ __global__ __launch_bounds__(1024) void k_cr_assemble_build(FteDims d, const dou
                                                             const double* __restrict__ Hloc,
                                                             const double* __restrict__ gloc, double* __restrict__ Dc,
                                                             double* __restrict__ Ec, double* __restrict__ GBc,
-                                                            double* __restrict__ gmaxp) {
+                                                            double* __restrict__ gmaxp, int b0, int lo, int hi,
+                                                            int end_l, int end_r, double* __restrict__ rdiag,
+                                                            double* __restrict__ graw) {
   if (st->status != 0) return;
   constexpr int BP = 16 * NB, NE = (BP * BP + 1023) / 1024;
-  const int i = blockIdx.x, tid = threadIdx.x;
+  const int i = blockIdx.x + b0, tid = threadIdx.x;
+  const bool damp = i != end_l && i != end_r;
   const int P = d.P, PP = P * P, GR = d.GR, Cg = d.Cg;
   const int cur = st->cur;
   Hloc += (size_t)cur * d.N * FTE_NZP * FTE_NZP;
@@ -933,8 +940,15 @@ __global__ __launch_bounds__(1024) void k_cr_assemble_build(FteDims d, const dou
     const int f = 3 * i + a;
     const bool act = grp < 3 && f < d.M;
     // inactive threads (the 64 spare ones, rows past the sequence) start past every loop
-    assemble_row(d, f, X, qinv, 0, INT_MAX, Hloc, gloc, rowA(a), rowg(a), rowB(a), act ? tid - 320 * grp : 1 << 30,
+    assemble_row(d, f, X, qinv, lo, hi, Hloc, gloc, rowA(a), rowg(a), rowB(a), act ? tid - 320 * grp : 1 << 30,
                  320);
+  }
+  if (rdiag && tid < 3 * d.P) {
+    const int a = tid / d.P, p = tid - a * d.P, f = 3 * i + a;
+    if (f < d.M) {
+      rdiag[(size_t)f * d.P + p] = rowA(a)[p * d.P + p];
+      graw[(size_t)f * d.P + p] = rowg(a)[p];
+    }
   }
   // |g| max of each row (max is order-free): wave a < 3 takes row 3i + a
   if (tid < 192) {
@@ -958,7 +972,7 @@ __global__ __launch_bounds__(1024) void k_cr_assemble_build(FteDims d, const dou
     double dv = 0.0, ev = 0.0;
     if (rin && cin) {
       double v = (ar >= ac) ? rowA(ar)[(ar - ac) * PP + pr * P + pc] : rowA(ac)[(ac - ar) * PP + pc * P + pr];
-      if (r == c) v += lam * fmax(v, 1e-12);
+      if (r == c && damp) v += lam * fmax(v, 1e-12);
       dv = v;
     } else if (r == c) {
       dv = 1.0;  // padding: identity
@@ -2128,10 +2142,14 @@ static void cr_launch_top(const FteDims& d, hipStream_t s, int nlev, int a0, int
 #undef CR_TOP
 }
 
-static void cr_launch_assemble_build(const FteDims& d, hipStream_t s, const FteBuffers& b) {
+static void cr_launch_assemble_build(const FteDims& d, hipStream_t s, const FteBuffers& b, int b0 = 0,
+                                     int nblk = -1, int lo = 0, int hi = INT_MAX, int end_l = -1, int end_r = -1,
+                                     double* rdiag = nullptr, double* graw = nullptr) {
+  if (nblk < 0) nblk = d.nblk;
+  if (nblk <= 0) return;
 #define CR_ABUILD(nb)                                                                                          \
-  hipLaunchKernelGGL((k_cr_assemble_build<nb>), dim3(d.nblk), dim3(1024), asm_build_lds_bytes(d), s, d, b.X, \
-                     b.qinv, b.st, b.Hloc, b.gloc, b.Dc, b.Ec, b.GBc, b.gmaxp)
+  hipLaunchKernelGGL((k_cr_assemble_build<nb>), dim3(nblk), dim3(1024), asm_build_lds_bytes(d), s, d, b.X, \
+                     b.qinv, b.st, b.Hloc, b.gloc, b.Dc, b.Ec, b.GBc, b.gmaxp, b0, lo, hi, end_l, end_r, rdiag, graw)
   switch (d.BP >> 4) {
     case 1: CR_ABUILD(1); break;
     case 2: CR_ABUILD(2); break;
@@ -2232,13 +2250,13 @@ static DistLayout dist_layout(const FteDims& d, int R) {
 __global__ __launch_bounds__(256) void k_dist_pack(FteDims d, const FteState* __restrict__ st, DistLayout Lo,
                                                    int rank, int a0, int bend, const double* __restrict__ Dc,
                                                    const double* __restrict__ Ec, const double* __restrict__ GBc,
-                                                   const double* __restrict__ Ab, const double* __restrict__ gb,
+                                                   const double* __restrict__ rdiag, const double* __restrict__ gb,
                                                    double* __restrict__ p1) {
   if (st->status != 0) return;
   const int side = blockIdx.y;  // 0 left end, 1 right end
   const int blk = side ? bend : a0, q = rank + side;
   if (blk >= d.nblk) return;
-  const int BP = d.BP, GR = d.GR, P = d.P, PP = P * P;
+  const int BP = d.BP, GR = d.GR, P = d.P;
   const size_t nBB = (size_t)BP * BP;
   for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < nBB; e += (size_t)gridDim.x * blockDim.x) {
     p1[Lo.oD + q * nBB + e] = Dc[(size_t)blk * nBB + e];
@@ -2252,7 +2270,7 @@ __global__ __launch_bounds__(256) void k_dist_pack(FteDims d, const FteState* __
       const int fr = 3 * blk + r / P, pr = r % P;
       const bool in = r < 3 * P && fr < d.M;
       p1[Lo.oGraw + (size_t)q * BP + r] = in ? gb[(size_t)fr * P + pr] : 0.0;
-      p1[Lo.oRdiag + (size_t)q * BP + r] = in ? Ab[(size_t)fr * 4 * PP + pr * P + pr] : 0.0;
+      p1[Lo.oRdiag + (size_t)q * BP + r] = in ? rdiag[(size_t)fr * P + pr] : 0.0;
     }
   }
 }
@@ -2947,16 +2965,17 @@ static int dist_phase1_body(acs_fte_dist* h, double* p1) {
   ACS_HIP(ctx, hipMemsetAsync(p1, 0, sizeof(double) * h->Lo.n1, s));
   if (h->a0 < d.nblk) {
     // the linearisation of X[cur] is there already (init, or the speculative one of phase 3)
-    hipLaunchKernelGGL(k_fte_assemble, dim3(h->f_hi - h->f_lo), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, 0,
-                       h->f_lo, h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1);
+    // the chain's rows assembled in LDS and its super-blocks built in one pass (the banded
+    // rows never reach HBM), as the single-GPU solve; the ends' raw diagonals / gradients
+    // go to Adiag / gb (row layout) for the payload
     const int top = std::min(h->bend, d.nblk - 1);
-    cr_launch_build(d, s, top - h->a0 + 1, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, h->a0, h->a0, h->bend, nullptr);
+    cr_launch_assemble_build(d, s, b, h->a0, top - h->a0 + 1, h->own_lo, h->own_hi, h->a0, h->bend, b.Adiag, b.gb);
     const double* Efin = dist_local_cr(h);
     hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part,
                        h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk), 1,
                        (const double*)b.Tc);
     hipLaunchKernelGGL(k_dist_pack, dim3(32, 2), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.Dc, Efin,
-                       b.GBc, b.Ab, b.gb, p1);
+                       b.GBc, b.Adiag, b.gb, p1);
     hipLaunchKernelGGL(k_dist_pack_small, dim3(1), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.part,
                        b.gmaxp, p1);
   }

@@ -543,7 +543,7 @@ def bench_pipeline(ctx, torch, stream, world, rank, n_seq=80, n_frames=250, n_ca
 
 def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl', steps=3):
     """configs[3]: one FTE trajectory of `n_frames` frames; with W ranks its super-blocks
-    are split into W frame windows (acinoset_amd.dist, two all-reduces per LM step over
+    are split into W frame windows (acinoset_amd.dist, one all-reduce per LM step over
     RCCL). Strong scaling: the total work is fixed. W = 1 runs acs_fte_solve. Inputs are
     resident in HBM on every rank before the timed solves (device pointers)."""
     import torch.distributed as tdist
@@ -595,8 +595,9 @@ def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl',
             'ranks': world, 'scaling': 'strong', 'frames_per_s': n_frames / dt, 'ms_per_solve': dt * 1e3,
             'status': rep['status_name'], 'iters': rep['iters'], 'cost_after': rep['cost_after'],
             'pos_rms_vs_truth_m': pos_rms, 'tau_err_max_s': float(np.abs(tau - seq.tau).max()),
-            'exchange': 'none' if world == 1 else (f'torch.distributed {exchange} all-reduce x2 per LM step '
-                                                    '(reduced system, 4 doubles) + solution rows once')}
+            'exchange': 'none' if world == 1 else (f'torch.distributed {exchange}: one all-reduce per LM step '
+                                                    '(chain-end reduced system + trial cost, one payload) + the '
+                                                    'solution rows once')}
 
 
 def fte_cpu_baseline(wl):

@@ -4,7 +4,11 @@ flops per launch.
 
 HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
 WRITE_SIZE come from separate passes, are reported in KiB, and on gfx950 FETCH_SIZE counts
-half of the bytes of wide coalesced reads (x2 correction; WRITE_SIZE is exact).
+half of the bytes of wide coalesced reads (16 B per lane); other widths are uncalibrated.
+So the x2 correction applies only to the share of a kernel's reads that are 16-B-per-lane
+streams (WIDE_SHARE below, from the kernel's own load widths); the rest is taken as
+counted (fetch_bytes = FETCH_SIZE x (1 + wide share)), and kernels without an entry are
+reported uncorrected with `fetch_calibrated: false`.
 FP64 flops = 64 lanes x (2 FMA + ADD + MUL + TRANS) wave instructions (SQ_INSTS_VALU_*_F64;
 an upper bound when lanes are masked off).
 
@@ -14,6 +18,12 @@ import json
 import sys
 
 import pandas as pd
+
+
+# share of the algorithmic read bytes loaded 16 B per lane (double2), per kernel:
+# k_sba_lm reads per point 16 B x C of observations (double2 per lane), C mask bytes
+# (1 B per lane) and 24 B of start point (8-B loads): 96 / (96 + 6 + 24) at C = 6
+WIDE_SHARE = {'k_sba_lm': 96.0 / 126.0}
 
 
 def load(prefix, kind):
@@ -36,7 +46,11 @@ def main(prefix, out):
     for key, c in rows.items():
         r = {}
         if 'FETCH_SIZE' in c:
-            r['fetch_bytes'] = 2 * 1024 * c['FETCH_SIZE']
+            kname = key.split('@')[0]
+            share = WIDE_SHARE.get(kname)
+            r['fetch_bytes'] = 1024 * c['FETCH_SIZE'] * (1.0 + (share or 0.0))
+            r['fetch_calibrated'] = share is not None
+            r['fetch_wide_share'] = share
         if 'WRITE_SIZE' in c:
             r['write_bytes'] = 1024 * c['WRITE_SIZE']
         if 'fetch_bytes' in r and 'write_bytes' in r:
