@@ -32,13 +32,19 @@ if [[ $STEPS == *all* || $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
   run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_${TAG}" -o run -- python3 "$REPO/bench.py" --no-cpu-baseline --steps 200 --warmup 20 ${BENCH_ARGS:-}
 fi
+if [[ $STEPS == *ftetrace* ]]; then
+  export TMPDIR=/tmp
+  run ftetrace 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/ftetrace_${TAG}" -o run -- python3 "$REPO/tools/prof_fte.py" --frames ${FTE_FRAMES:-1000}
+  python tools/fte_iter_breakdown.py "$OUT/ftetrace_${TAG}" ${FTE_FRAMES:-1000} > "$OUT/fte_breakdown_${TAG}.log" 2>&1 || true
+  tail -n 3 "$OUT/fte_breakdown_${TAG}.log"
+fi
 if [[ $STEPS == *list* ]]; then
   run counters 120 rocprofv3 -L
 fi
 if [[ $STEPS == *pmc* ]]; then
   # HBM traffic (guide: separate passes; FETCH_SIZE x2 on gfx950) and FP64 VALU counts
   export TMPDIR=/tmp
-  PMC_ARGS="--no-cpu-baseline --no-fte --steps 3 --warmup 1"
+  PMC_ARGS="--no-cpu-baseline --no-fte --steps 3 --warmup 1 --ekf-seqs 0 --pipeline-seqs 0 --window-frames 0"
   PMC_VALU=${PMC_VALU:-"SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAVES SQ_INSTS_SALU SQ_WAVE_CYCLES"}
   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_${TAG}_fetch" -o run -- python3 "$REPO/bench.py" $PMC_ARGS
   run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_${TAG}_write" -o run -- python3 "$REPO/bench.py" $PMC_ARGS
