@@ -671,7 +671,8 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
                                                       const double* __restrict__ gloc, double* __restrict__ Ab,
                                                       double* __restrict__ gb, double* __restrict__ Bt,
                                                       double* __restrict__ gmaxp, double* __restrict__ Adiag,
-                                                      int hsel) {
+                                                      int hsel, double* __restrict__ graw = nullptr,
+                                                      double* __restrict__ gmaxt = nullptr) {
   // Terms are owned by the lowest X row they touch: frame k (rows k..k+2) iff lo <= k < hi,
   // model stencil m (rows m-3..m) iff lo <= m-3 < hi. The single-GPU solve owns all terms;
   // a frame-window rank owns the terms starting in its window (dist path below).
@@ -719,10 +720,17 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
   assemble_row(d, f, X, qinv, lo, hi, Hloc, gloc, A, g, B, tid, nth);
   double mx = 0.0;
   for (int i = tid; i < P; i += nth) mx = fmax(mx, fabs(g[i]));
+  double mt = 0.0;
   if (d.var)
-    for (int c = tid; c < C; c += nth) mx = fmax(mx, fabs(s_tg[0][c]));  // each frame once (kown)
-  mx = block_max(mx, s_red);
+    for (int c = tid; c < C; c += nth) mt = fmax(mt, fabs(s_tg[0][c]));  // each frame once (kown)
+  mx = block_max(fmax(mx, mt), s_red);
   if (tid == 0) gmaxp[f] = mx;
+  if (gmaxt) {
+    mt = block_max(mt, s_red);
+    if (tid == 0) gmaxt[f] = mt;
+  }
+  if (graw)
+    for (int i = tid; i < P; i += nth) graw[(size_t)f * P + i] = g[i];
   if (!elim) return;
   for (int i = tid; i < P; i += nth) Adiag[(size_t)f * P + i] = A[i * P + i];
   __syncthreads();
@@ -1654,11 +1662,15 @@ __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int 
 // dtau[k, c] = -(g_c + h_c^T dx_k) / T_c over the local unknowns of frame k.
 // Blocks b0 + blockIdx.x. The (replicated) const-mode delays are stepped by the first
 // workgroup; their norm terms count only where tau_norm (once over the ranks).
+// Frame-window ranks (normt != null): only the delays of the owned frames [klo, khi) are
+// stepped (the others are copied: this rank's terms never read them); their norm terms go to
+// normt so that they count over every block of the chain, not only the published rows'.
 __global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __restrict__ st,
                                                   const double* __restrict__ dcv, const double* __restrict__ dtau,
                                                   const double* __restrict__ Hloc, const double* __restrict__ gloc,
                                                   double* __restrict__ Xbuf, double* __restrict__ taubuf,
-                                                  double* __restrict__ normp, int hsel, int b0, int tau_norm) {
+                                                  double* __restrict__ normp, int hsel, int b0, int tau_norm,
+                                                  int klo = 0, int khi = INT_MAX, double* __restrict__ normt = nullptr) {
   if (st->status != 0) return;
   if (hsel) {
     Hloc += (size_t)st->cur * d.N * FTE_NZP * FTE_NZP;
@@ -1692,6 +1704,7 @@ __global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __r
       }
     }
   }
+  double dnt = 0.0, xnt = 0.0;
   if (d.var) {
     const int C = d.C;
     const double* tau = taubuf + (size_t)cur * d.NT;
@@ -1700,6 +1713,10 @@ __global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __r
     for (int e = threadIdx.x; e < 3 * C; e += blockDim.x) {
       const int k = 3 * i - 2 + e / C, c = e % C;
       if (k < 0 || k >= d.N) continue;
+      if (k < klo || k >= khi) {
+        taun[(size_t)k * C + c] = tau[(size_t)k * C + c];
+        continue;
+      }
       const double* H = Hloc + (size_t)k * FTE_NZP * FTE_NZP + (size_t)(P + 6 + c) * FTE_NZP;
       const double t = tau[(size_t)k * C + c], gc = gloc[(size_t)k * FTE_NZP + P + 6 + c];
       double dv = 0.0;
@@ -1715,15 +1732,27 @@ __global__ __launch_bounds__(256) void k_cr_trial(FteDims d, const FteState* __r
         dv = -v / (h + lam * fmax(h, 1e-12));
       }
       taun[(size_t)k * C + c] = (c == 0) ? 0.0 : fmin(fmax(t + dv, -d.Ts), d.Ts);
-      dn += dv * dv;
-      xn += t * t;
+      dnt += dv * dv;
+      xnt += t * t;
     }
+  }
+  if (!normt) {
+    dn += dnt;
+    xn += xnt;
   }
   dn = block_sum(dn, s_red);
   xn = block_sum(xn, s_red);
   if (threadIdx.x == 0 && i < d.nblk) {
     normp[2 * i] = dn;
     normp[2 * i + 1] = xn;
+  }
+  if (normt) {
+    dnt = block_sum(dnt, s_red);
+    xnt = block_sum(xnt, s_red);
+    if (threadIdx.x == 0 && i < d.nblk) {
+      normt[2 * i] = dnt;
+      normt[2 * i + 1] = xnt;
+    }
   }
 }
 
@@ -1886,6 +1915,9 @@ struct FteBuffers {
   double *Hloc, *gloc, *Floc, *Tc, *Ab, *gb, *Bt, *gmaxp, *Dc, *Ec, *GBc, *Wc, *Tau, *dcv, *dtau, *normp, *Fm, *Fq, *part;
   double* Adiag;
   double *Ec2, *dL, *dR;  // second coupling buffer (levels alternate), pending Schur terms
+  // frame-window ranks with per-frame delays: rows' gradients before the delay elimination,
+  // per-row max |delay gradient| of the frame the row starts, per-block delay step / state norms
+  double *graw, *gmaxt, *normt;
   int* bad;
   FteState* st;
 };
@@ -1962,7 +1994,8 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
                oE2 = take((size_t)n * BP * BP), odL = take((size_t)n * BP * (BP + GR)),
                odR = take((size_t)n * BP * (BP + GR)),
                odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)),
-               onp = take(2 * (size_t)n), oTc = take(nlin * N * std::max(tc_stride(d.Cg), 1)), oFm = take(N), oFq = take(N), ost = take(16), oint = take(8);
+               onp = take(2 * (size_t)n), oTc = take(nlin * N * std::max(tc_stride(d.Cg), 1)), oFm = take(N), oFq = take(N), ost = take(16), oint = take(8),
+               ogr = take((size_t)M * P), ogt = take(M), ont = take(2 * (size_t)n);
   // staged inputs (owned mode only)
   const size_t oI = take((n_ints + 1) / 2 + 1), oR = take(n_reals), oC = take((size_t)ACS_CAM_STRIDE * C),
                oMe = take((size_t)N * C * L * 2), oWt = take((size_t)N * C * L), oQ = take(P);
@@ -2028,6 +2061,9 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.part = arena + opart;
   b.dtau = arena + odt;
   b.normp = arena + onp;
+  b.graw = arena + ogr;
+  b.gmaxt = arena + ogt;
+  b.normt = arena + ont;
   b.Fm = arena + oFm;
   b.Fq = arena + oFq;
   b.st = (FteState*)(arena + ost);
@@ -2241,7 +2277,7 @@ static DistLayout dist_layout(const FteDims& d, int R) {
   L.oTau = L.oRdiag + nb * BP;
   L.oGmax = L.oTau + nE;
   L.n1 = L.oGmax + R;
-  L.n2 = (size_t)d.nblk * BP;
+  L.n2 = (size_t)d.nblk * BP + (d.var ? (size_t)d.NT : 0);  // solution rows (+ per-frame delays)
   L.n3 = 4;
   return L;
 }
@@ -2280,7 +2316,8 @@ __global__ __launch_bounds__(256) void k_dist_pack_small(FteDims d, const FteSta
                                                          int rank, int a0, int bend,
                                                          const double* __restrict__ part,
                                                          const double* __restrict__ gmaxp,
-                                                         double* __restrict__ p1) {
+                                                         double* __restrict__ p1,
+                                                         const double* __restrict__ gmaxt = nullptr) {
   if (st->status != 0) return;
   __shared__ double s_red[256];
   const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
@@ -2292,6 +2329,8 @@ __global__ __launch_bounds__(256) void k_dist_pack_small(FteDims d, const FteSta
   const int f0 = 3 * (a0 + 1), f1 = min(3 * min(bend, d.nblk), d.M);
   double mx = 0.0;
   mx = strided_max(gmaxp, f0 + (int)threadIdx.x, f1, blockDim.x, mx);
+  // per-frame delays: every owned frame's (rows of the whole chain; other frames give 0)
+  if (gmaxt) mx = strided_max(gmaxt, 3 * a0 + (int)threadIdx.x, min(3 * min(bend, d.nblk - 1) + 3, d.M), blockDim.x, mx);
   mx = block_max(mx, s_red);
   if (threadIdx.x == 0) p1[Lo.oGmax + rank] = mx;
 }
@@ -2356,7 +2395,9 @@ __global__ void k_dist_scatter(FteDims d, const FteState* __restrict__ st, int r
 __global__ __launch_bounds__(256) void k_dist_cost_pack(FteState* __restrict__ st, int which, int N, int m0,
                                                         int m1, int q0, int q1, const double* __restrict__ Fm,
                                                         const double* __restrict__ Fq, int n0, int n1,
-                                                        const double* __restrict__ normp, double* __restrict__ p3) {
+                                                        const double* __restrict__ normp, double* __restrict__ p3,
+                                                        int t0 = 0, int t1 = 0,
+                                                        const double* __restrict__ normt = nullptr) {
   if (which == 1 && st->status != 0) return;
   if (which == 1) Fm += (size_t)(st->cur ^ 1) * N;
   __shared__ double s_red[256];
@@ -2373,6 +2414,10 @@ __global__ __launch_bounds__(256) void k_dist_cost_pack(FteState* __restrict__ s
     const double* xs[2] = {normp, normp + 1};
     strided_sums<2>(xs, 2, n0 + (int)threadIdx.x, n1, blockDim.x, nrm);
   }
+  if (normt && t1 > t0) {  // per-frame delays of the owned frames, over every block of the chain
+    const double* xs[2] = {normt, normt + 1};
+    strided_sums<2>(xs, 2, t0 + (int)threadIdx.x, t1, blockDim.x, nrm);
+  }
   double dn = nrm[0], xn = nrm[1];
   a = block_sum(a, s_red);
   b = block_sum(b, s_red);
@@ -2387,9 +2432,11 @@ __global__ __launch_bounds__(256) void k_dist_cost_pack(FteState* __restrict__ s
   }
 }
 
-// X[cur] rows of super-blocks [b_lo, b_hi) in the block layout of the step (BP per block)
+// X[cur] rows of super-blocks [b_lo, b_hi) in the block layout of the step (BP per block);
+// per-frame delays: those of the owned frames [k_lo, k_hi) after the rows
 __global__ __launch_bounds__(256) void k_dist_x_out(FteDims d, const FteState* __restrict__ st, int b_lo, int b_hi,
-                                                    const double* __restrict__ Xbuf, double* __restrict__ p2) {
+                                                    const double* __restrict__ Xbuf, double* __restrict__ p2,
+                                                    const double* __restrict__ taubuf, int k_lo, int k_hi) {
   const double* X = Xbuf + (size_t)st->cur * d.M * d.P;
   const int P = d.P, BP = d.BP;
   for (size_t e = (size_t)b_lo * BP + (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)b_hi * BP;
@@ -2397,17 +2444,29 @@ __global__ __launch_bounds__(256) void k_dist_x_out(FteDims d, const FteState* _
     const int i = (int)(e / BP), r = (int)(e % BP), f = 3 * i + r / P;
     if (r < 3 * P && f < d.M) p2[e] = X[(size_t)f * P + r % P];
   }
+  if (d.var) {
+    const double* tau = taubuf + (size_t)st->cur * d.NT;
+    for (size_t e = (size_t)k_lo * d.C + (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)k_hi * d.C;
+         e += (size_t)gridDim.x * blockDim.x)
+      p2[(size_t)d.nblk * BP + e] = tau[e];
+  }
 }
 
-// every row of X[cur] from the gathered block layout
+// every row of X[cur] (and every per-frame delay) from the gathered layout
 __global__ __launch_bounds__(256) void k_dist_x_in(FteDims d, const FteState* __restrict__ st,
-                                                   const double* __restrict__ p2, double* __restrict__ Xbuf) {
+                                                   const double* __restrict__ p2, double* __restrict__ Xbuf,
+                                                   double* __restrict__ taubuf) {
   double* X = Xbuf + (size_t)st->cur * d.M * d.P;
   const int P = d.P, BP = d.BP;
   for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)d.nblk * BP;
        e += (size_t)gridDim.x * blockDim.x) {
     const int i = (int)(e / BP), r = (int)(e % BP), f = 3 * i + r / P;
     if (r < 3 * P && f < d.M) X[(size_t)f * P + r % P] = p2[e];
+  }
+  if (d.var) {
+    double* tau = taubuf + (size_t)st->cur * d.NT;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)d.NT; e += (size_t)gridDim.x * blockDim.x)
+      tau[e] = p2[(size_t)d.nblk * BP + e];
   }
 }
 
@@ -2815,8 +2874,6 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
   acs_fte_opts op;
   acs_fte_default_opts(&op);
   if (opts) op = *opts;
-  ACS_CHECK(ctx, sd_mode == 0 || !shutter_delay,
-            "fte_dist: shutter_delay_mode='variable' runs on one GPU (acs_fte_solve)");
   ACS_CHECK(ctx, op.max_iters >= 0, "fte: max_iters < 0");
   ACS_CHECK(ctx, world >= 1 && world <= 1024 && rank >= 0 && rank < world, "fte_dist: rank %d / world %d", rank,
             world);
@@ -2969,15 +3026,24 @@ static int dist_phase1_body(acs_fte_dist* h, double* p1) {
     // rows never reach HBM), as the single-GPU solve; the ends' raw diagonals / gradients
     // go to Adiag / gb (row layout) for the payload
     const int top = std::min(h->bend, d.nblk - 1);
-    cr_launch_assemble_build(d, s, b, h->a0, top - h->a0 + 1, h->own_lo, h->own_hi, h->a0, h->bend, b.Adiag, b.gb);
+    if (d.var) {
+      // per-frame delays: eliminated per frame in the row assembly (damped with the LM
+      // lambda), the rows' gradients before that kept for the payload, then the build
+      hipLaunchKernelGGL(k_fte_assemble, dim3(h->f_hi - h->f_lo), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, 0,
+                         h->f_lo, h->own_lo, h->own_hi, b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1, b.graw,
+                         b.gmaxt);
+      cr_launch_build(d, s, top - h->a0 + 1, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, h->a0, h->a0, h->bend, b.Adiag);
+    } else {
+      cr_launch_assemble_build(d, s, b, h->a0, top - h->a0 + 1, h->own_lo, h->own_hi, h->a0, h->bend, b.Adiag, b.graw);
+    }
     const double* Efin = dist_local_cr(h);
     hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part,
                        h->k_lo, h->k_hi, h->a0 + 1, std::min(h->bend, d.nblk), 1,
                        (const double*)b.Tc);
     hipLaunchKernelGGL(k_dist_pack, dim3(32, 2), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.Dc, Efin,
-                       b.GBc, b.Adiag, b.gb, p1);
+                       b.GBc, b.Adiag, b.graw, p1);
     hipLaunchKernelGGL(k_dist_pack_small, dim3(1), dim3(256), 0, s, d, b.st, h->Lo, h->rank, h->a0, h->bend, b.part,
-                       b.gmaxp, p1);
+                       b.gmaxp, p1, d.var ? (const double*)b.gmaxt : (const double*)nullptr);
   }
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
@@ -3024,7 +3090,8 @@ static int dist_phase2_body(acs_fte_dist* h, const double* p1) {
     }
     const int top = std::min(h->bend, d.nblk - 1);
     hipLaunchKernelGGL(k_cr_trial, dim3(top - h->a0 + 1), dim3(256), 0, s, d, b.st, (const double*)b.dcv, b.dtau,
-                       b.Hloc, b.gloc, b.X, b.tau, b.normp, 0, h->a0, h->rank == 0 ? 1 : 0);
+                       b.Hloc, b.gloc, b.X, b.tau, b.normp, 1, h->a0, h->rank == 0 ? 1 : 0, h->k_lo, h->k_hi,
+                       b.normt);
   } else {
     // a rank past the last block still steps the replicated delays
     hipLaunchKernelGGL(k_cr_trial, dim3(1), dim3(256), 0, s, d, b.st, (const double*)b.dcv, b.dtau, b.Hloc, b.gloc,
@@ -3049,8 +3116,10 @@ static int dist_phase3_body(acs_fte_dist* h, double* p3) {
     hipLaunchKernelGGL(k_fte_linearize, dim3(l_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
                        b.meas, b.w, b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv, b.Tc);
   const int q0 = std::max(h->k_lo + 1, 1), q1 = l_hi;
+  const int t_hi = std::min(h->bend, d.nblk - 1) + 1;
   hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 1, d.N, h->k_lo, h->k_hi, q0,
-                     std::max(q0, q1), (const double*)b.Floc, (const double*)b.Fq, h->out_lo, h->out_hi, b.normp, p3);
+                     std::max(q0, q1), (const double*)b.Floc, (const double*)b.Fq, h->out_lo, h->out_hi, b.normp, p3,
+                     d.var ? h->a0 : 0, d.var ? t_hi : 0, (const double*)b.normt);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }
@@ -3103,7 +3172,8 @@ int acs_fte_dist_gather(acs_fte_dist* h, double* p2) {
   hipStream_t s = ctx->stream;
   ACS_HIP(ctx, hipMemsetAsync(p2, 0, sizeof(double) * h->Lo.n2, s));
   if (h->out_hi > h->out_lo)
-    hipLaunchKernelGGL(k_dist_x_out, dim3(64), dim3(256), 0, s, d, b.st, h->out_lo, h->out_hi, (const double*)b.X, p2);
+    hipLaunchKernelGGL(k_dist_x_out, dim3(64), dim3(256), 0, s, d, b.st, h->out_lo, h->out_hi, (const double*)b.X, p2,
+                       (const double*)b.tau, h->k_lo, h->k_hi);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }
@@ -3113,7 +3183,7 @@ int acs_fte_dist_scatter(acs_fte_dist* h, const double* p2) {
   acs_ctx* ctx = h->ctx;
   const FteDims& d = h->S.d;
   FteBuffers& b = h->S.b;
-  hipLaunchKernelGGL(k_dist_x_in, dim3(64), dim3(256), 0, ctx->stream, d, b.st, p2, b.X);
+  hipLaunchKernelGGL(k_dist_x_in, dim3(64), dim3(256), 0, ctx->stream, d, b.st, p2, b.X, b.tau);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }

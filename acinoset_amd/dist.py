@@ -74,13 +74,13 @@ def lm_loop2(ranks, allreduce):
             return st[0]
 
 
-def _check_dev(torch, dev, device, table, N, Cn):
+def _check_dev(torch, dev, device, table, N, Cn, var=False):
     """The HBM-resident inputs of a rank go to the C ABI as raw pointers: check what the
     kernels assume (device, dtype, contiguity, element counts) before handing them over."""
     want = {'ints': (torch.int32, len(table.ints)), 'reals': (torch.float64, len(table.reals)),
             'cams': (torch.float64, Cn * _native.ACS_CAM_STRIDE), 'meas': (torch.float64, N * Cn * table.L * 2),
             'w': (torch.float64, N * Cn * table.L), 'qinv': (torch.float64, table.P),
-            'X': (torch.float64, (N + 2) * table.P), 'tau': (torch.float64, Cn)}
+            'X': (torch.float64, (N + 2) * table.P), 'tau': (torch.float64, N * Cn if var else Cn)}
     for k, (dt, n) in want.items():
         t = dev.get(k)
         if t is None:
@@ -99,33 +99,38 @@ class HipFteRank:
     tensors, so torch.distributed can reduce them in place)."""
 
     def __init__(self, ctx, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutter_delay=True, intermode=1,
-                 opts=None, rank=0, world=1, dev=None):
+                 opts=None, rank=0, world=1, dev=None, sd_mode=0):
         """`dev`: the inputs already resident in HBM, as torch device tensors
         {'ints', 'reals', 'cams', 'meas', 'w', 'qinv', 'X', 'tau'} (copied device to device
-        into the handle; the host arrays are then only used for the shapes)."""
+        into the handle; the host arrays are then only used for the shapes). sd_mode 0 =
+        'const' (tau (C,)), 1 = 'variable' (tau (N, C): each frame's delays eliminated and
+        stepped by the rank owning the frame, gathered with the solution rows)."""
         import torch
         self.ctx = ctx
         self.torch = torch
         opts = opts or ctx.fte_default_opts()
+        sd_mode = _native.SD_MODES.get(sd_mode, sd_mode)
         h = C.c_void_p()
         sizes = (C.c_int64 * 3)()
         if dev is None:
             ints, reals, cams, meas, w, qinv, N, Cn = ctx._fte_args(table, cams, meas, w, Ts, qinv, shutter_delay,
                                                                     intermode)
             X = _native._c64(X0).reshape(N + 2, table.P)
-            tau = np.zeros(Cn) if tau0 is None else _native._c64(tau0)
+            tau = ctx._tau_init(tau0, N, Cn, sd_mode if shutter_delay else 0)
             P_ = _native._ptr
             ptrs = [P_(a) for a in (ints, reals, cams, meas, w, qinv, X, tau)]
             n_ints, n_reals, flags = len(ints), len(reals), 0
         else:
             N, Cn = int(np.shape(meas)[0]), int(np.shape(meas)[1])
-            _check_dev(torch, dev, ctx.device, table, N, Cn)
+            _check_dev(torch, dev, ctx.device, table, N, Cn, sd_mode == 1 and shutter_delay)
             ptrs = [C.c_void_p(dev[k].data_ptr()) for k in ('ints', 'reals', 'cams', 'meas', 'w', 'qinv', 'X', 'tau')]
             n_ints, n_reals, flags = dev['ints'].numel(), dev['reals'].numel(), _native.ACS_DEVICE_PTRS
         self.N, self.P, self.C = N, table.P, Cn
+        self.tau_shape = (N, Cn) if (sd_mode == 1 and shutter_delay) else (Cn,)
         ctx.check(ctx.lib.acs_fte_dist_create(ctx.h, ptrs[0], n_ints, ptrs[1], n_reals, ptrs[2], Cn, ptrs[3], ptrs[4], N,
-                                              int(bool(shutter_delay)), float(Ts), ptrs[5], 0, int(intermode), ptrs[6],
-                                              ptrs[7], C.byref(opts), int(rank), int(world), C.byref(h), sizes, flags),
+                                              int(bool(shutter_delay)), float(Ts), ptrs[5], int(sd_mode),
+                                              int(intermode), ptrs[6], ptrs[7], C.byref(opts), int(rank), int(world),
+                                              C.byref(h), sizes, flags),
                   'acs_fte_dist_create')
         self.h = h
         dev = torch.device('cuda', ctx.device)
@@ -162,7 +167,7 @@ class HipFteRank:
 
     def result(self):
         X = np.empty((self.N + 2, self.P))
-        tau = np.empty(self.C)
+        tau = np.empty(self.tau_shape)
         rep = _native.FteReport()
         self.ctx.check(self.ctx.lib.acs_fte_dist_result(self.h, _native._ptr(X), _native._ptr(tau), C.byref(rep), 0),
                        'acs_fte_dist_result')
@@ -221,13 +226,14 @@ class _on_torch_stream:
 
 
 def fte_solve_dist(ctx, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutter_delay=True, intermode=1, opts=None,
-                   group=None):
+                   group=None, sd_mode=0):
     """Drop-in for Context.fte_solve under torch.distributed (one rank per GPU): returns
     (X, tau, report), identical on every rank."""
     import torch.distributed as tdist
     rank, world = tdist.get_rank(group), tdist.get_world_size(group)
     with _on_torch_stream(ctx):
-        r = HipFteRank(ctx, table, cams, meas, w, Ts, qinv, X0, tau0, shutter_delay, intermode, opts, rank, world)
+        r = HipFteRank(ctx, table, cams, meas, w, Ts, qinv, X0, tau0, shutter_delay, intermode, opts, rank, world,
+                       sd_mode=sd_mode)
         try:
             lm_loop([r], torch_allreduce(group))
             return r.result()
@@ -236,12 +242,12 @@ def fte_solve_dist(ctx, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutter_d
 
 
 def fte_solve_virtual(ctx, table, cams, meas, w, Ts, qinv, X0, tau0=None, shutter_delay=True, intermode=1,
-                      opts=None, world=2):
+                      opts=None, world=2, sd_mode=0):
     """The distributed algorithm with `world` ranks emulated in one process on one device
     (parity tests of the decomposition without a multi-GPU node)."""
     with _on_torch_stream(ctx):
-        ranks = [HipFteRank(ctx, table, cams, meas, w, Ts, qinv, X0, tau0, shutter_delay, intermode, opts, r, world)
-                 for r in range(world)]
+        ranks = [HipFteRank(ctx, table, cams, meas, w, Ts, qinv, X0, tau0, shutter_delay, intermode, opts, r, world,
+                            sd_mode=sd_mode) for r in range(world)]
         try:
             lm_loop(ranks, local_allreduce)
             outs = [r.result() for r in ranks]

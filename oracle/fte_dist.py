@@ -52,8 +52,9 @@ class OracleFteRank:
         self.rank, self.world = rank, world
         self.opts = dict(max_iters=max_iters, ftol=ftol, xtol=xtol, gtol=gtol)
         self.X = np.array(X0, np.float64).reshape(p.M, p.P)
-        self.tau = np.zeros(p.C) if tau0 is None else np.array(tau0, np.float64)
-        self.tau[0] = 0.0
+        self.var = bool(p.var)
+        self.tau = np.zeros(p.tau_shape) if tau0 is None else np.array(tau0, np.float64).reshape(p.tau_shape)
+        self.tau[..., 0] = 0.0
         self.lam, self.status, self.iters, self.nacc, self.relin = lam0, 0, 0, 0, True
         M, P = p.M, p.P
         nblk = (M + 2) // 3
@@ -63,10 +64,17 @@ class OracleFteRank:
         self.hi = 3 * bend if rank < world - 1 else 1 << 40  # the last rank owns the tail
         rows = lambda b0, b1: [f for f in range(3 * b0, 3 * b1) if f < M]  # noqa: E731
         var = lambda fs: np.array([f * P + q for f in fs for q in range(P)], np.int64)  # noqa: E731
+        self.frames = (np.arange(p.N) >= self.lo) & (np.arange(p.N) < self.hi)
+        self.stencils = (np.arange(p.N - 1) >= self.lo) & (np.arange(p.N - 1) < self.hi)
         self.I = var(rows(a0 + 1, min(bend, nblk)))                      # interior unknowns
         ends = sorted(set(rows(a0, a0 + 1)) | set(rows(bend, bend + 1)))
         self.chain = np.concatenate([var(ends), self.I]).astype(np.int64)  # rows this rank steps
-        self.ntau = p.C if p.sd else 0
+        # variable delays: those of the owned frames touch only this rank's terms, so they are
+        # interior unknowns eliminated with the chain (no border); const: C border delays
+        owned_k = np.flatnonzero(self.frames)
+        self.Itau = (M * P + owned_k[:, None] * p.C + np.arange(p.C)).ravel() if self.var else np.zeros(0, np.int64)
+        self.I = np.concatenate([self.I, self.Itau]).astype(np.int64)
+        self.ntau = p.C if (p.sd and not self.var) else 0
         tau_idx = np.arange(self.ntau) + M * P
         self.B = np.concatenate([var(ends), tau_idx]).astype(np.int64)  # border unknowns
         # global reduced index space: rows of every chain end e_q = q span (q = 0..R) + tau
@@ -74,13 +82,11 @@ class OracleFteRank:
         self.S = np.concatenate([var(all_ends), tau_idx]).astype(np.int64)
         self.pos = {v: i for i, v in enumerate(self.S)}
         self.Bpos = np.array([self.pos[v] for v in self.B], np.int64)
-        self.frames = (np.arange(p.N) >= self.lo) & (np.arange(p.N) < self.hi)
-        self.stencils = (np.arange(p.N - 1) >= self.lo) & (np.arange(p.N - 1) < self.hi)
         out_hi = bend + 1 if rank == world - 1 else bend
         self.out = var(rows(a0, min(out_hi, nblk)))
         nS = len(self.S)
         self.n1 = nS * nS + 3 * nS + world
-        self.n2 = M * P
+        self.n2 = M * P + (p.N * p.C if self.var else 0)
         self.n3 = 4
 
     # ---- protocol (one payload per round: [p1 | p3]) --------------------------------------
@@ -89,7 +95,7 @@ class OracleFteRank:
         _, H, g = self.prob.linearize(self.X, self.tau, self.frames, self.stencils)
         self.H, self.g = H.toarray(), g
         self.first, self.pending, self.statuses = True, False, []
-        return np.concatenate([self.phase1(self.H, self.g, self.lam), [fm, fq, 0.0, 0.0]])
+        return np.concatenate([self.phase1(self.H, self.g, self.lam, self.tau), [fm, fq, 0.0, 0.0]])
 
     def round(self, P):
         p1, p3 = P[:self.n1], P[self.n1:]
@@ -113,24 +119,37 @@ class OracleFteRank:
                 # acceptance (linearised there for the trial cost)
                 _, Hn, gn = self.prob.linearize(self.Xn, self.taun, self.frames, self.stencils)
                 self.Hn, self.gn = Hn.toarray(), gn
-                out[:self.n1] = self.phase1(self.Hn, self.gn, max(self.lam * 0.1, 1e-15))
+                out[:self.n1] = self.phase1(self.Hn, self.gn, max(self.lam * 0.1, 1e-15), self.taun)
             else:
-                out[:self.n1] = self.phase1(self.H, self.g, self.lam)
+                out[:self.n1] = self.phase1(self.H, self.g, self.lam, self.tau)
         self.statuses.append(self.status)
         return out
 
     def poll(self, k):
         return self.statuses[k]
 
-    def phase1(self, H, g, lam):
+    def phase1(self, H, g, lam, tau):
+        """The chain interior eliminated onto the border (ends + const delays); `tau` is the
+        state the linearisation (H, g) belongs to (variable delays: tau_0 and the delays held
+        at a bound are pinned, as oracle/fte.py solve does)."""
         p = self.prob
         I, B = self.I, self.B
         HII = H[np.ix_(I, I)].copy()
         HII[np.diag_indices_from(HII)] += lam * np.maximum(np.diag(HII), 1e-12)
-        HIB, HBB = H[np.ix_(I, B)], H[np.ix_(B, B)]
-        self.HII, self.HIB = HII, HIB
+        HIB, HBB = H[np.ix_(I, B)].copy(), H[np.ix_(B, B)]
+        gI = g[I].copy()
+        if self.var and len(self.Itau):
+            from .fte import active_bounds
+            pinned = set(p.pinned().tolist()) | set(active_bounds(p, tau, g).tolist())
+            held = np.array([v in pinned for v in I], bool)
+            HII[held, :] = 0.0
+            HII[:, held] = 0.0
+            HII[held, held] = 1.0
+            HIB[held, :] = 0.0
+            gI[held] = 0.0
+        self.HII, self.HIB, self.gI = HII, HIB, gI
         if len(I):
-            Z = np.linalg.solve(HII, np.concatenate([HIB, -g[I][:, None]], 1))
+            Z = np.linalg.solve(HII, np.concatenate([HIB, -gI[:, None]], 1))
             Sb = HBB - HIB.T @ Z[:, :-1]
             rb = -g[B] - HIB.T @ Z[:, -1]
         else:
@@ -143,7 +162,7 @@ class OracleFteRank:
         out[nS * nS + self.Bpos] = rb
         out[nS * nS + nS + self.Bpos] = np.diag(HBB)
         out[nS * nS + 2 * nS + self.Bpos] = g[B]
-        out[nS * nS + 3 * nS + self.rank] = np.abs(g[I]).max() if len(I) else 0.0
+        out[nS * nS + 3 * nS + self.rank] = np.abs(gI).max() if len(I) else 0.0
         return out
 
     def phase2(self, p1):
@@ -173,11 +192,21 @@ class OracleFteRank:
         d = np.zeros(p.nv)
         d[self.S] = dS
         if len(self.I):
-            d[self.I] = np.linalg.solve(self.HII, -self.g[self.I] - self.HIB @ dS[self.Bpos])
+            d[self.I] = np.linalg.solve(self.HII, -self.gI - self.HIB @ dS[self.Bpos])
         self.dtau = dS[nS - self.ntau:] if self.ntau else np.zeros(0)
         # the trial state on this chain (other rows are never read by the owned terms)
         self.Xn = self.X.copy()
         self.Xn.flat[self.chain] += d[self.chain]
+        if self.var:
+            # the owned frames' delays (the others are never read by this rank's terms)
+            self.taun = self.tau.copy()
+            dtv = d[p.M * p.P:].reshape(p.N, p.C)
+            fr = self.frames
+            self.taun[fr] = np.clip(self.tau[fr] + dtv[fr], -p.Ts, p.Ts)
+            self.taun[:, 0] = 0.0
+            self.dn2 = float(np.sum(d[self.out] ** 2) + np.sum(dtv[fr] ** 2))
+            self.xn2 = float(np.sum(self.X.flat[self.out] ** 2) + np.sum(self.tau[fr] ** 2))
+            return
         if p.sd:
             self.taun = np.clip(self.tau + self.dtau, -p.Ts, p.Ts)
             self.taun[0] = 0.0
@@ -220,12 +249,18 @@ class OracleFteRank:
         return self.status
 
     def gather(self):
+        p = self.prob
         out = np.zeros(self.n2)
         out[self.out] = self.X.flat[self.out]
+        if self.var:
+            out[p.M * p.P:] = (self.tau * self.frames[:, None]).ravel()
         return out
 
     def scatter(self, p2):
-        self.X = np.array(p2, np.float64).reshape(self.prob.M, self.prob.P)
+        p = self.prob
+        self.X = np.array(p2[:p.M * p.P], np.float64).reshape(p.M, p.P)
+        if self.var:
+            self.tau = np.array(p2[p.M * p.P:], np.float64).reshape(p.N, p.C)
 
     def result(self):
         return self.X, self.tau, dict(status=self.status, iters=self.iters, n_accepted=self.nacc, cost_before=self.F0,

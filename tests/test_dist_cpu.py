@@ -20,11 +20,12 @@ from acinoset_amd import dist, synth
 from oracle import fte as ofte, fte_dist as odist, sba_ext_dist as osed
 
 
-def _problem(mode='head', N=40, sd=True, inter='vel', seed=2):
+def _problem(mode='head', N=40, sd=True, inter='vel', seed=2, sd_mode='const'):
     scene = synth.load_scene_file()
     seq = synth.make_sequence(N, scene, mode=mode, seed=seed, tau_max=0.004 if sd else 0.0)
     w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
-    prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter)
+    prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter,
+                        sd_mode=sd_mode)
     X0 = ofte.initial_state(prob, np.arange(N), seq.pos3d[:, 0, 0])
     return prob, X0
 
@@ -92,6 +93,22 @@ def test_dist_one_allreduce_per_lm_step(reject_at):
         assert n_rej == 1 and info['status'] in (2, 3)
         np.testing.assert_allclose(X, ref[0], rtol=0, atol=1e-8)
         assert abs(info['cost_after'] - ref[2]['cost_after']) <= 1e-10 * ref[2]['cost_after']
+
+
+@pytest.mark.parametrize('inter,N', [('vel', 24), ('acc', 17)])
+@pytest.mark.parametrize('world', [2, 3, 8])
+def test_dist_protocol_variable_delays_matches_monolithic(inter, N, world):
+    """shutter_delay_mode='variable' (src/core/fte.py:238): every frame's delays are
+    eliminated by the rank owning the frame; the solution rows and delays are gathered once."""
+    prob, X0 = _problem('head', N, True, inter, sd_mode='variable')
+    ref = ofte.solve(prob, X0, max_iters=30)
+    ranks = [odist.OracleFteRank(prob, X0, None, r, world, max_iters=30) for r in range(world)]
+    dist.lm_loop(ranks, dist.local_allreduce)
+    outs = [r.result() for r in ranks]
+    for o in outs[1:]:
+        assert np.array_equal(o[0], outs[0][0]) and np.array_equal(o[1], outs[0][1])
+    assert outs[0][1].shape == (N, 6)
+    _check(outs[0], ref)
 
 
 def test_dist_chain_partition_covers_every_term():

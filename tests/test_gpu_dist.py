@@ -23,11 +23,12 @@ from acinoset_amd import _native, dist, kinematics as pkin, synth
 pytestmark = pytest.mark.gpu
 
 
-def _problem(N, mode='default_nolure', sd=True, inter='vel', seed=2):
+def _problem(N, mode='default_nolure', sd=True, inter='vel', seed=2, sd_mode='const'):
     scene = synth.load_scene_file()
     seq = synth.make_sequence(N, scene, mode=mode, seed=seed, tau_max=0.004 if sd else 0.0)
     w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
-    prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter)
+    prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter,
+                        sd_mode=sd_mode)
     cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
     X0 = ofte.initial_state(prob, np.arange(N), seq.pos3d[:, 0, 0])
     return prob, cams, X0
@@ -48,6 +49,41 @@ def test_fte_dist_virtual_matches_single(ctx, mode, N, sd, inter, world):
     assert abs(rd['cost_after'] - r1['cost_after']) <= 1e-11 * r1['cost_after']
     np.testing.assert_allclose(Xd, X1, rtol=0, atol=1e-9)
     np.testing.assert_allclose(td, t1, rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize('mode,N,inter', [('default_nolure', 40, 'vel'), ('head', 47, 'acc')])
+@pytest.mark.parametrize('world', [2, 3, 8])
+def test_fte_dist_virtual_variable_delays_matches_single(ctx, mode, N, inter, world):
+    """shutter_delay_mode='variable' over frame windows: each frame's delays eliminated and
+    stepped by the rank owning the frame, gathered once with the rows. Same iterates as the
+    single-GPU solve (which eliminates them in one pass)."""
+    prob, cams, X0 = _problem(N, mode, True, inter, sd_mode='variable')
+    table = pkin.build_table(mode)
+    X1, t1, r1 = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, intermode=prob.im,
+                               sd_mode='variable')
+    Xd, td, rd = dist.fte_solve_virtual(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
+                                        intermode=prob.im, world=world, sd_mode='variable')
+    assert td.shape == (N, 6)
+    assert rd['iters'] == r1['iters'] and rd['n_accepted'] == r1['n_accepted'], (rd, r1)
+    assert rd['status'] == r1['status'] and rd['n_bad_pivots'] == 0
+    assert abs(rd['cost_after'] - r1['cost_after']) <= 1e-11 * r1['cost_after']
+    np.testing.assert_allclose(Xd, X1, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(td, t1, rtol=0, atol=1e-12)
+
+
+def test_fte_dist_variable_delays_matches_oracle_decomposition(ctx):
+    """The variable-delay rank protocol on the GPU against its numpy restatement
+    (oracle/fte_dist.py), 3 ranks, full solve: 1e-9."""
+    prob, cams, X0 = _problem(30, 'head', True, 'vel', sd_mode='variable')
+    table = pkin.build_table('head')
+    Xd, td, rd = dist.fte_solve_virtual(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, world=3,
+                                        sd_mode='variable')
+    ranks = [odist.OracleFteRank(prob, X0, None, r, 3) for r in range(3)]
+    dist.lm_loop(ranks, dist.local_allreduce)
+    Xo, to, io = ranks[0].result()
+    assert rd['iters'] == io['iters']
+    np.testing.assert_allclose(Xd, Xo, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(td, to, rtol=0, atol=1e-11)
 
 
 @pytest.mark.parametrize('world', [2, 5])
