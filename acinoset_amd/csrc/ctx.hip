@@ -53,7 +53,8 @@ void* acs_pinned(acs_ctx* ctx, size_t bytes) {
     ctx->pinned_bytes = 0;
   }
   const size_t n = (bytes + 255) & ~size_t(255);
-  if (hipHostMalloc(&ctx->pinned, n, hipHostMallocDefault) != hipSuccess) {
+  // coherent (fine-grained): kernels write their state snapshots straight into it
+  if (hipHostMalloc(&ctx->pinned, n, hipHostMallocCoherent) != hipSuccess) {
     ctx->pinned = nullptr;
     acs_fail(ctx, ACS_E_NOMEM, "hipHostMalloc(%zu) failed", n);
     return nullptr;

@@ -60,6 +60,7 @@ struct FteState {
   // first round (initial cost), and the state swapped for the speculative reduced system
   int pending, first, spec_on, save_cur;
   double save_lam;
+  int launch, pad2;  // iterations run by the solve loop (its host snapshot slot is launch & 1)
 };
 // transient status of a round whose step was rejected: its solve / step / trial kernels
 // (which all stop on status != 0) are skipped, then the status returns to 0
@@ -1523,10 +1524,19 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
   }
 }
 
+__device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, int bend, const double* __restrict__ Wc,
+                                              const double* __restrict__ dtau, double* __restrict__ dcv, double* sl,
+                                              double* sr_, double* st_);
+
+// fold_hi > fold_lo: the back substitution of levels s = 2^(fold_hi - 1) .. 2^fold_lo (few
+// blocks each) runs here too, block after block in this one workgroup, instead of one
+// latency-bound launch per level (blocks [0, bend])
 __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ W0,
                                                 const double* __restrict__ part, const double* __restrict__ gmaxp,
                                                 const double* __restrict__ taubuf, double* __restrict__ dcv,
-                                                double* __restrict__ dtau, int* __restrict__ bad) {
+                                                double* __restrict__ dtau, int* __restrict__ bad, int fold_hi = 0,
+                                                int fold_lo = 0, const double* __restrict__ Wc = nullptr,
+                                                int bend = 0) {
   // block 0 has been eliminated by k_cr_level (top_mode): W0 = its W (BP x WL), its tau Schur
   // term is in the Tau sums like every other block's
   if (st->status != 0) return;
@@ -1604,18 +1614,25 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
     for (int c = 0; c < Cg; ++c) v -= w[c] * dtau[c];
     dcv[r] = v;
   }
+  if (fold_hi > fold_lo) {
+    __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32];
+    for (int lv = fold_hi - 1; lv >= fold_lo; --lv) {
+      const int s = 1 << lv;
+      for (int i = s; i < d.nblk; i += 2 * s) {
+        __syncthreads();  // dcv / dtau of the blocks above are written
+        cr_back_block(d, i, s, bend, Wc, dtau, dcv, sl, sr_, st_);
+      }
+    }
+  }
 }
 
-__global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int bend,
-                                                  const FteState* __restrict__ st,
-                                                  const double* __restrict__ Wc, const double* __restrict__ dtau,
-                                                  double* __restrict__ dcv) {
-  if (st->status != 0) return;
-  const int i = a0 + s * (2 * blockIdx.x + 1);
+// back substitution of eliminated block i at level s (blockDim 1024; every thread calls it)
+__device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, int bend, const double* __restrict__ Wc,
+                                              const double* __restrict__ dtau, double* __restrict__ dcv, double* sl,
+                                              double* sr_, double* st_) {
   const int l = i - s, r = (i + s <= bend && i + s < d.nblk) ? i + s : -1;
   const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
   const double* W = Wc + (size_t)i * BP * WL;
-  __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32];
   const int tid = threadIdx.x;
   if (tid < BP) {
     sl[tid] = dcv[(size_t)l * BP + tid];
@@ -1655,6 +1672,15 @@ __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int 
   }
   v = group_sum<8>(v);
   if (live && j == 0) dcv[(size_t)i * BP + row] = rhs - v;
+}
+
+__global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int bend,
+                                                  const FteState* __restrict__ st,
+                                                  const double* __restrict__ Wc, const double* __restrict__ dtau,
+                                                  double* __restrict__ dcv) {
+  if (st->status != 0) return;
+  __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32];
+  cr_back_block(d, a0 + s * (2 * blockIdx.x + 1), s, bend, Wc, dtau, dcv, sl, sr_, st_);
 }
 
 // trial state X + delta, tau + dtau (clipped), norm partials per super-block. Variable
@@ -1825,9 +1851,20 @@ __global__ __launch_bounds__(64) void k_fte_cost(FteDims d, const int* __restric
 // ---------------------------------------------------------------------------------------
 // 7. LM control
 // ---------------------------------------------------------------------------------------
+// Every non-init launch ends by writing the LM state into host snapshot slot (launch & 1)
+// (`snap`: pinned host memory; the host waits on an event recorded after the iteration and
+// reads it there, with no copy node in the iteration).
+__device__ __forceinline__ void fte_snapshot(FteState* st, FteState* snap) {
+  if (!snap) return;
+  const int slot = st->launch & 1;
+  st->launch += 1;
+  snap[slot] = *st;  // coherent host memory (acs_pinned): visible once the iteration's event completes
+}
+
 __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict__ st, FteOptsDev o, int init,
                                                 const double* __restrict__ Fm, const double* __restrict__ Fq,
-                                                const double* __restrict__ normp, int spec) {
+                                                const double* __restrict__ normp, int spec,
+                                                FteState* __restrict__ snap = nullptr) {
   __shared__ double s_red[256];
   const int tid = threadIdx.x;
   // every load is issued before the LM state is read: both copies of the measurement terms
@@ -1852,12 +1889,16 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
     }
     return;
   }
-  if (st->status != 0) return;
+  if (st->status != 0) {
+    if (tid == 0) fte_snapshot(st, snap);
+    return;
+  }
   dn = block_sum(dn, s_red);
   xn = block_sum(xn, s_red);
   if (tid != 0) return;
   if (st->gmax <= o.gtol) {
     st->status = ACS_STATUS_GTOL;
+    fte_snapshot(st, snap);
     return;
   }
   const double Fn = fm + fq;
@@ -1884,6 +1925,7 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
     if (st->lam > 1e16) st->status = ACS_STATUS_STALLED;
   }
   if (st->status == 0 && st->iters >= o.max_iters) st->status = ACS_STATUS_MAXITER;
+  fte_snapshot(st, snap);
 }
 
 // =======================================================================================
@@ -1923,6 +1965,7 @@ struct FteBuffers {
 };
 
 struct FteSetup {
+  FteState* snap = nullptr;  // pinned host slots the LM kernel writes its state into
   FteDims d;
   FteBuffers b;
 };
@@ -2227,9 +2270,13 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, sym);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
                      d.N, 0, d.nblk, 1, (const double*)b.Tc);
+  // the top back-substitution levels (<= 5 blocks each) run inside k_cr_top's workgroup
+  int fold_lo = d.nlev;
+  while (fold_lo > 0 && (d.nblk - (1 << (fold_lo - 1)) + (2 << (fold_lo - 1)) - 1) / (2 << (fold_lo - 1)) <= 5)
+    --fold_lo;
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, d, b.st, (const double*)b.Wc, b.part, b.gmaxp, b.tau, b.dcv,
-                     b.dtau, b.bad);
-  for (int lv = d.nlev - 1; lv >= 0; --lv) {
+                     b.dtau, b.bad, d.nlev, fold_lo, (const double*)b.Wc, bend);
+  for (int lv = fold_lo - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
     hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, d, st, 0, bend, b.st, b.Wc, b.dtau, b.dcv);
@@ -2240,7 +2287,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   // are the trial cost (no separate cost pass)
   hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
                      b.X, b.tau, b.st, 0, 0, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv, b.Tc);
-  hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 0, b.Floc, b.Fq, b.normp, 1);
+  hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 0, b.Floc, b.Fq, b.normp, 1, S.snap);
 }
 
 // =======================================================================================
@@ -2664,7 +2711,15 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   // early-exiting iteration (was: chunks of 4 behind a full synchronisation, up to 3). The
   // instantiated graph stays in the context for the next solve with the same key.
   const int chunk = 1;
+  FteState* snap = nullptr;
+  if (op.max_iters > 0) {
+    snap = (FteState*)acs_pinned(ctx, 2 * sizeof(FteState));
+    if (!snap) return ACS_E_NOMEM;
+    std::memset(snap, 0, 2 * sizeof(FteState));
+  }
+  S.snap = snap;
   std::string key;
+  key_put(key, snap);
   key_put(key, d);
   key_put(key, b);
   key_put(key, o.max_iters);
@@ -2702,8 +2757,6 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   FteState hs;
   std::memset(&hs, 0, sizeof(hs));
   if (op.max_iters > 0) {
-    FteState* snap = (FteState*)acs_pinned(ctx, 2 * sizeof(FteState));
-    if (!snap) return ACS_E_NOMEM;
     // max_iters + 1 launches at most: the kernel sets MAXITER in iteration max_iters
     const int nmax = op.max_iters + 1;
     int last = 0;
@@ -2714,7 +2767,7 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
         else
           fte_enqueue_iteration(S, s, o);
         ACS_HIP(ctx, hipGetLastError());
-        ACS_HIP(ctx, hipMemcpyAsync(&snap[n & 1], b.st, sizeof(FteState), hipMemcpyDeviceToHost, s));
+        // k_fte_lm of iteration n wrote its state into snap[n & 1]
         ACS_HIP(ctx, hipEventRecord(ctx->snap_ev[n & 1], s));
         last = n;
       }

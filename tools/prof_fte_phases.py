@@ -2,7 +2,7 @@
 with -DFTE_PROFILE:
   B=acinoset_amd/csrc/build; hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -DFTE_PROFILE \
      -c acinoset_amd/csrc/fte.hip -o $B/fte_prof.o && hipcc --offload-arch=gfx950 -shared -fPIC \
-     $B/{ctx,ekf,fk,sba,sba_ext,tri}.o $B/fte_prof.o -o $B/libprof.so
+     $B/{ctx,ekf,fk,sba,sba_ext,tri,pipeline}.o $B/fte_prof.o -o $B/libprof.so
 then python tools/prof_fte_phases.py [frames]."""
 import ctypes as C
 import os
