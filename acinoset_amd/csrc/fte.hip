@@ -1524,19 +1524,10 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
   }
 }
 
-__device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, int bend, const double* __restrict__ Wc,
-                                              const double* __restrict__ dtau, double* __restrict__ dcv, double* sl,
-                                              double* sr_, double* st_);
-
-// fold_hi > fold_lo: the back substitution of levels s = 2^(fold_hi - 1) .. 2^fold_lo (few
-// blocks each) runs here too, block after block in this one workgroup, instead of one
-// latency-bound launch per level (blocks [0, bend])
 __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ W0,
                                                 const double* __restrict__ part, const double* __restrict__ gmaxp,
                                                 const double* __restrict__ taubuf, double* __restrict__ dcv,
-                                                double* __restrict__ dtau, int* __restrict__ bad, int fold_hi = 0,
-                                                int fold_lo = 0, const double* __restrict__ Wc = nullptr,
-                                                int bend = 0) {
+                                                double* __restrict__ dtau, int* __restrict__ bad) {
   // block 0 has been eliminated by k_cr_level (top_mode): W0 = its W (BP x WL), its tau Schur
   // term is in the Tau sums like every other block's
   if (st->status != 0) return;
@@ -1613,16 +1604,6 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
     double v = w[Cg];
     for (int c = 0; c < Cg; ++c) v -= w[c] * dtau[c];
     dcv[r] = v;
-  }
-  if (fold_hi > fold_lo) {
-    __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32];
-    for (int lv = fold_hi - 1; lv >= fold_lo; --lv) {
-      const int s = 1 << lv;
-      for (int i = s; i < d.nblk; i += 2 * s) {
-        __syncthreads();  // dcv / dtau of the blocks above are written
-        cr_back_block(d, i, s, bend, Wc, dtau, dcv, sl, sr_, st_);
-      }
-    }
   }
 }
 
@@ -2270,13 +2251,12 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, sym);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
                      d.N, 0, d.nblk, 1, (const double*)b.Tc);
-  // the top back-substitution levels (<= 5 blocks each) run inside k_cr_top's workgroup
-  int fold_lo = d.nlev;
-  while (fold_lo > 0 && (d.nblk - (1 << (fold_lo - 1)) + (2 << (fold_lo - 1)) - 1) / (2 << (fold_lo - 1)) <= 5)
-    --fold_lo;
+  // (one launch per back-substitution level: running the top levels' few blocks one after
+  // the other inside k_cr_top's workgroup was tried in r03 and took 30 us instead of the 18 us
+  // of four launches - one workgroup streams a block's W at ~2 us)
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, d, b.st, (const double*)b.Wc, b.part, b.gmaxp, b.tau, b.dcv,
-                     b.dtau, b.bad, d.nlev, fold_lo, (const double*)b.Wc, bend);
-  for (int lv = fold_lo - 1; lv >= 0; --lv) {
+                     b.dtau, b.bad);
+  for (int lv = d.nlev - 1; lv >= 0; --lv) {
     const int st = 1 << lv;
     const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
     hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, d, st, 0, bend, b.st, b.Wc, b.dtau, b.dcv);
