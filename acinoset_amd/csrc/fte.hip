@@ -1524,10 +1524,49 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
   }
 }
 
+// Trial state of super-block i (frames 3i..3i+2: X[cur ^ 1] = X[cur] + dv) and the
+// constant-mode delays when `taus` (block 0), with the block's step / state norm partials.
+// Thread e < 3P holds row e of the step (`dv`); thread c < C steps delay c. The sums are
+// k_cr_trial's bit for bit: the same per-thread terms in the same order, and block_sum's
+// tree over 1024 threads first folds threads >= 256 (zeros) exactly.
+__device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* st, int i, double dv,
+                                              const double* __restrict__ dtau, double* __restrict__ Xbuf,
+                                              double* __restrict__ taubuf, double* __restrict__ normp, bool taus,
+                                              double* s_red) {
+  const int P = d.P, e = threadIdx.x, cur = st->cur;
+  double dn = 0.0, xn = 0.0;
+  if (e < 3 * P) {
+    const int f = 3 * i + e / P, p = e % P;
+    if (f < d.M) {
+      const size_t o = (size_t)f * P + p;
+      const double x = Xbuf[(size_t)cur * d.M * P + o];
+      Xbuf[(size_t)(cur ^ 1) * d.M * P + o] = x + dv;
+      dn += dv * dv;
+      xn += x * x;
+    }
+  }
+  if (taus && e < d.C) {
+    const double* tau = taubuf + cur * d.NT;
+    double* taun = taubuf + (cur ^ 1) * d.NT;
+    const double t = (e == 0) ? 0.0 : dtau[e];
+    taun[e] = (e == 0) ? 0.0 : fmin(fmax(tau[e] + t, -d.Ts), d.Ts);
+    dn += t * t;
+    xn += tau[e] * tau[e];
+  }
+  dn = block_sum(dn, s_red);
+  xn = block_sum(xn, s_red);
+  if (threadIdx.x == 0) {
+    normp[2 * i] = dn;
+    normp[2 * i + 1] = xn;
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ W0,
                                                 const double* __restrict__ part, const double* __restrict__ gmaxp,
-                                                const double* __restrict__ taubuf, double* __restrict__ dcv,
-                                                double* __restrict__ dtau, int* __restrict__ bad) {
+                                                double* __restrict__ taubuf, double* __restrict__ dcv,
+                                                double* __restrict__ dtau, int* __restrict__ bad,
+                                                double* __restrict__ Xbuf = nullptr,
+                                                double* __restrict__ normp = nullptr) {
   // block 0 has been eliminated by k_cr_level (top_mode): W0 = its W (BP x WL), its tau Schur
   // term is in the Tau sums like every other block's
   if (st->status != 0) return;
@@ -1599,27 +1638,43 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
     }
     __syncthreads();
   }
-  for (int r = tid; r < BP; r += nth) {
-    const double* w = W0 + (size_t)r * WL + 2 * BP;
+  double v0 = 0.0;  // row tid of block 0's step (nth = 1024 > BP)
+  if (tid < BP) {
+    const double* w = W0 + (size_t)tid * WL + 2 * BP;
     double v = w[Cg];
     for (int c = 0; c < Cg; ++c) v -= w[c] * dtau[c];
-    dcv[r] = v;
+    dcv[tid] = v;
+    v0 = v;
   }
+  // the single-GPU solve steps block 0 (and the constant delays) here: no k_cr_trial launch
+  if (Xbuf) cr_trial_rows(d, st, 0, v0, dtau, Xbuf, taubuf, normp, d.Cg != 0, s_red);
 }
 
-// back substitution of eliminated block i at level s (blockDim 1024; every thread calls it)
+// back substitution of eliminated block i at level s (blockDim 1024; every thread calls it).
+// `ready(l, r)` runs after the W loads are issued and before the survivors' rows are read
+// (k_cr_back_all waits there for the blocks of coarser levels). HANDOFF: the rows of dcv are
+// read and written as agent-scope relaxed 8-byte accesses (global sc1: L2-served, written
+// through), the form k_cr_back_all's in-launch hand-off needs.
+struct CrNoWait {
+  __device__ void operator()(int, int) const {}
+};
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool HANDOFF = false, typename Ready = CrNoWait>
 __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, int bend, const double* __restrict__ Wc,
                                               const double* __restrict__ dtau, double* __restrict__ dcv, double* sl,
-                                              double* sr_, double* st_) {
+                                              double* sr_, double* st_, Ready ready = Ready{},
+                                              double* sout = nullptr) {
   const int l = i - s, r = (i + s <= bend && i + s < d.nblk) ? i + s : -1;
   const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
   const double* W = Wc + (size_t)i * BP * WL;
   const int tid = threadIdx.x;
-  if (tid < BP) {
-    sl[tid] = dcv[(size_t)l * BP + tid];
-    sr_[tid] = r >= 0 ? dcv[(size_t)r * BP + tid] : 0.0;
-  }
-  if (tid < 32) st_[tid] = tid < Cg ? dtau[tid] : 0.0;
   // one row per aligned group of 8 lanes (BP <= 96 < 128 groups): the W loads of every
   // row are issued together, then an FMA chain per lane and a 3-step DPP sum
   constexpr int NQ = CR_MAXBP / 8;
@@ -1639,6 +1694,19 @@ __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, in
     t[q] = (live && c < Cg) ? w[2 * BP + c] : 0.0;
   }
   const double rhs = live ? w[2 * BP + Cg] : 0.0;
+  ready(l, r);
+  if (tid < BP) {
+    if (HANDOFF) {
+      const double xl = ld_sc1(dcv + (size_t)l * BP + tid);
+      const double xr = ld_sc1(dcv + (size_t)(r >= 0 ? r : l) * BP + tid);
+      sl[tid] = xl;
+      sr_[tid] = r >= 0 ? xr : 0.0;
+    } else {
+      sl[tid] = dcv[(size_t)l * BP + tid];
+      sr_[tid] = r >= 0 ? dcv[(size_t)r * BP + tid] : 0.0;
+    }
+  }
+  if (tid < 32) st_[tid] = tid < Cg ? dtau[tid] : 0.0;
   __syncthreads();
   double v = 0.0;
 #pragma unroll
@@ -1652,7 +1720,13 @@ __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, in
     if (c < 32) v = fma(t[q], st_[c], v);
   }
   v = group_sum<8>(v);
-  if (live && j == 0) dcv[(size_t)i * BP + row] = rhs - v;
+  if (live && j == 0) {
+    if (HANDOFF)
+      st_sc1(dcv + (size_t)i * BP + row, rhs - v);
+    else
+      dcv[(size_t)i * BP + row] = rhs - v;
+    if (sout) sout[row] = rhs - v;
+  }
 }
 
 __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int bend,
@@ -1662,6 +1736,71 @@ __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int 
   if (st->status != 0) return;
   __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32];
   cr_back_block(d, a0 + s * (2 * blockIdx.x + 1), s, bend, Wc, dtau, dcv, sl, sr_, st_);
+}
+
+// Every back-substitution level of the single-GPU solve in one launch (nblk - 1
+// workgroups, one per eliminated block; block 0 is k_cr_top's). A workgroup takes a ticket
+// at entry; tickets are dealt coarse level first, so a block only ever waits for blocks of
+// lower tickets, whose workgroups have already started: the grid drains whatever the
+// residency (one 1024-thread workgroup per CU). Each workgroup issues its W loads (no
+// dependency) and then waits until the rows of its two survivors are published, so the
+// levels chain through L2 (a flag and 2 x BP doubles per level) instead of kernel
+// boundaries. Hand-off (MI355X_MICROARCH.md, visibility table row 1): the rows are stored
+// sc1 (written through to memory), every storing wave drains its stores, a barrier, then one
+// lane stores the block's stamp sc1; the consumer's lane 0 polls the stamps with relaxed sc1
+// loads, a barrier, and every load of the rows is an sc1 load - no L2 write-back or
+// invalidate anywhere. Stamps count launches (ticket / (nblk - 1) + 1): `bk` = [0] ticket
+// counter, [1 + b] stamp of block b, zeroed by fte_setup. A spin that outlives ~0.3 s gives
+// up and counts into *bad (the solve then reports a failed factorisation).
+__global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, const FteState* __restrict__ st,
+                                                      const double* __restrict__ Wc, const double* __restrict__ dtau,
+                                                      double* __restrict__ dcv, int* __restrict__ bk,
+                                                      int* __restrict__ bad, double* __restrict__ Xbuf,
+                                                      double* __restrict__ normp) {
+  __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32], sdv[CR_MAXBP], s_red[1024];
+  __shared__ int s_tk;
+  const int nwork = d.nblk - 1;
+  if (threadIdx.x == 0) s_tk = atomicAdd(bk, 1);
+  __syncthreads();
+  const unsigned tk = (unsigned)s_tk;
+  if (st->status != 0) return;
+  const int stamp = (int)(tk / (unsigned)nwork) + 1;
+  int w = (int)(tk % (unsigned)nwork), s = 1, i = 1;
+  for (int lv = d.nlev - 1; lv >= 0; --lv) {
+    const int sv = 1 << lv, ne = (d.nblk - sv + 2 * sv - 1) / (2 * sv);
+    if (w < ne) {
+      s = sv;
+      i = sv * (2 * w + 1);
+      break;
+    }
+    w -= ne;
+  }
+  int* flag = bk + 1;
+  cr_back_block<true>(d, i, s, bend, Wc, dtau, dcv, sl, sr_, st_, [&](int l, int r) {
+    if (threadIdx.x == 0) {
+      const unsigned long long t0 = wall_clock64();
+      bool late = false;
+      for (int k = 0; k < 2 && !late; ++k) {
+        const int b = k ? r : l;
+        if (b <= 0) continue;  // block 0: k_cr_top, an earlier launch
+        while (__hip_atomic_load(flag + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != stamp) {
+          if (wall_clock64() - t0 > 30000000ull) {
+            late = true;
+            atomicAdd(bad, 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+    }
+    __syncthreads();
+  }, Xbuf ? sdv : nullptr);
+  // this block's rows are out (sc1): drain every storing wave, then publish the stamp
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag + i, stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // constant / no delays: this block's trial state and norms (k_cr_trial's work)
+  if (Xbuf) cr_trial_rows(d, st, i, threadIdx.x < d.BP ? sdv[threadIdx.x] : 0.0, dtau, Xbuf, nullptr, normp, false, s_red);
 }
 
 // trial state X + delta, tau + dtau (clipped), norm partials per super-block. Variable
@@ -1916,7 +2055,8 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
 // pivot counter and the tau step zeroed (Xsrc / tausrc may be copy 0 itself)
 __global__ __launch_bounds__(256) void k_fte_init_state(double* __restrict__ X, const double* Xsrc, size_t MP,
                                                         double* __restrict__ tau, const double* tausrc, int NT,
-                                                        int* __restrict__ bad, double* __restrict__ dtau, int GR) {
+                                                        int* __restrict__ bad, double* __restrict__ dtau, int GR,
+                                                        int* __restrict__ bk, int nbk) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < MP) {
     const double v = Xsrc[i];
@@ -1929,6 +2069,7 @@ __global__ __launch_bounds__(256) void k_fte_init_state(double* __restrict__ X, 
     tau[NT + i] = 0.0;
   }
   if (i < (size_t)GR) dtau[i] = 0.0;
+  if (i < (size_t)nbk) bk[i] = 0;
   if (i == 0) *bad = 0;
 }
 
@@ -1942,6 +2083,7 @@ struct FteBuffers {
   // per-row max |delay gradient| of the frame the row starts, per-block delay step / state norms
   double *graw, *gmaxt, *normt;
   int* bad;
+  int* bk;  // k_cr_back_all: ticket counter + per-block stamps
   FteState* st;
 };
 
@@ -2019,7 +2161,8 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
                odR = take((size_t)n * BP * (BP + GR)),
                odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)),
                onp = take(2 * (size_t)n), oTc = take(nlin * N * std::max(tc_stride(d.Cg), 1)), oFm = take(N), oFq = take(N), ost = take(16), oint = take(8),
-               ogr = take((size_t)M * P), ogt = take(M), ont = take(2 * (size_t)n);
+               ogr = take((size_t)M * P), ogt = take(M), ont = take(2 * (size_t)n),
+               obk = take((size_t)n / 2 + 2);
   // staged inputs (owned mode only)
   const size_t oI = take((n_ints + 1) / 2 + 1), oR = take(n_reals), oC = take((size_t)ACS_CAM_STRIDE * C),
                oMe = take((size_t)N * C * L * 2), oWt = take((size_t)N * C * L), oQ = take(P);
@@ -2092,6 +2235,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.Fq = arena + oFq;
   b.st = (FteState*)(arena + ost);
   b.bad = (int*)(arena + oint);
+  b.bk = (int*)(arena + obk);
   // state buffers in one launch (was six copies / fills): host inputs are copied into copy 0
   // first and the kernel then works in place
   const double* Xs = X;
@@ -2103,9 +2247,9 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
     ts = tau ? b.tau : nullptr;
   }
   const size_t MP = (size_t)M * P;
-  const size_t nI = std::max(MP, (size_t)std::max(d.NT, GR));
+  const size_t nI = std::max(std::max(MP, (size_t)n + 1), (size_t)std::max(d.NT, GR));
   hipLaunchKernelGGL(k_fte_init_state, dim3(acs_grid((int64_t)nI, 256)), dim3(256), 0, s, b.X, Xs, MP, b.tau, ts,
-                     d.NT, b.bad, b.dtau, GR);
+                     d.NT, b.bad, b.dtau, GR, b.bk, n + 1);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }
@@ -2251,18 +2395,21 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, sym);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
                      d.N, 0, d.nblk, 1, (const double*)b.Tc);
-  // (one launch per back-substitution level: running the top levels' few blocks one after
-  // the other inside k_cr_top's workgroup was tried in r03 and took 30 us instead of the 18 us
-  // of four launches - one workgroup streams a block's W at ~2 us)
+  // constant / no delays: the trial state is stepped by k_cr_top (block 0, delays) and
+  // k_cr_back_all (every other block); variable delays need the neighbours' rows: k_cr_trial
+  double* Xt = d.var ? nullptr : b.X;
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, d, b.st, (const double*)b.Wc, b.part, b.gmaxp, b.tau, b.dcv,
-                     b.dtau, b.bad);
-  for (int lv = d.nlev - 1; lv >= 0; --lv) {
-    const int st = 1 << lv;
-    const int ne = (d.nblk - st + 2 * st - 1) / (2 * st);
-    hipLaunchKernelGGL(k_cr_back, dim3(ne), dim3(1024), 0, s, d, st, 0, bend, b.st, b.Wc, b.dtau, b.dcv);
-  }
-  hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
-                     b.normp, 1, 0, 1);
+                     b.dtau, b.bad, Xt, b.normp);
+  // every back-substitution level in one launch, chained by per-block stamps (running the
+  // top levels' few blocks one after the other inside k_cr_top's workgroup was tried in r03
+  // and took 30 us: one workgroup streams a block's W at ~2 us, so the W loads of every
+  // block have to be in flight at once)
+  if (d.nblk > 1)
+    hipLaunchKernelGGL(k_cr_back_all, dim3(d.nblk - 1), dim3(1024), 0, s, d, bend, b.st, (const double*)b.Wc,
+                       (const double*)b.dtau, b.dcv, b.bk, b.bad, Xt, b.normp);
+  if (d.var)
+    hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
+                       b.normp, 1, 0, 1);
   // speculative linearisation at the trial state: its measurement terms and the model terms
   // are the trial cost (no separate cost pass)
   hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,

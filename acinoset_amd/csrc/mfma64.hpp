@@ -70,9 +70,43 @@ __device__ __forceinline__ double read_lane_f64(double x, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
                           __builtin_amdgcn_readlane(__double2loint(x), l));
 }
+// acc - x[lane 16 (l >> 4) + S] * y in ONE instruction: the pivot column's DPP row_newbcast
+// folded into a 64-bit DPP FMA (gfx950 DPP64 supports row_newbcast; the compiler emits
+// v_mov_b64_dpp + v_fma_f64 for the same expression). The s_nop covers the VALU-write ->
+// DPP-read hazard on x, which the compiler cannot see inside the asm.
+template <int S>
+__device__ __forceinline__ double fnmac_colb(double acc, double x, double y) {
+  asm("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+      : "+v"(acc)
+      : "v"(x), "v"(y), "i"(S));
+  return acc;
+}
+
 // One Gauss-Jordan step (pivot S) of tile16_gj_inverse; nbad counts failed pivots (uniform).
+// With the pivot row r_c = a_Sc (r_S taken as 1) and aip_c = r_c / p, every element off the
+// pivot row is  a_ic [c != S] - a_iS aip_c  (c = S: -a_iS / p; else a_ic - a_iS a_Sc / p) and
+// the pivot row is aip: per register one multiply by the column mask and one DPP FMA, the
+// same roundings as the select form (tile16_gj_step_v1), ~29 VALU instructions instead of ~48.
 template <int S, bool SPD>
 __device__ __forceinline__ void tile16_gj_step(double* v, int lane, int& nbad) {
+  constexpr int QS = S >> 2, RS = S & 3;
+  const bool rowS = (lane >> 4) == RS, colS = (lane & 15) == S;
+  double p = read_lane_f64(v[QS], RS * 16 + S);  // A[S][S] (uniform)
+  const double asc = tile_row_bcast<RS>(v[QS]);  // A[S][c]
+  const bool ok = SPD ? p > 0.0 : fabs(p) > 1e-300;
+  nbad += ok ? 0 : 1;
+  p = ok ? p : 1e-300;
+  const double ip = rcp_nr(p);
+  const double aip = colS ? ip : asc * ip;
+  const double m = colS ? 0.0 : 1.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double t = fnmac_colb<S>(v[q] * m, v[q], aip);
+    v[q] = (q == QS && rowS) ? aip : t;
+  }
+}
+template <int S, bool SPD>
+__device__ __forceinline__ void tile16_gj_step_v1(double* v, int lane, int& nbad) {
   constexpr int QS = S >> 2, RS = S & 3;
   const bool rowS = (lane >> 4) == RS, colS = (lane & 15) == S;
   double p = read_lane_f64(v[QS], RS * 16 + S);  // A[S][S] (uniform)
@@ -110,6 +144,18 @@ template <bool SPD, typename Hook>
 __device__ __forceinline__ void tile16_gj_inverse_hook(double* v, int lane, int* bad, Hook&& hook) {
   int nbad = 0;
   tile16_gj_steps_hook<SPD>(v, lane, nbad, hook, std::make_integer_sequence<int, 16>{});
+  if (nbad && bad && lane == 0) atomicAdd(bad, nbad);
+}
+
+// the select form of the step (round 1-2), kept for tools/probe/tile_inv_probe.hip
+template <bool SPD, int... S>
+__device__ __forceinline__ void tile16_gj_steps_v1(double* v, int lane, int& nbad, std::integer_sequence<int, S...>) {
+  (tile16_gj_step_v1<S, SPD>(v, lane, nbad), ...);
+}
+template <bool SPD>
+__device__ __forceinline__ void tile16_gj_inverse_v1(double* v, int lane, int* bad) {
+  int nbad = 0;
+  tile16_gj_steps_v1<SPD>(v, lane, nbad, std::make_integer_sequence<int, 16>{});
   if (nbad && bad && lane == 0) atomicAdd(bad, nbad);
 }
 

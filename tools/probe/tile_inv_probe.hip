@@ -36,7 +36,9 @@ __global__ void k_inv(const double* A, double* out, long long* cyc, int* bad, in
   for (int q = 0; q < 4; ++q) v[q] = a[(r0 + 4 * q) * 16 + c];
   long long t0 = clock64();
   for (int r = 0; r < reps; ++r) {
-    if (MODE == 0) inv_shfl(v, lane); else tile16_gj_inverse<true>(v, lane, bad);
+    if (MODE == 0) inv_shfl(v, lane);
+    else if (MODE == 1) tile16_gj_inverse_v1<true>(v, lane, bad);
+    else tile16_gj_inverse<true>(v, lane, bad);
   }
   long long t1 = clock64();
   for (int q = 0; q < 4; ++q) out[blockIdx.x * 256 + (r0 + 4 * q) * 16 + c] = v[q];
@@ -58,6 +60,7 @@ int main() {
   double* ref = (double*)malloc(NT * 256 * 8);
   double* o0 = (double*)malloc(NT * 256 * 8);
   double* o1 = (double*)malloc(NT * 256 * 8);
+  double* o2 = (double*)malloc(NT * 256 * 8);
   srand(1);
   for (int t = 0; t < NT; ++t) {
     double B[256];
@@ -73,17 +76,23 @@ int main() {
   hipMalloc(&dA, NT * 256 * 8); hipMalloc(&dO, NT * 256 * 8); hipMalloc(&dc, NT * 8); hipMalloc(&db, 4);
   hipMemcpy(dA, hA, NT * 256 * 8, hipMemcpyHostToDevice); hipMemset(db, 0, 4);
   long long cyc[NT];
-  for (int mode = 0; mode < 2; ++mode) {
+  const char* names[3] = {"shfl", "valu-select", "valu-dpp64"};
+  double* outs[3] = {o0, o1, o2};
+  for (int mode = 0; mode < 3; ++mode) {
     for (int reps : {1, 1, 9}) {
       if (mode == 0) hipLaunchKernelGGL(k_inv<0>, dim3(NT), dim3(64), 0, 0, dA, dO, dc, db, reps);
-      else hipLaunchKernelGGL(k_inv<1>, dim3(NT), dim3(64), 0, 0, dA, dO, dc, db, reps);
+      else if (mode == 1) hipLaunchKernelGGL(k_inv<1>, dim3(NT), dim3(64), 0, 0, dA, dO, dc, db, reps);
+      else hipLaunchKernelGGL(k_inv<2>, dim3(NT), dim3(64), 0, 0, dA, dO, dc, db, reps);
       hipDeviceSynchronize();
       hipMemcpy(cyc, dc, NT * 8, hipMemcpyDeviceToHost);
-      if (reps == 1) hipMemcpy(mode ? o1 : o0, dO, NT * 256 * 8, hipMemcpyDeviceToHost);
+      if (reps == 1) hipMemcpy(outs[mode], dO, NT * 256 * 8, hipMemcpyDeviceToHost);
       double mc = 0; for (int t = 0; t < NT; ++t) mc += cyc[t];
-      printf("mode %s reps %d: %.0f clock64 ticks per inverse\n", mode ? "valu" : "shfl", reps, mc / NT / reps);
+      printf("mode %s reps %d: %.0f clock64 ticks per inverse\n", names[mode], reps, mc / NT / reps);
     }
   }
+  long long ndiff = 0;
+  for (int e = 0; e < NT * 256; ++e) ndiff += (o1[e] != o2[e]);
+  printf("dpp64 vs select: %lld of %d elements differ\n", ndiff, NT * 256);
   double e0 = 0, e1 = 0, e01 = 0;
   for (int t = 0; t < NT; ++t) {
     double mx = 0; for (int e = 0; e < 256; ++e) mx = fmax(mx, fabs(ref[t * 256 + e]));
