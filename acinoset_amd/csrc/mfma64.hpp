@@ -70,25 +70,30 @@ __device__ __forceinline__ double read_lane_f64(double x, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
                           __builtin_amdgcn_readlane(__double2loint(x), l));
 }
-// acc - x[lane 16 (l >> 4) + S] * y in ONE instruction: the pivot column's DPP row_newbcast
-// folded into a 64-bit DPP FMA (gfx950 DPP64 supports row_newbcast; the compiler emits
-// v_mov_b64_dpp + v_fma_f64 for the same expression). The s_nop covers the VALU-write ->
-// DPP-read hazard on x, which the compiler cannot see inside the asm.
+// x from lane 16 (l >> 4) + S as one 64-bit DPP move (gfx950 DPP64 row_newbcast; the
+// 32-bit form, tile_col_bcast, needs two)
 template <int S>
-__device__ __forceinline__ double fnmac_colb(double acc, double x, double y) {
-  asm("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-      : "+v"(acc)
-      : "v"(x), "v"(y), "i"(S));
-  return acc;
+__device__ __forceinline__ double tile_col_bcast64(double x) {
+  const long long b = __double_as_longlong(x);
+  return __longlong_as_double(__builtin_amdgcn_update_dpp(b, b, 0x150 + S, 0xf, 0xf, true));
 }
 
 // One Gauss-Jordan step (pivot S) of tile16_gj_inverse; nbad counts failed pivots (uniform).
-// With the pivot row r_c = a_Sc (r_S taken as 1) and aip_c = r_c / p, every element off the
-// pivot row is  a_ic [c != S] - a_iS aip_c  (c = S: -a_iS / p; else a_ic - a_iS a_Sc / p) and
-// the pivot row is aip: per register one multiply by the column mask and one DPP FMA, the
-// same roundings as the select form (tile16_gj_step_v1), ~29 VALU instructions instead of ~48.
+// With aip_c = a_Sc / p off column S and 1 / p on it, every element off the pivot row is
+// a_ic [c != S] - a_iS aip_c  (c = S: -a_iS / p; else a_ic - a_iS a_Sc / p) and the pivot row
+// is aip: per register a multiply by the column mask, one 64-bit DPP broadcast of the pivot
+// column and one FMA. The roundings are the select form's (tile16_gj_step_v1): 3,723 instead
+// of 4,386 clock ticks per 16x16 inverse, bit-identical results (tools/probe/tile_inv_probe.hip,
+// profiles/r03/tile_inv_dpp2.log). Tried: the broadcast folded into v_fmac_f64_dpp by
+// inline asm (3,887 ticks in the probe, but the asm operands made k_cr_level spill), the
+// pivot row through ds_bpermute (4,338: its latency sits on the step's chain) and the
+// positivity count on the SALU from the pivot's bits (4,597).
+// `mhi`: high word of the column mask (1.0 off column S, 0.0 on it), rotated one lane per
+// step (DPP row_ror:1) rather than formed per step: sixteen lane-constant masks would be
+// hoisted to the kernel entry and cost 32 VGPRs in the callers.
+__device__ __forceinline__ unsigned tile16_colmask_init(int lane) { return (lane & 15) == 0 ? 0u : 0x3FF00000u; }
 template <int S, bool SPD>
-__device__ __forceinline__ void tile16_gj_step(double* v, int lane, int& nbad) {
+__device__ __forceinline__ void tile16_gj_step(double* v, int lane, int& nbad, unsigned& mhi) {
   constexpr int QS = S >> 2, RS = S & 3;
   const bool rowS = (lane >> 4) == RS, colS = (lane & 15) == S;
   double p = read_lane_f64(v[QS], RS * 16 + S);  // A[S][S] (uniform)
@@ -98,12 +103,13 @@ __device__ __forceinline__ void tile16_gj_step(double* v, int lane, int& nbad) {
   p = ok ? p : 1e-300;
   const double ip = rcp_nr(p);
   const double aip = colS ? ip : asc * ip;
-  const double m = colS ? 0.0 : 1.0;
+  const double m = __hiloint2double((int)mhi, 0);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const double t = fnmac_colb<S>(v[q] * m, v[q], aip);
+    const double t = fma(-tile_col_bcast64<S>(v[q]), aip, v[q] * m);
     v[q] = (q == QS && rowS) ? aip : t;
   }
+  if (S < 15) mhi = (unsigned)__builtin_amdgcn_mov_dpp((int)mhi, 0x121, 0xf, 0xf, false);  // row_ror:1
 }
 template <int S, bool SPD>
 __device__ __forceinline__ void tile16_gj_step_v1(double* v, int lane, int& nbad) {
@@ -129,7 +135,8 @@ __device__ __forceinline__ void tile16_gj_step_v1(double* v, int lane, int& nbad
 }
 template <bool SPD, int... S>
 __device__ __forceinline__ void tile16_gj_steps(double* v, int lane, int& nbad, std::integer_sequence<int, S...>) {
-  (tile16_gj_step<S, SPD>(v, lane, nbad), ...);
+  unsigned mhi = tile16_colmask_init(lane);
+  (tile16_gj_step<S, SPD>(v, lane, nbad, mhi), ...);
 }
 
 // The same 16 steps with hook(std::integral_constant<int, s>) called after step s: lets
@@ -138,7 +145,8 @@ __device__ __forceinline__ void tile16_gj_steps(double* v, int lane, int& nbad, 
 template <bool SPD, typename Hook, int... S>
 __device__ __forceinline__ void tile16_gj_steps_hook(double* v, int lane, int& nbad, Hook& hook,
                                                      std::integer_sequence<int, S...>) {
-  ((tile16_gj_step<S, SPD>(v, lane, nbad), hook(std::integral_constant<int, S>{})), ...);
+  unsigned mhi = tile16_colmask_init(lane);
+  ((tile16_gj_step<S, SPD>(v, lane, nbad, mhi), hook(std::integral_constant<int, S>{})), ...);
 }
 template <bool SPD, typename Hook>
 __device__ __forceinline__ void tile16_gj_inverse_hook(double* v, int lane, int* bad, Hook&& hook) {
