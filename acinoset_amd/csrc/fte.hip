@@ -1529,7 +1529,15 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
 // Thread e < 3P holds row e of the step (`dv`); thread c < C steps delay c. The sums are
 // k_cr_trial's bit for bit: the same per-thread terms in the same order, and block_sum's
 // tree over 1024 threads first folds threads >= 256 (zeros) exactly.
-__device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* st, int i, double dv,
+// this thread's current-state element of block i (issued early by the callers: its load
+// latency then hides behind their work)
+__device__ __forceinline__ double cr_trial_x(const FteDims& d, const FteState* st, int i,
+                                             const double* __restrict__ Xbuf) {
+  const int P = d.P, e = threadIdx.x;
+  if (!Xbuf || e >= 3 * P || 3 * i + e / P >= d.M) return 0.0;
+  return Xbuf[(size_t)st->cur * d.M * P + (size_t)(3 * i + e / P) * P + e % P];
+}
+__device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* st, int i, double dv, double x,
                                               const double* __restrict__ dtau, double* __restrict__ Xbuf,
                                               double* __restrict__ taubuf, double* __restrict__ normp, bool taus,
                                               double* s_red) {
@@ -1539,7 +1547,6 @@ __device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* 
     const int f = 3 * i + e / P, p = e % P;
     if (f < d.M) {
       const size_t o = (size_t)f * P + p;
-      const double x = Xbuf[(size_t)cur * d.M * P + o];
       Xbuf[(size_t)(cur ^ 1) * d.M * P + o] = x + dv;
       dn += dv * dv;
       xn += x * x;
@@ -1573,6 +1580,7 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
   const int tid = threadIdx.x, nth = blockDim.x;
   const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
   const double lam = st->lam;
+  const double xpre = cr_trial_x(d, st, 0, Xbuf);
   __shared__ double sS[32 * 32];
   __shared__ double sr[32];
   __shared__ double tmp[512];
@@ -1581,19 +1589,38 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
   const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
   __shared__ double s_sum[16 * 16 + 16 + 32 * 32];
   __shared__ int s_held[32];
-  for (int e = tid; e < nE; e += nth) {
-    // 16 loads in flight at a time, summed in chunk order
-    double v = 0.0;
-    for (int c0 = 0; c0 < CR_NCHUNK; c0 += 16) {
-      double pv[16];
+  {
+    // the chunk range split over ns = nth / nE thread slices (every load of a slice in
+    // flight at once, at most 32 per thread), each summed in chunk order, then the slices
+    // in slice order: a fixed order, independent of timing
+    const int ns = nE <= nth ? min(nth / nE, 4) : 1;
+    const int cps = (CR_NCHUNK + ns - 1) / ns;
+    for (int t = tid; t < ns * nE; t += nth) {
+      const int sl = t / nE, e = t - sl * nE;
+      const int c0 = sl * cps, c1 = min(CR_NCHUNK, c0 + cps);
+      double v = 0.0;
+      for (int cb = c0; cb < c1; cb += 16) {
+        double pv[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) pv[q] = part[(size_t)(c0 + q) * nE + e];
+        for (int q = 0; q < 16; ++q) pv[q] = cb + q < c1 ? part[(size_t)(cb + q) * nE + e] : 0.0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) v += pv[q];
+        for (int q = 0; q < 16; ++q) v += pv[q];
+      }
+      if (ns == 1)
+        s_sum[e] = v;  // nE may exceed the 1024 slots of s_red
+      else
+        s_red[t] = v;
     }
-    s_sum[e] = v;
+    __syncthreads();
+    if (ns > 1) {
+      for (int e = tid; e < nE; e += nth) {
+        double v = 0.0;
+        for (int sl = 0; sl < ns; ++sl) v += s_red[sl * nE + e];
+        s_sum[e] = v;
+      }
+      __syncthreads();
+    }
   }
-  __syncthreads();
   if (tid < 32) s_held[tid] = tid >= Cg || tau_held(taubuf[(size_t)st->cur * d.NT + tid], s_sum[nH + tid], d.Ts, tid);
   __syncthreads();
   // gradient max (frames + free tau border)
@@ -1647,7 +1674,7 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
     v0 = v;
   }
   // the single-GPU solve steps block 0 (and the constant delays) here: no k_cr_trial launch
-  if (Xbuf) cr_trial_rows(d, st, 0, v0, dtau, Xbuf, taubuf, normp, d.Cg != 0, s_red);
+  if (Xbuf) cr_trial_rows(d, st, 0, v0, xpre, dtau, Xbuf, taubuf, normp, d.Cg != 0, s_red);
 }
 
 // back substitution of eliminated block i at level s (blockDim 1024; every thread calls it).
@@ -1776,6 +1803,7 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, const
     w -= ne;
   }
   int* flag = bk + 1;
+  const double xpre = cr_trial_x(d, st, i, Xbuf);
   cr_back_block<true>(d, i, s, bend, Wc, dtau, dcv, sl, sr_, st_, [&](int l, int r) {
     if (threadIdx.x == 0) {
       const unsigned long long t0 = wall_clock64();
@@ -1800,7 +1828,8 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, const
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(flag + i, stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // constant / no delays: this block's trial state and norms (k_cr_trial's work)
-  if (Xbuf) cr_trial_rows(d, st, i, threadIdx.x < d.BP ? sdv[threadIdx.x] : 0.0, dtau, Xbuf, nullptr, normp, false, s_red);
+  if (Xbuf) cr_trial_rows(d, st, i, threadIdx.x < d.BP ? sdv[threadIdx.x] : 0.0, xpre, dtau, Xbuf, nullptr, normp, false,
+                          s_red);
 }
 
 // trial state X + delta, tau + dtau (clipped), norm partials per super-block. Variable
