@@ -1678,26 +1678,12 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
 }
 
 // back substitution of eliminated block i at level s (blockDim 1024; every thread calls it).
-// `ready(l, r)` runs after the W loads are issued and before the survivors' rows are read
-// (k_cr_back_all waits there for the blocks of coarser levels). HANDOFF: the rows of dcv are
-// read and written as agent-scope relaxed 8-byte accesses (global sc1: L2-served, written
-// through), the form k_cr_back_all's in-launch hand-off needs.
-struct CrNoWait {
-  __device__ void operator()(int, int) const {}
-};
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __longlong_as_double(
-      (long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-template <bool HANDOFF = false, typename Ready = CrNoWait>
+// `fetch(l, r)` runs after the W loads are issued and fills sl / sr_ (threads < BP) with the
+// survivors' rows; `publish(row, value)` stores one row of the block's step.
+template <typename Fetch, typename Publish>
 __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, int bend, const double* __restrict__ Wc,
-                                              const double* __restrict__ dtau, double* __restrict__ dcv, double* sl,
-                                              double* sr_, double* st_, Ready ready = Ready{},
-                                              double* sout = nullptr) {
+                                              const double* __restrict__ dtau, double* sl, double* sr_, double* st_,
+                                              Fetch fetch, Publish publish) {
   const int l = i - s, r = (i + s <= bend && i + s < d.nblk) ? i + s : -1;
   const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
   const double* W = Wc + (size_t)i * BP * WL;
@@ -1721,18 +1707,7 @@ __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, in
     t[q] = (live && c < Cg) ? w[2 * BP + c] : 0.0;
   }
   const double rhs = live ? w[2 * BP + Cg] : 0.0;
-  ready(l, r);
-  if (tid < BP) {
-    if (HANDOFF) {
-      const double xl = ld_sc1(dcv + (size_t)l * BP + tid);
-      const double xr = ld_sc1(dcv + (size_t)(r >= 0 ? r : l) * BP + tid);
-      sl[tid] = xl;
-      sr_[tid] = r >= 0 ? xr : 0.0;
-    } else {
-      sl[tid] = dcv[(size_t)l * BP + tid];
-      sr_[tid] = r >= 0 ? dcv[(size_t)r * BP + tid] : 0.0;
-    }
-  }
+  fetch(l, r);
   if (tid < 32) st_[tid] = tid < Cg ? dtau[tid] : 0.0;
   __syncthreads();
   double v = 0.0;
@@ -1747,13 +1722,7 @@ __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, in
     if (c < 32) v = fma(t[q], st_[c], v);
   }
   v = group_sum<8>(v);
-  if (live && j == 0) {
-    if (HANDOFF)
-      st_sc1(dcv + (size_t)i * BP + row, rhs - v);
-    else
-      dcv[(size_t)i * BP + row] = rhs - v;
-    if (sout) sout[row] = rhs - v;
-  }
+  if (live && j == 0) publish(row, rhs - v);
 }
 
 __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int bend,
@@ -1762,7 +1731,16 @@ __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int 
                                                   double* __restrict__ dcv) {
   if (st->status != 0) return;
   __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32];
-  cr_back_block(d, a0 + s * (2 * blockIdx.x + 1), s, bend, Wc, dtau, dcv, sl, sr_, st_);
+  const int i = a0 + s * (2 * blockIdx.x + 1), BP = d.BP;
+  cr_back_block(
+      d, i, s, bend, Wc, dtau, sl, sr_, st_,
+      [&](int l, int r) {
+        if ((int)threadIdx.x < BP) {
+          sl[threadIdx.x] = dcv[(size_t)l * BP + threadIdx.x];
+          sr_[threadIdx.x] = r >= 0 ? dcv[(size_t)r * BP + threadIdx.x] : 0.0;
+        }
+      },
+      [&](int row, double v) { dcv[(size_t)i * BP + row] = v; });
 }
 
 // Every back-substitution level of the single-GPU solve in one launch (nblk - 1
@@ -1770,20 +1748,22 @@ __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int 
 // at entry; tickets are dealt coarse level first, so a block only ever waits for blocks of
 // lower tickets, whose workgroups have already started: the grid drains whatever the
 // residency (one 1024-thread workgroup per CU). Each workgroup issues its W loads (no
-// dependency) and then waits until the rows of its two survivors are published, so the
-// levels chain through L2 (a flag and 2 x BP doubles per level) instead of kernel
-// boundaries. Hand-off (MI355X_MICROARCH.md, visibility table row 1): the rows are stored
-// sc1 (written through to memory), every storing wave drains its stores, a barrier, then one
-// lane stores the block's stamp sc1; the consumer's lane 0 polls the stamps with relaxed sc1
-// loads, a barrier, and every load of the rows is an sc1 load - no L2 write-back or
-// invalidate anywhere. Stamps count launches (ticket / (nblk - 1) + 1): `bk` = [0] ticket
-// counter, [1 + b] stamp of block b, zeroed by fte_setup. A spin that outlives ~0.3 s gives
-// up and counts into *bad (the solve then reports a failed factorisation).
+// dependency) and then waits for the rows of its two survivors, so the levels chain through
+// memory instead of kernel boundaries. Hand-off: the data is the flag
+// (cdna_hip_programming.md §6 Guideline 16, R2; MI355X_MICROARCH.md handoff-1to1): every
+// row goes out as two 8-byte granules {stamp, high word} {stamp, low word}, each ONE
+// relaxed agent-scope store (sc1, written through), and each consumer thread re-reads its
+// survivors' granules with sc1 loads until all carry this launch's stamp - no flag, no
+// drain, no fence, one memory round trip per level. Stamps count launches
+// (ticket / (nblk - 1) + 1; `bk[0]` the ticket counter, the granules `gdcv`, both zeroed by
+// fte_setup). The plain dcv rows are written too (k_cr_trial of the per-frame-delay mode
+// reads them). A spin that outlives ~0.3 s gives up and counts into *bad (the solve then
+// reports a failed factorisation instead of hanging).
 __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, const FteState* __restrict__ st,
                                                       const double* __restrict__ Wc, const double* __restrict__ dtau,
                                                       double* __restrict__ dcv, int* __restrict__ bk,
-                                                      int* __restrict__ bad, double* __restrict__ Xbuf,
-                                                      double* __restrict__ normp) {
+                                                      unsigned long long* __restrict__ gdcv, int* __restrict__ bad,
+                                                      double* __restrict__ Xbuf, double* __restrict__ normp) {
   __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32], sdv[CR_MAXBP], s_red[1024];
   __shared__ int s_tk;
   const int nwork = d.nblk - 1;
@@ -1791,7 +1771,7 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, const
   __syncthreads();
   const unsigned tk = (unsigned)s_tk;
   if (st->status != 0) return;
-  const int stamp = (int)(tk / (unsigned)nwork) + 1;
+  const unsigned long long stamp = tk / (unsigned)nwork + 1u;
   int w = (int)(tk % (unsigned)nwork), s = 1, i = 1;
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
     const int sv = 1 << lv, ne = (d.nblk - sv + 2 * sv - 1) / (2 * sv);
@@ -1802,33 +1782,52 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, const
     }
     w -= ne;
   }
-  int* flag = bk + 1;
+  const int BP = d.BP;
   const double xpre = cr_trial_x(d, st, i, Xbuf);
-  cr_back_block<true>(d, i, s, bend, Wc, dtau, dcv, sl, sr_, st_, [&](int l, int r) {
-    if (threadIdx.x == 0) {
-      const unsigned long long t0 = wall_clock64();
-      bool late = false;
-      for (int k = 0; k < 2 && !late; ++k) {
-        const int b = k ? r : l;
-        if (b <= 0) continue;  // block 0: k_cr_top, an earlier launch
-        while (__hip_atomic_load(flag + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != stamp) {
+  cr_back_block(
+      d, i, s, bend, Wc, dtau, sl, sr_, st_,
+      [&](int l, int r) {
+        const int t = threadIdx.x;
+        if (t >= BP) return;
+        if (l == 0) sl[t] = dcv[t];  // block 0: k_cr_top, an earlier launch
+        const unsigned long long* gl = gdcv + ((size_t)l * BP + t) * 2;
+        const unsigned long long* gr = gdcv + ((size_t)(r > 0 ? r : l) * BP + t) * 2;
+        const bool wl = l > 0, wr = r > 0;
+        const unsigned long long t0 = wall_clock64();
+        unsigned long long a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+        for (;;) {
+          if (wl) {
+            a0 = __hip_atomic_load(gl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a1 = __hip_atomic_load(gl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (wr) {
+            b0 = __hip_atomic_load(gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            b1 = __hip_atomic_load(gr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          const bool ok = (!wl || ((a0 >> 32) == stamp && (a1 >> 32) == stamp)) &&
+                          (!wr || ((b0 >> 32) == stamp && (b1 >> 32) == stamp));
+          if (ok) break;
           if (wall_clock64() - t0 > 30000000ull) {
-            late = true;
             atomicAdd(bad, 1);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
         }
-      }
-    }
-    __syncthreads();
-  }, Xbuf ? sdv : nullptr);
-  // this block's rows are out (sc1): drain every storing wave, then publish the stamp
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (wl) sl[t] = __hiloint2double((int)(unsigned)a0, (int)(unsigned)a1);
+        sr_[t] = wr ? __hiloint2double((int)(unsigned)b0, (int)(unsigned)b1) : 0.0;
+      },
+      [&](int row, double v) {
+        const size_t e = (size_t)i * BP + row;
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+        __hip_atomic_store(gdcv + 2 * e, (stamp << 32) | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gdcv + 2 * e + 1, (stamp << 32) | (bits & 0xffffffffull), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        dcv[e] = v;
+        sdv[row] = v;
+      });
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag + i, stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // constant / no delays: this block's trial state and norms (k_cr_trial's work)
-  if (Xbuf) cr_trial_rows(d, st, i, threadIdx.x < d.BP ? sdv[threadIdx.x] : 0.0, xpre, dtau, Xbuf, nullptr, normp, false,
+  if (Xbuf) cr_trial_rows(d, st, i, threadIdx.x < BP ? sdv[threadIdx.x] : 0.0, xpre, dtau, Xbuf, nullptr, normp, false,
                           s_red);
 }
 
@@ -2085,7 +2084,8 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
 __global__ __launch_bounds__(256) void k_fte_init_state(double* __restrict__ X, const double* Xsrc, size_t MP,
                                                         double* __restrict__ tau, const double* tausrc, int NT,
                                                         int* __restrict__ bad, double* __restrict__ dtau, int GR,
-                                                        int* __restrict__ bk, int nbk) {
+                                                        int* __restrict__ bk, int nbk,
+                                                        unsigned long long* __restrict__ gd, size_t ngd) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < MP) {
     const double v = Xsrc[i];
@@ -2099,6 +2099,7 @@ __global__ __launch_bounds__(256) void k_fte_init_state(double* __restrict__ X, 
   }
   if (i < (size_t)GR) dtau[i] = 0.0;
   if (i < (size_t)nbk) bk[i] = 0;
+  if (i < ngd) gd[i] = 0ull;
   if (i == 0) *bad = 0;
 }
 
@@ -2112,7 +2113,8 @@ struct FteBuffers {
   // per-row max |delay gradient| of the frame the row starts, per-block delay step / state norms
   double *graw, *gmaxt, *normt;
   int* bad;
-  int* bk;  // k_cr_back_all: ticket counter + per-block stamps
+  int* bk;                    // k_cr_back_all: ticket counter
+  unsigned long long* gdcv;   // k_cr_back_all: the step rows as {stamp, word} granules
   FteState* st;
 };
 
@@ -2191,7 +2193,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
                odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)),
                onp = take(2 * (size_t)n), oTc = take(nlin * N * std::max(tc_stride(d.Cg), 1)), oFm = take(N), oFq = take(N), ost = take(16), oint = take(8),
                ogr = take((size_t)M * P), ogt = take(M), ont = take(2 * (size_t)n),
-               obk = take((size_t)n / 2 + 2);
+               obk = take((size_t)n / 2 + 2), ogd = take((size_t)n * BP * 2);
   // staged inputs (owned mode only)
   const size_t oI = take((n_ints + 1) / 2 + 1), oR = take(n_reals), oC = take((size_t)ACS_CAM_STRIDE * C),
                oMe = take((size_t)N * C * L * 2), oWt = take((size_t)N * C * L), oQ = take(P);
@@ -2265,6 +2267,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   b.st = (FteState*)(arena + ost);
   b.bad = (int*)(arena + oint);
   b.bk = (int*)(arena + obk);
+  b.gdcv = (unsigned long long*)(arena + ogd);
   // state buffers in one launch (was six copies / fills): host inputs are copied into copy 0
   // first and the kernel then works in place
   const double* Xs = X;
@@ -2276,9 +2279,10 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
     ts = tau ? b.tau : nullptr;
   }
   const size_t MP = (size_t)M * P;
-  const size_t nI = std::max(std::max(MP, (size_t)n + 1), (size_t)std::max(d.NT, GR));
+  const size_t ngd = (size_t)n * BP * 2;
+  const size_t nI = std::max(std::max(std::max(MP, (size_t)n + 1), ngd), (size_t)std::max(d.NT, GR));
   hipLaunchKernelGGL(k_fte_init_state, dim3(acs_grid((int64_t)nI, 256)), dim3(256), 0, s, b.X, Xs, MP, b.tau, ts,
-                     d.NT, b.bad, b.dtau, GR, b.bk, n + 1);
+                     d.NT, b.bad, b.dtau, GR, b.bk, n + 1, b.gdcv, ngd);
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
 }
@@ -2435,7 +2439,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   // block have to be in flight at once)
   if (d.nblk > 1)
     hipLaunchKernelGGL(k_cr_back_all, dim3(d.nblk - 1), dim3(1024), 0, s, d, bend, b.st, (const double*)b.Wc,
-                       (const double*)b.dtau, b.dcv, b.bk, b.bad, Xt, b.normp);
+                       (const double*)b.dtau, b.dcv, b.bk, b.gdcv, b.bad, Xt, b.normp);
   if (d.var)
     hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
                        b.normp, 1, 0, 1);
