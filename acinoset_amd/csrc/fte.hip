@@ -1589,38 +1589,20 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
   const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
   __shared__ double s_sum[16 * 16 + 16 + 32 * 32];
   __shared__ int s_held[32];
-  {
-    // the chunk range split over ns = nth / nE thread slices (every load of a slice in
-    // flight at once, at most 32 per thread), each summed in chunk order, then the slices
-    // in slice order: a fixed order, independent of timing
-    const int ns = nE <= nth ? min(nth / nE, 4) : 1;
-    const int cps = (CR_NCHUNK + ns - 1) / ns;
-    for (int t = tid; t < ns * nE; t += nth) {
-      const int sl = t / nE, e = t - sl * nE;
-      const int c0 = sl * cps, c1 = min(CR_NCHUNK, c0 + cps);
-      double v = 0.0;
-      for (int cb = c0; cb < c1; cb += 16) {
-        double pv[16];
+  for (int e = tid; e < nE; e += nth) {
+    // 16 loads in flight at a time, summed in chunk order (one CU streams the 64 x nE
+    // partials from L2: splitting the chunks over more threads did not help, r03j)
+    double v = 0.0;
+    for (int c0 = 0; c0 < CR_NCHUNK; c0 += 16) {
+      double pv[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) pv[q] = cb + q < c1 ? part[(size_t)(cb + q) * nE + e] : 0.0;
+      for (int q = 0; q < 16; ++q) pv[q] = part[(size_t)(c0 + q) * nE + e];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v += pv[q];
-      }
-      if (ns == 1)
-        s_sum[e] = v;  // nE may exceed the 1024 slots of s_red
-      else
-        s_red[t] = v;
+      for (int q = 0; q < 16; ++q) v += pv[q];
     }
-    __syncthreads();
-    if (ns > 1) {
-      for (int e = tid; e < nE; e += nth) {
-        double v = 0.0;
-        for (int sl = 0; sl < ns; ++sl) v += s_red[sl * nE + e];
-        s_sum[e] = v;
-      }
-      __syncthreads();
-    }
+    s_sum[e] = v;
   }
+  __syncthreads();
   if (tid < 32) s_held[tid] = tid >= Cg || tau_held(taubuf[(size_t)st->cur * d.NT + tid], s_sum[nH + tid], d.Ts, tid);
   __syncthreads();
   // gradient max (frames + free tau border)
