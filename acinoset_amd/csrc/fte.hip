@@ -1128,19 +1128,23 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     }
   }
   PROF_T0
-  {
-    // every load in flight before the LDS stores (blockDim = 1024)
-    constexpr int NCP = (BP * BP + 1023) / 1024;
+  if (!dwave) {
+    // the column waves copy the coupling blocks (read only in the Schur phase, after the
+    // pivot steps' barriers); the row waves go straight to their loads: wave 0's first
+    // pivot tile no longer waits behind this copy's round trip. Every load in flight
+    // before the LDS stores (blockDim = 1024).
+    constexpr int CN = 1024 - 64 * NB, NCP = (BP * BP + CN - 1) / CN;
+    const int ct = tid - 64 * NB;
     double ve[NCP], vr[NCP];
 #pragma unroll
     for (int q = 0; q < NCP; ++q) {
-      const int e = tid + 1024 * q;
+      const int e = ct + CN * q;
       ve[q] = (Ei && e < BP * BP) ? Ei[e] : 0.0;
       vr[q] = (sEr && e < BP * BP) ? Er[e] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < NCP; ++q) {
-      const int e = tid + 1024 * q;
+      const int e = ct + CN * q;
       if (e < BP * BP) {
         sEi[e] = ve[q];
         if (sEr) sEr[(e / BP) * (BP + 1) + e % BP] = vr[q];
