@@ -25,6 +25,10 @@ v = np.array(buf[:], np.float64) * 10e-3 / n   # 100 MHz ticks -> us, per launch
 names = {32: 'wave 0 loads done', 33: 'col wave loads done', 34: 'pivot 0 inv+row', 35: 'pivot 1', 36: 'pivot 2',
          37: 'pivot 3', 38: 'pivot 4', 39: 'pivot 5', 40: 'col wave GJ done', 41: 'left term done',
          42: 'right term done', 43: 'Tau done'}
+# next pivot wave: after the barrier (44 + k) and after its inverse (50 + k)
+for k in range(4):
+    names[44 + k] = f'pivot {k + 1} start (after barrier)'
+    names[50 + k] = f'pivot {k + 1} inverse done'
 print(f'deep launches {buf[63]}; mean us since kernel start:')
 for k, nm in sorted(names.items(), key=lambda kv: v[kv[0]]):
     print(f'{nm:24s} {v[k]:8.2f}')
