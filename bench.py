@@ -53,6 +53,9 @@ def parse():
                     help='also time SBA at configs[4] scale on one GPU (0 = skip)')
     ap.add_argument('--scale-cams', type=int, default=12)
     ap.add_argument('--fte-frames', type=int, default=1000)
+    ap.add_argument('--no-graph', dest='graph', action='store_false', default=True,
+                    help='launch the K timed solves one by one on the stream instead of replaying them '
+                         'from one captured hipGraph')
     ap.add_argument('--event-every', type=int, default=8,
                     help='HIP event pairs bracket groups of this many consecutive timed steps '
                          '(kernel duration for the roofline)')
@@ -122,32 +125,73 @@ def main():
     rms_gpu, rms_ref = workloads.reproj_rms(res_gpu), workloads.reproj_rms(wl.ref_resid_after)
     dref = np.sqrt(np.sum((sol - wl.ref_pts) ** 2, 1))
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     # HIP events on the kernel's stream bracket consecutive groups of `every` steps (a pair
     # per launch would cost more host time than the launch itself and add its own latency
     # to the bracket); kernel_ms = bracketed GPU time / launches
     every = max(1, min(args.event_every, args.steps))
     ngrp = args.steps // every
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(ngrp)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        g, j = divmod(i, every)
-        if g < ngrp and j == 0:
-            ev[g][0].record(stream)
-        step()
-        if g < ngrp and j == every - 1:
-            ev[g][1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) / every
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+
+    def timed_stream():
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(ngrp)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            g, j = divmod(i, every)
+            if g < ngrp and j == 0:
+                ev[g][0].record(stream)
+            step()
+            if g < ngrp and j == every - 1:
+                ev[g][1].record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0, float(np.mean([a.elapsed_time(b) for a, b in ev])) / every
+
+    graph = None
+    if args.graph:
+        # the K timed solves captured once as K kernel nodes of one hipGraph (a graph node
+        # costs ~1.6 us of dispatch, a stream launch ~2.5 us: profiles/r02/launch_probe.log);
+        # every node is the full LM solve from the resident initial points. Captured and
+        # replayed once before the timed region (untimed warm-up).
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            for _ in range(args.steps):
+                step()
+        graph.replay()
+        torch.cuda.synchronize()
+
+    def timed_graph():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(stream)
+        graph.replay()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0, e0.elapsed_time(e1) / args.steps
+
+    def max_over_ranks(dt):
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
+
+    dt, kern_ms = timed_graph() if graph is not None else timed_stream()
+    dt = max_over_ranks(dt)
+    stream_line = None
+    if graph is not None:
+        # the same K solves launched one by one, for comparison (after the headline timing)
+        dts, kms = timed_stream()
+        dts = max_over_ranks(dts)
+        stream_line = {'value': wl.n_frames * world * args.steps / dts, 'ms_per_step': 1e3 * dts / args.steps,
+                       'kernel_ms': kms}
     ms_per_step = 1e3 * dt / args.steps
     frames_total = wl.n_frames * world * args.steps
     value = frames_total / dt
@@ -182,7 +226,8 @@ def main():
                    'parallelism': f'frame-shard x{world}'},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                     'kernel': 'k_sba_lm', 'kernel_ms': kern_ms, 'kernel_ms_launches': ngrp * every,
+                     'kernel': 'k_sba_lm', 'kernel_ms': kern_ms,
+                     'kernel_ms_launches': args.steps if graph is not None else ngrp * every,
                      'bytes_per_launch': bytes_launch,
                      'traffic_source': pmc['source'] if pmc else None,
                      'note': f'latency-bound at this size: {int(n_pts * _group(C) // 64)} waves for '
@@ -192,6 +237,9 @@ def main():
         'convergence': {'status': rep['status_counts'], 'iters_max': rep['iters_max'],
                         'gn_steps_mean': iters_mean, 'cost_before': rep['cost_before'],
                         'cost_after': rep['cost_after'], 'pos_rms_vs_truth_m': pos_rms},
+        'launch': ('one hipGraph of the K solves (K kernel nodes), replayed once in the timed region'
+                   if graph is not None else 'K stream launches'),
+        'stream_launch': stream_line,
         'reproj_rms_px': rms_gpu,
         'reproj_rms_ref_px': rms_ref,
         'reproj_rms_vs_ref_px': rms_gpu - rms_ref,
