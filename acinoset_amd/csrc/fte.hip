@@ -420,6 +420,14 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   //     tiles of NT x NT, tile t on wave t % 4
   // tile t = wave + 4q (q = 0..2) of the NT (NT + 1) / 2 upper-triangle tiles, row-major
   const int ntile = NT * (NT + 1) / 2;
+  // tile of this wave's q-th accumulator (-1: none): tile wave + 4q. (Dealing the
+  // products that survive the zero-tile skip as two 3-step chains per wave, with the
+  // gradient on wave 0, was slower in r03n: the gradient's dependent LDS chain then sits on
+  // a wave with a full MFMA share.)
+  auto tile_of = [&](int q) -> int {
+    const int t = wave + 4 * q;
+    return t < ntile ? t : -1;
+  };
   auto tile_ab = [&](int t, int& a, int& b) {
     a = 0;
     while (t >= NT - a) {
@@ -477,19 +485,28 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      if (wave + 4 * q >= ntile) break;
+      const int t = tile_of(q);
+      if (t < 0) continue;
       int ta, tb;
-      tile_ab(wave + 4 * q, ta, tb);
+      tile_ab(t, ta, tb);
       const int ci = ta * 16 + li, cj = tb * 16 + li;
+      // D rows are zero past column P (FK columns only) and Q rows are zero outside the
+      // own-shift (0..2) and shift / delay (P..NZ-1) columns: a product whose operand tile
+      // is all zero adds exact zeros and is skipped (at P = 26, NZ = 38: 12 of the 36 MFMAs
+      // per marker chunk; tile (2, 2) is the delay block, tpart only)
+      if (ta * 16 < P) {
 #pragma unroll
-      for (int r0 = 0; r0 < RC; r0 += 4) {
-        const int r = (r0 + lk) * LD;
-        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(sD[r + ci], sB[r + cj], acc[q], 0, 0, 0);
+        for (int r0 = 0; r0 < RC; r0 += 4) {
+          const int r = (r0 + lk) * LD;
+          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(sD[r + ci], sB[r + cj], acc[q], 0, 0, 0);
+        }
       }
+      if (tb * 16 < P && (ta == 0 || (ta * 16 + 15 >= P && ta * 16 < NZ))) {
 #pragma unroll
-      for (int r0 = 0; r0 < RC; r0 += 4) {
-        const int r = (r0 + lk) * LD;
-        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(sQ[r + ci], sD[r + cj], acc[q], 0, 0, 0);
+        for (int r0 = 0; r0 < RC; r0 += 4) {
+          const int r = (r0 + lk) * LD;
+          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(sQ[r + ci], sD[r + cj], acc[q], 0, 0, 0);
+        }
       }
     }
     __syncthreads();
@@ -525,9 +542,10 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   double* H = Hloc + (size_t)k * FTE_NZP * FTE_NZP;
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
-    if (wave + 4 * q >= ntile) break;
+    const int t = tile_of(q);
+    if (t < 0) continue;
     int ta, tb;
-    tile_ab(wave + 4 * q, ta, tb);
+    tile_ab(t, ta, tb);
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) {
       const int row = ta * 16 + lk + 4 * rg, col = tb * 16 + li;
