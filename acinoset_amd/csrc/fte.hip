@@ -1093,17 +1093,35 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     const double* pl = (j + hs < iend) ? dL + (size_t)(j + hs) * BP * LDD : nullptr;
     double* D = Dc + (size_t)j * BP * BP;
     double* G = GBc + (size_t)j * BP * GR;
-    for (int e = tid; e < BP * LDD; e += blockDim.x) {
+    // every load of the block in flight before the first store (blockDim = 1024; the loop
+    // form waited for each round of loads: ~15 us per survivor, which at 10,000 frames
+    // occupied whole CUs for rounds of the level)
+    constexpr int NQ = (BP * (BP + 32) + 1023) / 1024;  // GR <= 32
+    const int n = BP * LDD;
+    double vr[NQ], vl[NQ], vd[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int e = tid + 1024 * q;
       const int r = e / LDD, c = e - r * LDD;
       // D parts of the pending terms hold their upper tiles only (symmetric)
       const int es = (sym_in && c < BP && (r >> 4) > (c >> 4)) ? c * LDD + r : e;
+      const bool ok = e < n;
+      vr[q] = (ok && pr) ? pr[es] : 0.0;
+      vl[q] = (ok && pl) ? pl[es] : 0.0;
+      vd[q] = ok ? (c < BP ? D[r * BP + c] : G[r * GR + c - BP]) : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int e = tid + 1024 * q;
+      if (e >= n) continue;
+      const int r = e / LDD, c = e - r * LDD;
       double v = 0.0;
-      if (pr) v += pr[es];
-      if (pl) v += pl[es];
+      if (pr) v += vr[q];
+      if (pl) v += vl[q];
       if (c < BP)
-        D[r * BP + c] -= v;
+        D[r * BP + c] = vd[q] - v;
       else
-        G[r * GR + c - BP] -= v;
+        G[r * GR + c - BP] = vd[q] - v;
     }
     return;
   }
