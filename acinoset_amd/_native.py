@@ -39,8 +39,8 @@ SYMBOLS = (
     'acs_fte_dist_create', 'acs_fte_dist_init', 'acs_fte_dist_round', 'acs_fte_dist_poll',
     'acs_fte_dist_gather', 'acs_fte_dist_scatter', 'acs_fte_dist_result',
     'acs_fte_dist_destroy',
-    'acs_sba_ext_dist_create', 'acs_sba_ext_dist_init', 'acs_sba_ext_dist_phase1', 'acs_sba_ext_dist_phase2',
-    'acs_sba_ext_dist_phase3', 'acs_sba_ext_dist_result', 'acs_sba_ext_dist_destroy', 'acs_ekf_run',
+    'acs_sba_ext_dist_create', 'acs_sba_ext_dist_init', 'acs_sba_ext_dist_round', 'acs_sba_ext_dist_poll',
+    'acs_sba_ext_dist_result', 'acs_sba_ext_dist_destroy', 'acs_ekf_run',
     'acs_sba_ekf_pipeline',
 )
 
@@ -115,7 +115,7 @@ class SbaExtReport(C.Structure):
 
 
 # must equal ACS_ABI_VERSION in include/acinoset_hip.h (checked when the library loads)
-ABI_VERSION = 3
+ABI_VERSION = 4
 _lib = None
 _lock = threading.Lock()
 _P = C.c_void_p
@@ -163,9 +163,8 @@ def _declare(lib):
         'acs_sba_ext_dist_create': (C.c_int, [_P, _P, i32, _P, _P, _P, i64, _P, i64, C.POINTER(SbaExtOpts), i32, i32,
                                               C.POINTER(_P), C.POINTER(i64), u32]),
         'acs_sba_ext_dist_init': (C.c_int, [_P, _P]),
-        'acs_sba_ext_dist_phase1': (C.c_int, [_P, _P]),
-        'acs_sba_ext_dist_phase2': (C.c_int, [_P, _P, _P]),
-        'acs_sba_ext_dist_phase3': (C.c_int, [_P, _P, i32, C.POINTER(i32)]),
+        'acs_sba_ext_dist_round': (C.c_int, [_P, _P, _P]),
+        'acs_sba_ext_dist_poll': (C.c_int, [_P, C.c_int64, C.POINTER(i32)]),
         'acs_sba_ext_dist_result': (C.c_int, [_P, _P, _P, C.POINTER(SbaExtReport), u32]),
         'acs_sba_ext_dist_destroy': (C.c_int, [_P]),
         'acs_ekf_run': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, dbl, dbl, dbl, _P, _P, _P, _P, i32,

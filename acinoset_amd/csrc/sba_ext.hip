@@ -39,7 +39,12 @@ struct ExtDims {
 struct ExtState {
   double F, F0, lam, gmax, dnorm, xnorm;
   int cur, status, iters, nacc, relin, pad;
+  // rank round protocol (acs_sba_ext_dist_round): first round pending, a trial awaiting
+  // its decision, the speculative swap of the state for the next system
+  int first, pending, spec_on, save_cur;
+  double save_lam;
 };
+#define EXT_STATUS_SKIP 100  // a rejected round: no step, the system is re-formed only
 
 struct ExtOpts {
   int max_iters;
@@ -713,15 +718,19 @@ __global__ __launch_bounds__(256) void k_ext_pack3(ExtDims d, const ExtState* __
     for (int k = 0; k < 3; ++k) p3[k] = s_red[k][0];
 }
 
-__global__ void k_ext_lm_dist(ExtDims d, ExtState* __restrict__ st, ExtOpts o, int init,
-                              const double* __restrict__ p3, const double* __restrict__ camnorm) {
+// Rank round protocol: the decision on the pending trial from the all-reduced (cost,
+// |dX|^2, |X|^2) of the previous round (k_ext_lm's rule); a rejection marks the round
+// SKIP (no step: the system is re-formed at the current state with the raised damping).
+__global__ void k_ext_decide(ExtDims d, ExtState* __restrict__ st, ExtOpts o, const double* __restrict__ p3,
+                             const double* __restrict__ camnorm) {
   if (threadIdx.x != 0) return;
-  const double f = p3[0];
-  if (init) {
-    st->F = st->F0 = f;
+  if (st->first) {
+    st->first = 0;
+    st->F = st->F0 = p3[0];
     return;
   }
-  if (st->status != 0) return;
+  if (st->status != 0 || !st->pending) return;
+  st->pending = 0;
   double dn = p3[1], xn = p3[2];
   for (int c = 0; c < d.C; ++c) {
     dn += camnorm[2 * c];
@@ -731,6 +740,7 @@ __global__ void k_ext_lm_dist(ExtDims d, ExtState* __restrict__ st, ExtOpts o, i
     st->status = ACS_STATUS_GTOL;
     return;
   }
+  const double f = p3[0];
   st->iters += 1;
   st->dnorm = sqrt(dn);
   st->xnorm = sqrt(xn);
@@ -752,7 +762,37 @@ __global__ void k_ext_lm_dist(ExtDims d, ExtState* __restrict__ st, ExtOpts o, i
     if (st->lam > 1e16) st->status = ACS_STATUS_STALLED;
   }
   if (st->status == 0 && st->iters >= o.max_iters) st->status = ACS_STATUS_MAXITER;
+  if (st->status == 0 && !st->relin) st->status = EXT_STATUS_SKIP;
 }
+
+// Around the system of a round: a round that took a step forms the next system at its trial
+// state (points / cameras copy cur ^ 1) with the damping an acceptance sets (speculation:
+// the next round's decision keeps it or discards it); the LM state is swapped for those
+// kernels and restored after them. A rejected round re-linearises at the current state
+// (the speculative system overwrote its linearisation).
+__global__ void k_ext_spec(ExtState* __restrict__ st, int enter) {
+  if (threadIdx.x != 0) return;
+  if (enter) {
+    if (st->status == EXT_STATUS_SKIP) {
+      st->status = 0;
+      st->relin = 1;
+    } else if (st->status == 0) {
+      st->pending = 1;
+      st->spec_on = 1;
+      st->save_cur = st->cur;
+      st->save_lam = st->lam;
+      st->cur ^= 1;
+      st->lam = fmax(st->lam * 0.1, EXT_LAM_MIN);
+      st->relin = 1;
+    }
+  } else if (st->spec_on) {
+    st->spec_on = 0;
+    st->cur = st->save_cur;
+    st->lam = st->save_lam;
+  }
+}
+
+#define EXT_DIST_RING 4
 
 struct acs_sba_ext_dist {
   acs_ctx* ctx;
@@ -765,6 +805,10 @@ struct acs_sba_ext_dist {
   uint8_t *mk, *cid;
   ExtState* st;
   int* bad;
+  // status after each round: pinned ring with completion events (acs_sba_ext_dist_poll)
+  int32_t* snap = nullptr;
+  hipEvent_t snap_ev[EXT_DIST_RING] = {};
+  int64_t rounds = 0;
 };
 
 template <int G>
@@ -876,10 +920,21 @@ int acs_sba_ext_dist_create(acs_ctx* ctx, const double* cams, int32_t n_cams, co
   std::memset(&st0, 0, sizeof(st0));
   st0.lam = op.lambda0;
   st0.relin = 1;
+  st0.first = 1;
   ACS_HIP(ctx, hipMemcpyAsync(h->st, &st0, sizeof(st0), hipMemcpyHostToDevice, s));
   ACS_HIP(ctx, hipStreamSynchronize(s));
+  bool snap_ok = hipHostMalloc((void**)&h->snap, sizeof(int32_t) * EXT_DIST_RING, hipHostMallocDefault) == hipSuccess;
+  for (auto& e : h->snap_ev)
+    if (snap_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      e = nullptr;
+      snap_ok = false;
+    }
+  if (!snap_ok) {
+    acs_sba_ext_dist_destroy(h);
+    return acs_fail(ctx, ACS_E_HIP, "sba_ext_dist: pinned status ring allocation failed");
+  }
   if (payload_sizes) {
-    payload_sizes[0] = nE + world;
+    payload_sizes[0] = nE + world + 3;  // [reduced camera system | (cost, |dX|^2, |X|^2)]
     payload_sizes[1] = 3;
   }
   *out = h;
@@ -890,24 +945,18 @@ int acs_sba_ext_dist_destroy(acs_sba_ext_dist* h) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   if (!h) return ACS_OK;
   (void)hipStreamSynchronize(h->ctx->stream);
+  for (auto& e : h->snap_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->snap) (void)hipHostFree(h->snap);
   if (h->own) (void)hipFree(h->own);
   delete h;
   return ACS_OK;
 }
 
-int acs_sba_ext_dist_init(acs_sba_ext_dist* h, double* p3) {
-  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
-  hipStream_t s = h->ctx->stream;
-#define EXT_COST0(g) ext_dist_cost<g>(h, s, 0)
-  EXT_G_SWITCH(h->d.G, EXT_COST0)
-#undef EXT_COST0
-  hipLaunchKernelGGL(k_ext_pack3, dim3(1), dim3(256), 0, s, h->d, h->st, 0, h->Fp, h->normp, p3);
-  ACS_HIP(h->ctx, hipGetLastError());
-  return ACS_OK;
-}
+}  // extern "C"
 
-int acs_sba_ext_dist_phase1(acs_sba_ext_dist* h, double* p1) {
-  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
+// the rank's reduced camera system at the current state (payload part 1, zeroed first)
+static int ext_dist_system(acs_sba_ext_dist* h, double* p1) {
   acs_ctx* ctx = h->ctx;
   hipStream_t s = ctx->stream;
   const ExtDims& d = h->d;
@@ -923,8 +972,9 @@ int acs_sba_ext_dist_phase1(acs_sba_ext_dist* h, double* p1) {
   return ACS_OK;
 }
 
-int acs_sba_ext_dist_phase2(acs_sba_ext_dist* h, const double* p1, double* p3) {
-  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
+// solve the summed system p1, step cameras and this rank's points, (cost, |dX|^2, |X|^2) of
+// the trial into p3
+static int ext_dist_step(acs_sba_ext_dist* h, const double* p1, double* p3) {
   acs_ctx* ctx = h->ctx;
   hipStream_t s = ctx->stream;
   const ExtDims& d = h->d;
@@ -944,16 +994,51 @@ int acs_sba_ext_dist_phase2(acs_sba_ext_dist* h, const double* p1, double* p3) {
   return ACS_OK;
 }
 
-int acs_sba_ext_dist_phase3(acs_sba_ext_dist* h, const double* p3, int32_t init, int32_t* status) {
+extern "C" {
+
+// payload [p1 | p3] of the starting state: its system and its cost
+int acs_sba_ext_dist_init(acs_sba_ext_dist* h, double* payload) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
+  hipStream_t s = h->ctx->stream;
+  const int NC = 6 * h->d.C, n1 = NC * NC + 3 * NC + h->R;
+#define EXT_COST0(g) ext_dist_cost<g>(h, s, 0)
+  EXT_G_SWITCH(h->d.G, EXT_COST0)
+#undef EXT_COST0
+  hipLaunchKernelGGL(k_ext_pack3, dim3(1), dim3(256), 0, s, h->d, h->st, 0, h->Fp, h->normp, payload + n1);
+  ACS_HIP(h->ctx, hipGetLastError());
+  return ext_dist_system(h, payload);
+}
+
+// One round: decide on the pending trial (in: all-reduced payload of the previous round),
+// step from its system, and the next system (speculatively at the trial state) with the
+// trial's cost into out - one all-reduce per LM step, the status polled a round late.
+int acs_sba_ext_dist_round(acs_sba_ext_dist* h, const double* in, double* out) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
   hipStream_t s = ctx->stream;
-  hipLaunchKernelGGL(k_ext_lm_dist, dim3(1), dim3(64), 0, s, h->d, h->st, h->o, init, p3, h->camnorm);
+  const int NC = 6 * h->d.C, n1 = NC * NC + 3 * NC + h->R;
+  int rc;
+  hipLaunchKernelGGL(k_ext_decide, dim3(1), dim3(64), 0, s, h->d, h->st, h->o, in + n1, (const double*)h->camnorm);
+  if ((rc = ext_dist_step(h, in, out + n1))) return rc;
+  hipLaunchKernelGGL(k_ext_spec, dim3(1), dim3(64), 0, s, h->st, 1);
+  if ((rc = ext_dist_system(h, out))) return rc;
+  hipLaunchKernelGGL(k_ext_spec, dim3(1), dim3(64), 0, s, h->st, 0);
   ACS_HIP(ctx, hipGetLastError());
-  int32_t stv = 0;
-  ACS_HIP(ctx, hipMemcpyAsync(&stv, &h->st->status, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  ACS_HIP(ctx, hipStreamSynchronize(s));
-  if (status) *status = stv;
+  const int slot = (int)(h->rounds % EXT_DIST_RING);
+  ACS_HIP(ctx, hipMemcpyAsync(h->snap + slot, &h->st->status, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  ACS_HIP(ctx, hipEventRecord(h->snap_ev[slot], s));
+  h->rounds++;
+  return ACS_OK;
+}
+
+// LM status after round r (waits for that round only)
+int acs_sba_ext_dist_poll(acs_sba_ext_dist* h, int64_t round, int32_t* status) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
+  ACS_CHECK(h ? h->ctx : nullptr, h && status && round >= 0 && round < h->rounds && round >= h->rounds - EXT_DIST_RING,
+            "sba_ext_dist_poll: round %lld not among the last %d enqueued", (long long)round, EXT_DIST_RING);
+  const int slot = (int)(round % EXT_DIST_RING);
+  ACS_HIP(h->ctx, hipEventSynchronize(h->snap_ev[slot]));
+  *status = h->snap[slot];
   return ACS_OK;
 }
 

@@ -21,9 +21,11 @@ ranks once, after the last round.
 `lm_loop` is the protocol, independent of the backend: the HIP ranks below, or the numpy
 restatement in oracle/fte_dist.py that the CPU tests plug in.
 
-Points + extrinsics SBA (`lm_loop2`): points are split over the ranks, cameras replicated;
-per LM step the summed reduced camera system (6C x 6C + vectors, 11 KB at C = 6) and the
-summed cost / step norms (3 doubles).
+Points + extrinsics SBA (`lm_loop` too): points are split over the ranks, cameras
+replicated; per LM step ONE all-reduce of one payload: the reduced camera system
+(6C x 6C + vectors, 11 KB at C = 6) formed speculatively at the trial state, and that
+trial's cost / step norms (3 doubles), with the same decide / step / re-form round as the
+frame-window FTE.
 """
 import ctypes as C
 
@@ -50,28 +52,13 @@ def lm_loop(ranks, allreduce):
             if st[0] != 0:
                 break
         k += 1
-    p2 = [r.gather() for r in ranks]
-    allreduce(p2)
-    for r, a in zip(ranks, p2):
-        r.scatter(a)
+    if hasattr(ranks[0], 'gather'):
+        # frame-window FTE: the solution rows of every chain, once
+        p2 = [r.gather() for r in ranks]
+        allreduce(p2)
+        for r, a in zip(ranks, p2):
+            r.scatter(a)
     return st[0]
-
-
-def lm_loop2(ranks, allreduce):
-    """Two-payload variant of lm_loop (points + extrinsics SBA)."""
-    p3 = [r.init() for r in ranks]
-    allreduce(p3)
-    for r, p in zip(ranks, p3):
-        r.phase3(p, init=True)
-    while True:
-        p1 = [r.phase1() for r in ranks]
-        allreduce(p1)
-        p3 = [r.phase2(a) for r, a in zip(ranks, p1)]
-        allreduce(p3)
-        st = [r.phase3(a) for r, a in zip(ranks, p3)]
-        assert len(set(st)) == 1, f'ranks diverged: {st}'
-        if st[0] != 0:
-            return st[0]
 
 
 def _check_dev(torch, dev, device, table, N, Cn, var=False):
@@ -281,29 +268,29 @@ class HipSbaExtRank:
                                                   0), 'acs_sba_ext_dist_create')
         self.h = h
         dev = torch.device('cuda', ctx.device)
-        self.p = [torch.zeros(int(n), dtype=torch.float64, device=dev) for n in sizes]
+        # two round payloads [p1 | p3]: a round reads one and writes the other
+        self.bufs = [torch.zeros(int(sizes[0]), dtype=torch.float64, device=dev) for _ in range(2)]
+        self.k = 0
 
     @staticmethod
     def _ptr(t):
         return C.c_void_p(t.data_ptr())
 
     def init(self):
-        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_init(self.h, self._ptr(self.p[1])), 'acs_sba_ext_dist_init')
-        return self.p[1]
+        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_init(self.h, self._ptr(self.bufs[0])), 'acs_sba_ext_dist_init')
+        self.k = 0
+        return self.bufs[0]
 
-    def phase1(self):
-        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_phase1(self.h, self._ptr(self.p[0])), 'acs_sba_ext_dist_phase1')
-        return self.p[0]
+    def round(self, payload):
+        out = self.bufs[1] if payload.data_ptr() == self.bufs[0].data_ptr() else self.bufs[0]
+        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_round(self.h, self._ptr(payload), self._ptr(out)),
+                       'acs_sba_ext_dist_round')
+        self.k += 1
+        return out
 
-    def phase2(self, p1):
-        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_phase2(self.h, self._ptr(p1), self._ptr(self.p[1])),
-                       'acs_sba_ext_dist_phase2')
-        return self.p[1]
-
-    def phase3(self, p3, init=False):
+    def poll(self, k):
         st = C.c_int32(0)
-        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_phase3(self.h, self._ptr(p3), int(bool(init)), C.byref(st)),
-                       'acs_sba_ext_dist_phase3')
+        self.ctx.check(self.ctx.lib.acs_sba_ext_dist_poll(self.h, int(k), C.byref(st)), 'acs_sba_ext_dist_poll')
         return st.value
 
     def result(self):
@@ -351,7 +338,7 @@ def sba_extrinsics_dist(ctx, cams, uv, pt_idx, cam_idx, pts, opts=None, group=No
         r = HipSbaExtRank(ctx, cams, np.asarray(uv).reshape(-1, 2)[obs], loc, np.asarray(cam_idx)[obs], pts[lo:hi],
                           opts, rank, world)
         try:
-            lm_loop2([r], torch_allreduce(group))
+            lm_loop([r], torch_allreduce(group))
             c, p, rep = r.result()
         finally:
             r.close()
@@ -369,7 +356,7 @@ def sba_extrinsics_virtual(ctx, cams, uv, pt_idx, cam_idx, pts, opts=None, world
         ranks = [HipSbaExtRank(ctx, cams, np.asarray(uv).reshape(-1, 2)[obs], loc, np.asarray(cam_idx)[obs],
                                pts[lo:hi], opts, r, world) for r, (lo, hi, obs, loc) in enumerate(shards)]
         try:
-            lm_loop2(ranks, local_allreduce)
+            lm_loop(ranks, local_allreduce)
             outs = [r.result() for r in ranks]
         finally:
             for r in ranks:

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ACS_ABI_VERSION 3
+#define ACS_ABI_VERSION 4
 #define ACS_CAM_STRIDE 20
 
 /* status codes */
@@ -261,23 +261,25 @@ int acs_sba_extrinsics(acs_ctx* ctx, double* cams, int32_t n_cams, const double*
 
 /* ---- §8(e): points + extrinsics SBA over ranks -------------------------------------
  * Each rank passes its own points and their observations (point indices local to the
- * rank); cameras are replicated. One LM iteration:
- *   phase1(p1) -> all-reduce(p1, sum) -> phase2(p1, p3) -> all-reduce(p3, sum)
- *   -> phase3(p3, 0, &status)
- * starting with init(p3) -> all-reduce(p3) -> phase3(p3, 1, NULL). p1 = the reduced camera
- * system [S (6C x 6C) | b | diag U | g_c] + one |g| slot per rank (payload_sizes[0]
- * doubles), p3 = (cost, |dX|^2, |X|^2) of the rank's points (3 doubles). Device buffers.
- * result() returns the (replicated) cameras and this rank's points.                    */
+ * rank); cameras are replicated. ONE all-reduce per LM step:
+ *   init(P) -> all-reduce(P, sum); then for k = 0, 1, ...:
+ *     round(P, P') -> all-reduce(P', sum); poll(k - 1, &status) until status != 0
+ * P = [p1 | p3] (payload_sizes[0] doubles): p1 = the reduced camera system
+ * [S (6C x 6C) | b | diag U | g_c] + one |g| slot per rank, p3 = (cost, |dX|^2, |X|^2) of the
+ * rank's points at the pending trial. A round decides on the pending trial from p3 (the
+ * rule of acs_sba_extrinsics), steps from p1, and forms the next p1 at the new trial state
+ * with the damping an acceptance sets (a rejected trial costs one extra round that
+ * re-forms the system). poll() waits only for that round (pinned status ring of 4).
+ * Device buffers. result() returns the (replicated) cameras and this rank's points.    */
 typedef struct acs_sba_ext_dist acs_sba_ext_dist;
 int acs_sba_ext_dist_create(acs_ctx* ctx, const double* cams, int32_t n_cams, const double* uv,
                             const int32_t* pt_idx, const int32_t* cam_idx, int64_t n_obs,
                             const double* pts, int64_t n_pts, const acs_sba_ext_opts* opts,
                             int32_t rank, int32_t world, acs_sba_ext_dist** out,
                             int64_t* payload_sizes, uint32_t flags);
-int acs_sba_ext_dist_init(acs_sba_ext_dist* h, double* p3);
-int acs_sba_ext_dist_phase1(acs_sba_ext_dist* h, double* p1);
-int acs_sba_ext_dist_phase2(acs_sba_ext_dist* h, const double* p1, double* p3);
-int acs_sba_ext_dist_phase3(acs_sba_ext_dist* h, const double* p3, int32_t init, int32_t* status);
+int acs_sba_ext_dist_init(acs_sba_ext_dist* h, double* payload);
+int acs_sba_ext_dist_round(acs_sba_ext_dist* h, const double* in, double* out);
+int acs_sba_ext_dist_poll(acs_sba_ext_dist* h, int64_t round, int32_t* status);
 int acs_sba_ext_dist_result(acs_sba_ext_dist* h, double* cams, double* pts, acs_sba_ext_report* report,
                             uint32_t flags);
 int acs_sba_ext_dist_destroy(acs_sba_ext_dist* h);

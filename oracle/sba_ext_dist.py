@@ -12,6 +12,13 @@ their observations, the cameras are replicated.
 * every rank damps S = sum S_r with lam * max(diag U, 1e-12), solves for the camera step,
   steps its own points, and puts (cost, |dX|^2, |X|^2) of its points into payload 3;
 * the accept/reject rule and the damping floor are oracle/sba_ext.py's.
+
+Round protocol (one all-reduce per LM step, acs_sba_ext_dist_round): the payload is
+[p1 | p3]. init() gives the starting state's system and cost; round(P) decides on the
+pending trial from P's p3, steps from P's p1, and returns the next payload: the trial's p3
+and the system at the trial state with the damping an acceptance sets (speculation). A
+rejection skips the step and re-forms the system at the current state (one extra round).
+poll(k) is the status after round k.
 """
 import numpy as np
 
@@ -38,7 +45,44 @@ class OracleSbaExtRank:
         return ose.cost(X, R, t, self.K, self.D, self.uv, self.pi, self.ci, self.f)
 
     def init(self):
-        return np.array([self._cost(self.X, self.R, self.t), 0.0, 0.0])
+        self.first, self.pending, self.rounds = True, False, []
+        p3 = np.array([self._cost(self.X, self.R, self.t), 0.0, 0.0])
+        return np.concatenate([self.phase1(), p3])
+
+    def _decide(self, p3):
+        """k_ext_decide: the pending trial kept or discarded; True = skip this round's step."""
+        if self.first:
+            self.first = False
+            self.F = self.F0 = float(p3[0])
+            return False
+        if self.status or not self.pending:
+            return False
+        self.pending = False
+        self.phase3(p3)
+        return self.status == 0 and not self.relin
+
+    def round(self, P):
+        n1 = len(P) - 3
+        skip = self._decide(P[n1:])
+        out = np.zeros_like(P)
+        if self.status == 0 and not skip:
+            out[n1:] = self.phase2(P[:n1])
+            self.pending = True
+            # the next system at the trial state, with an acceptance's damping
+            keep = (self.X, self.R, self.t, self.lam)
+            self.X, self.R, self.t = self.Xn, self.Rn, self.tn
+            self.lam = max(self.lam * 0.1, ose.LAM_MIN)
+            self.relin = True
+            out[:n1] = self.phase1()
+            self.X, self.R, self.t, self.lam = keep
+        elif self.status == 0:
+            self.relin = True            # the speculative system replaced this state's linearisation
+            out[:n1] = self.phase1()
+        self.rounds.append(self.status)
+        return out
+
+    def poll(self, k):
+        return self.rounds[k]
 
     def phase1(self):
         C, n = self.C, len(self.X)

@@ -1,6 +1,6 @@
 """CPU tests of the multi-GPU protocols (acinoset_amd/dist.py).
 
-The product's LM drivers (`lm_loop` for the frame-window FTE, `lm_loop2` for points +
+The product's LM driver (`lm_loop`, for the frame-window FTE and for points +
 extrinsics SBA) run the oracle restatement of every rank (oracle/fte_dist.py,
 oracle/sba_ext_dist.py) and must reproduce the monolithic oracle solves (oracle/fte.py,
 oracle/sba_ext.py): single-process emulation for several rank counts, and world_size 2
@@ -184,8 +184,17 @@ def test_ext_dist_protocol_matches_monolithic(world):
     g, uv, X, pi, ci = _ext_problem()
     Xm, Rm, tm, im = ose.sba_extrinsics(uv, X, pi, ci, g['K'], g['D'], g['R0'], g['t0'], max_iters=200)
     ranks = _ext_ranks(world)
-    dist.lm_loop2(ranks, dist.local_allreduce)
+    sizes = []
+
+    def counting(payloads):
+        sizes.append(len(payloads[0]))
+        dist.local_allreduce(payloads)
+    dist.lm_loop(ranks, counting)
     outs = [r.result() for r in ranks]
+    # one all-reduce per LM step: init, one round per step (+1 per rejected step), and the
+    # round queued before the stop was read
+    n_rej = outs[0][3]['iters'] - outs[0][3]['n_accepted']
+    assert len(sizes) - 1 == outs[0][3]['iters'] + n_rej + 2, (len(sizes), outs[0][3])
     for o in outs[1:]:
         assert np.array_equal(o[0], outs[0][0]) and np.array_equal(o[1], outs[0][1])
     R, t, _, info = outs[0]
@@ -206,7 +215,7 @@ def _gloo_ext_worker(rank, world, port, out_dir):
     try:
         r = _ext_ranks(world)[rank]
         allreduce = dist.torch_allreduce()
-        dist.lm_loop2([r], lambda ps: allreduce([torch.from_numpy(ps[0])]))
+        dist.lm_loop([r], lambda ps: allreduce([torch.from_numpy(ps[0])]))
         R, t, X, info = r.result()
         np.savez(os.path.join(out_dir, f'ext{rank}.npz'), R=R, t=t, X=X, iters=info['iters'])
     finally:

@@ -16,7 +16,7 @@ def _header_functions():
 def test_library_loads_and_exports_header_symbols():
     from acinoset_amd import _native
     lib = _native.load_library()
-    assert lib.acs_abi_version() == _native.ABI_VERSION == 3
+    assert lib.acs_abi_version() == _native.ABI_VERSION == 4
     nm = subprocess.run(['nm', '-D', '--defined-only', _native.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r'\b(acs_[a-z0-9_]+)\b', nm))
     missing = [f for f in _header_functions() if f not in exported]
