@@ -1,16 +1,43 @@
-import sys, ctypes as C, numpy as np, importlib, torch
-sys.path.insert(0, '.')
-from acinoset_amd import _native, synth, kinematics as pkin
+"""Per-phase cycle counts of k_ekf_filter from a library built with -DEKF_PROFILE (the same
+libprof.so as tools/prof_fte_phases.py, with ekf.hip compiled with -DEKF_PROFILE):
+python tools/prof_ekf_phases.py [mode] [n_cams] [frames]   (default: default 6 200)."""
+import ctypes as C
+import importlib
+import os
+import sys
+
+os.environ['ACINOSET_HIP_LIB'] = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'acinoset_amd',
+                                              'csrc', 'build', 'libprof.so')
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from acinoset_amd import _native, synth, kinematics as pkin  # noqa: E402
+
 cekf = importlib.import_module('acinoset_amd.core.ekf')
+mode = sys.argv[1] if len(sys.argv) > 1 else 'default'
+n_cams = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+N = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 ctx = _native.Context(0)
 buf = torch.zeros(8, dtype=torch.int64, device='cuda')
 ctx.lib.acs_ekf_prof.argtypes = [C.c_void_p]
 ctx.lib.acs_ekf_prof(C.c_void_p(buf.data_ptr()))
-mode, N = 'default', 200
-scene = synth.load_scene_file(); seq = synth.make_sequence(N, scene, mode=mode, seed=5)
-table = pkin.build_table(mode); cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t); P = table.P
-s0 = np.zeros(3 * P); s0[:3] = seq.pos3d[0, 0, 0]
-ctx.ekf_run(table, cams, seq.uv, seq.likelihood, 90.0, 0.5, 2704.0, cekf.measurement_std(6), cekf.process_covariance(P, 1/90.), cekf.initial_covariance(mode), s0)
+scene = synth.load_scene_file() if n_cams == 6 else synth.ring_scene(n_cams)
+seq = synth.make_sequence(N, scene, mode='default_nolure', seed=5)
+table = pkin.build_table(mode)
+markers = pkin.get_markers(mode)
+cols = [seq.markers.index(m) for m in markers]
+cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+P = table.P
+covs = cekf.ring_cal_covs(n_cams)
+s0 = np.zeros(3 * P)
+s0[:3] = seq.pos3d[0, 0, :3]
+ctx.ekf_run(table, cams, np.ascontiguousarray(seq.uv[:, :, cols]), np.ascontiguousarray(seq.likelihood[:, :, cols]),
+            90.0, 0.5, float(scene.res[0]), cekf.measurement_std(n_cams, covs), cekf.process_covariance(P, 1 / 90.),
+            cekf.initial_covariance(mode), s0)
 v = buf.cpu().numpy() / N
 names = ["predict+PFPt", "FK/proj", "H build", "A,G,b,outl", "aug", "GJ", "update", "store+FK-only"]
-for nm, x in zip(names, v): print(f'{nm:12s} {x:10.0f} cycles/frame  ({x/2.4e3:.1f} us @2.4GHz)')
+print(f'{mode}, {n_cams} cams, {N} frames, one sequence')
+for nm, x in zip(names, v):
+    print(f'{nm:14s} {x:10.0f} cycles/frame  ({x / 2.4e3:.1f} us @2.4GHz)')
+print(f'{"total":14s} {v.sum():10.0f} cycles/frame  ({v.sum() / 2.4e3:.1f} us @2.4GHz)')
