@@ -26,8 +26,6 @@ enum WsSlot {
   WS_PIPE0, WS_PIPE1, WS_PIPE2, WS_PIPE3, WS_PIPE4, WS_PIPE5, WS_PIPE6, WS_PIPE7,
   WS_NSLOTS
 };
-enum GraphSlot { GRAPH_FTE = 0, GRAPH_NSLOTS };
-
 struct acs_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -36,30 +34,15 @@ struct acs_ctx {
   void* ws[WS_NSLOTS] = {};
   size_t ws_bytes[WS_NSLOTS] = {};
   int n_cu = 256;
-  // Instantiated hipGraphs kept across calls: `key` holds every value their kernels
-  // captured (dimensions, buffer pointers, options, stream), so a call with the same key
-  // replays the graph instead of capturing and instantiating it again.
-  struct GraphCache {
-    hipGraphExec_t exec = nullptr;
-    std::string key;
-  };
-  GraphCache graphs[GRAPH_NSLOTS];
-  // pinned host slots for asynchronous device-state snapshots and their completion events
-  // (the FTE solve reads the LM status of iteration n while iteration n + 1 runs)
+  // pinned (coherent) host slots the kernels write device-state snapshots into (the FTE
+  // solve reads the LM status of iteration n while iteration n + 1 runs)
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
-  hipEvent_t snap_ev[2] = {};
 };
 
-// Pinned host buffer of at least `bytes` (grow-only) and the two snapshot events.
+// Coherent pinned host buffer of at least `bytes` (grow-only).
 // Returns nullptr (and sets the error) on failure.
 void* acs_pinned(acs_ctx* ctx, size_t bytes);
-
-// append the bytes of a trivially copyable value to a graph-cache key
-template <typename T>
-inline void key_put(std::string& k, const T& v) {
-  k.append(reinterpret_cast<const char*>(&v), sizeof(T));
-}
 
 int acs_fail(acs_ctx* ctx, int code, const char* fmt, ...);
 

@@ -35,16 +35,6 @@ void* acs_ws(acs_ctx* ctx, int slot, size_t bytes) {
 }
 
 void* acs_pinned(acs_ctx* ctx, size_t bytes) {
-  // every snapshot event is checked on its own: a partial failure on an earlier call
-  // leaves the missing ones null and they are created here on the next call
-  for (auto& e : ctx->snap_ev) {
-    if (e) continue;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      e = nullptr;
-      acs_fail(ctx, ACS_E_HIP, "hipEventCreateWithFlags failed");
-      return nullptr;
-    }
-  }
   if (ctx->pinned_bytes >= bytes) return ctx->pinned;
   if (ctx->pinned) {
     (void)hipStreamSynchronize(ctx->stream);
@@ -131,13 +121,9 @@ int acs_ctx_destroy(acs_ctx* ctx) {
   if (!ctx) return ACS_OK;
   ACS_DEVICE_GUARD(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  for (auto& g : ctx->graphs)
-    if (g.exec) (void)hipGraphExecDestroy(g.exec);
   for (int i = 0; i < WS_NSLOTS; ++i)
     if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
-  for (auto& e : ctx->snap_ev)
-    if (e) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
   return ACS_OK;

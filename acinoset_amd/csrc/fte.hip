@@ -8,21 +8,21 @@
 // (:492-510) is  sum rho(w * (proj(FK(x_n) + shift) - meas)) + sum (Delta^3 x / Ts^2)^2 / Q.
 // It is minimised by Levenberg-Marquardt with the spec in oracle/fte.py.
 //
-// One LM iteration (captured into a hipGraph, 4 iterations per graph, no host round trip):
-//   k_fte_linearize  [N blocks]  FK + analytic FK Jacobian (fk.hpp), fisheye projection
-//                                and its Jacobian, loss derivatives, per-frame local
-//                                Jacobian rows (2CL x NZ) in LDS and the per-frame normal
-//                                block J^T W J via v_mfma_f64_16x16x4f64, gradient, cost
-//   k_fte_assemble   [M blocks]  block-banded (bandwidth 3) normal matrix + tau border
-//                                + exact model term (third differences)
-//   k_cr_build       [n blocks]  3-frame super-blocks (block tridiagonal) + LM damping
+// One LM iteration (one hipGraph replay, the next one queued behind it; the host polls a
+// pinned status word one iteration late, fte_snapshot / fte_wait_snapshot):
+//   k_cr_assemble_build [n blocks]  block-banded normal matrix (bandwidth 3) + tau border +
+//                                exact model term, gathered into 3-frame super-blocks (block
+//                                tridiagonal) + LM damping
 //   k_cr_level       [log2 n levels]  block cyclic reduction, one launch per level:
 //                                register-tiled Gauss-Jordan on [D | couplings | rhs] and the
 //                                neighbours' Schur terms, all on f64 MFMA tiles
-//   k_cr_top         [1 block ]  last block + tau border
-//   k_cr_back        [log2 n levels]  back substitution
-//   k_cr_trial       [n blocks]  trial state X + delta, tau clipped to [-Ts, Ts]
-//   k_fte_cost       [N blocks]  exact objective at the trial state (per-frame partials)
+//   k_cr_tau_partial, k_cr_top [1 block]  last block + tau border, block 0's trial rows
+//   k_cr_back_all    [n - 1 blocks]  every back-substitution level in one launch (ticket-
+//                                ordered workgroups, granule hand-offs) + the trial state
+//   k_fte_linearize  [N blocks]  at the trial state, speculatively: FK + analytic FK
+//                                Jacobian (fk.hpp), fisheye projection and its Jacobian, loss
+//                                derivatives, per-frame J^T W J on v_mfma_f64_16x16x4f64,
+//                                gradient and the exact objective (per-frame partials)
 //   k_fte_lm         [1 block ]  fixed-order reduction, accept/reject, lambda, stop tests
 #include <climits>
 
@@ -2022,13 +2022,27 @@ __global__ __launch_bounds__(64) void k_fte_cost(FteDims d, const int* __restric
 // 7. LM control
 // ---------------------------------------------------------------------------------------
 // Every non-init launch ends by writing the LM state into host snapshot slot (launch & 1)
-// (`snap`: pinned host memory; the host waits on an event recorded after the iteration and
-// reads it there, with no copy node in the iteration).
+// of `snap` (coherent pinned host memory, acs_pinned) and then the iteration count into the
+// word after the two slots, which the host polls: the state goes out as system-scope
+// (write-through) stores, and the count only after they have all completed, so a host that
+// sees count n reads iteration n's state. No event between iterations: an event record
+// between two graph launches cost ~13 us of idle GPU per iteration (a system-scope
+// release behind the whole iteration), the poll costs nothing on the device.
 __device__ __forceinline__ void fte_snapshot(FteState* st, FteState* snap) {
   if (!snap) return;
-  const int slot = st->launch & 1;
-  st->launch += 1;
-  snap[slot] = *st;  // coherent host memory (acs_pinned): visible once the iteration's event completes
+  const int slot = st->launch & 1, seq = st->launch + 1;
+  st->launch = seq;
+  static_assert(sizeof(FteState) % 8 == 0, "FteState is copied in 8-byte words");
+  constexpr int NW = (int)(sizeof(FteState) / 8);
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(st);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(snap + slot);
+  unsigned long long v[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) v[i] = src[i];  // all loads before the first store
+#pragma unroll
+  for (int i = 0; i < NW; ++i) __hip_atomic_store(dst + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(reinterpret_cast<int*>(snap + 2), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict__ st, FteOptsDev o, int init,
@@ -2841,6 +2855,26 @@ static const double* dist_local_cr(acs_fte_dist* h) {
   return cr_reduce(d, h->ctx->stream, b.st, b, h->a0, std::min(h->bend, d.nblk), top, h->klev, b.bad);
 }
 
+// Wait until the solve loop's iteration count in the pinned word after the two snapshot
+// slots (fte_snapshot) reaches `want`. The stream is queried now and then, so a failed or
+// drained stream ends the wait with an error instead of a hang.
+static int fte_wait_snapshot(acs_ctx* ctx, hipStream_t s, FteState* snap, int want) {
+  const int* seqw = reinterpret_cast<const int*>(snap + 2);
+  for (unsigned it = 1;; ++it) {
+    if (__atomic_load_n(seqw, __ATOMIC_ACQUIRE) >= want) return ACS_OK;
+    if ((it & 4095) == 0) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) {  // everything queued has finished: the count is final
+        if (__atomic_load_n(seqw, __ATOMIC_ACQUIRE) >= want) return ACS_OK;
+        return acs_fail(ctx, ACS_E_HIP, "fte: stream idle at iteration count %d, expected %d",
+                        __atomic_load_n(seqw, __ATOMIC_ACQUIRE), want);
+      }
+      if (q != hipErrorNotReady) return acs_fail(ctx, ACS_E_HIP, "fte: %s", hipGetErrorString(q));
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 extern "C" {
 
 void acs_fte_default_opts(acs_fte_opts* o) {
@@ -2886,80 +2920,39 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
     hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
                        b.X, b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr, b.Tc);
   ACS_HIP(ctx, hipGetLastError());
-  // capture one iteration into a hipGraph (kernels read the LM state from device memory,
-  // so the graph is static) and replay it until the device reports a stop status, one
-  // iteration queued ahead: the host reads iteration n's status snapshot (pinned slot n & 1)
-  // while iteration n + 1 runs, so the GPU never waits for the host, and a stop costs one
-  // early-exiting iteration (was: chunks of 4 behind a full synchronisation, up to 3). The
-  // instantiated graph stays in the context for the next solve with the same key.
-  const int chunk = 1;
+  // enqueue the iterations one ahead of the host: the host reads iteration n's status
+  // snapshot (pinned slot n & 1, published with its iteration count, fte_snapshot) while
+  // iteration n + 1 runs, so the GPU never waits for the host, and a stop costs one
+  // early-exiting iteration. Plain stream launches (~16 per iteration, ~56 us of host time
+  // against >= ~100 us of GPU time): a hipGraph replay per iteration left ~9-13 us of idle
+  // GPU between replays, 2 % of the 1000-frame solve (profiles/r03/fte_launch_ab.log).
   FteState* snap = nullptr;
   if (op.max_iters > 0) {
-    snap = (FteState*)acs_pinned(ctx, 2 * sizeof(FteState));
+    snap = (FteState*)acs_pinned(ctx, 3 * sizeof(FteState));
     if (!snap) return ACS_E_NOMEM;
-    std::memset(snap, 0, 2 * sizeof(FteState));
+    std::memset(snap, 0, 3 * sizeof(FteState));
   }
   S.snap = snap;
-  std::string key;
-  key_put(key, snap);
-  key_put(key, d);
-  key_put(key, b);
-  key_put(key, o.max_iters);
-  key_put(key, o.ftol);
-  key_put(key, o.xtol);
-  key_put(key, o.gtol);
-  key_put(key, s);
-  key_put(key, chunk);
-  acs_ctx::GraphCache& gc = ctx->graphs[GRAPH_FTE];
-  hipGraphExec_t exec = nullptr;
-  bool use_graph = op.max_iters > 0;
-  if (use_graph && gc.exec && gc.key == key) {
-    exec = gc.exec;
-  } else if (use_graph) {
-    if (gc.exec) (void)hipGraphExecDestroy(gc.exec);
-    gc.exec = nullptr;
-    gc.key.clear();
-    hipGraph_t graph = nullptr;
-    if (hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) != hipSuccess) use_graph = false;
-    if (use_graph) {
-      for (int c = 0; c < chunk; ++c) fte_enqueue_iteration(S, s, o);
-      if (hipStreamEndCapture(s, &graph) != hipSuccess ||
-          hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        exec = nullptr;
-        use_graph = false;
-      }
-      if (graph) (void)hipGraphDestroy(graph);
-    }
-    if (exec) {
-      gc.exec = exec;
-      gc.key = key;
-    }
-  }
   FteState hs;
   std::memset(&hs, 0, sizeof(hs));
   if (op.max_iters > 0) {
     // max_iters + 1 launches at most: the kernel sets MAXITER in iteration max_iters
     const int nmax = op.max_iters + 1;
-    int last = 0;
+    int last = 0, rc_wait;
     for (int n = 0;; ++n) {
       if (n < nmax) {
-        if (use_graph)
-          ACS_HIP(ctx, hipGraphLaunch(exec, s));
-        else
-          fte_enqueue_iteration(S, s, o);
+        fte_enqueue_iteration(S, s, o);
         ACS_HIP(ctx, hipGetLastError());
-        // k_fte_lm of iteration n wrote its state into snap[n & 1]
-        ACS_HIP(ctx, hipEventRecord(ctx->snap_ev[n & 1], s));
         last = n;
       }
       if (n >= 1) {
-        ACS_HIP(ctx, hipEventSynchronize(ctx->snap_ev[(n - 1) & 1]));
+        // k_fte_lm of iteration n - 1 wrote its state into snap[(n - 1) & 1], then count n
+        if ((rc_wait = fte_wait_snapshot(ctx, s, snap, n))) return rc_wait;
         if (snap[(n - 1) & 1].status != 0 || n >= nmax) break;
       }
     }
     // the last queued iteration exits early on a stop status (the state is unchanged)
-    ACS_HIP(ctx, hipEventSynchronize(ctx->snap_ev[last & 1]));
+    if ((rc_wait = fte_wait_snapshot(ctx, s, snap, last + 1))) return rc_wait;
     hs = snap[last & 1];
   } else {
     ACS_HIP(ctx, hipMemcpyAsync(&hs, b.st, sizeof(hs), hipMemcpyDeviceToHost, s));

@@ -23,16 +23,15 @@ buf = torch.zeros(8, dtype=torch.int64, device='cuda')
 ctx.lib.acs_ekf_prof.argtypes = [C.c_void_p]
 ctx.lib.acs_ekf_prof(C.c_void_p(buf.data_ptr()))
 scene = synth.load_scene_file() if n_cams == 6 else synth.ring_scene(n_cams)
-seq = synth.make_sequence(N, scene, mode='default_nolure', seed=5)
+seq = synth.make_sequence(N, scene, mode=mode, seed=5)     # as bench.py's EKF leg
 table = pkin.build_table(mode)
-markers = pkin.get_markers(mode)
-cols = [seq.markers.index(m) for m in markers]
 cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
 P = table.P
 covs = cekf.ring_cal_covs(n_cams)
-s0 = np.zeros(3 * P)
-s0[:3] = seq.pos3d[0, 0, :3]
-ctx.ekf_run(table, cams, np.ascontiguousarray(seq.uv[:, :, cols]), np.ascontiguousarray(seq.likelihood[:, :, cols]),
+s0 = np.zeros((1, 3 * P))
+s0[0, :P] = seq.x[0]
+s0[0, P:2 * P] = (seq.x[1] - seq.x[0]) / seq.Ts
+ctx.ekf_run(table, cams, seq.uv[None], seq.likelihood[None],
             90.0, 0.5, float(scene.res[0]), cekf.measurement_std(n_cams, covs), cekf.process_covariance(P, 1 / 90.),
             cekf.initial_covariance(mode), s0)
 v = buf.cpu().numpy() / N
