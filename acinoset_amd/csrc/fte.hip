@@ -1514,21 +1514,20 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 // order by k_cr_top): per-frame tau blocks of the normal matrix / gradient, and the tau
 // Schur contributions of every eliminated super-block.
 #define CR_NCHUNK 64
-__global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteState* __restrict__ st,
-                                                        const double* __restrict__ Hloc,
-                                                        const double* __restrict__ gloc,
-                                                        const double* __restrict__ Tau, double* __restrict__ part,
-                                                        int k_lo, int k_hi, int b_lo, int b_hi, int hsel,
-                                                        const double* __restrict__ Tc) {
+// chunk `ch` of the partial sums; `store(e, v)` writes element e of the chunk's row of `part`
+template <typename Store>
+__device__ __forceinline__ void cr_tau_partial_chunk(const FteDims& d, const FteState* __restrict__ st,
+                                                     const double* __restrict__ Hloc, const double* __restrict__ gloc,
+                                                     const double* __restrict__ Tau, int k_lo, int k_hi, int b_lo,
+                                                     int b_hi, int hsel, const double* __restrict__ Tc, int ch,
+                                                     Store store) {
   // frames [k_lo, k_hi) (tau blocks of their normal matrices / gradients) and eliminated
   // super-blocks [b_lo, b_hi) (tau Schur terms), each range cut into CR_NCHUNK chunks
-  if (st->status != 0) return;
   if (hsel) {
     Hloc += (size_t)st->cur * d.N * FTE_NZP * FTE_NZP;
     gloc += (size_t)st->cur * d.N * FTE_NZP;
     if (Tc) Tc += (size_t)st->cur * d.N * tc_stride(d.Cg);
   }
-  const int ch = blockIdx.x;
   const int P = d.P, Cg = d.Cg, GR = d.GR;
   const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
   const int nf = max(0, k_hi - k_lo), nb = max(0, b_hi - b_lo);
@@ -1560,8 +1559,20 @@ __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteStat
     } else {
       v = sum8(Tau + (e - nH - Cg), (size_t)GR * GR, b0, b1);
     }
-    part[(size_t)ch * nE + e] = v;
+    store(e, v);
   }
+}
+
+__global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteState* __restrict__ st,
+                                                        const double* __restrict__ Hloc,
+                                                        const double* __restrict__ gloc,
+                                                        const double* __restrict__ Tau, double* __restrict__ part,
+                                                        int k_lo, int k_hi, int b_lo, int b_hi, int hsel,
+                                                        const double* __restrict__ Tc) {
+  if (st->status != 0) return;
+  const int ch = blockIdx.x, nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
+  cr_tau_partial_chunk(d, st, Hloc, gloc, Tau, k_lo, k_hi, b_lo, b_hi, hsel, Tc, ch,
+                       [&](int e, double v) { part[(size_t)ch * nE + e] = v; });
 }
 
 // Trial state of super-block i (frames 3i..3i+2: X[cur ^ 1] = X[cur] + dv) and the
@@ -1608,15 +1619,17 @@ __device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* 
   }
 }
 
-__global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ W0,
-                                                const double* __restrict__ part, const double* __restrict__ gmaxp,
-                                                double* __restrict__ taubuf, double* __restrict__ dcv,
-                                                double* __restrict__ dtau, int* __restrict__ bad,
-                                                double* __restrict__ Xbuf = nullptr,
-                                                double* __restrict__ normp = nullptr) {
+// k_cr_top's work (blockDim 1024, every thread): `loadp(i)` reads element i of the chunk
+// partials, `pub_tau(c, v)` (c < 32) and `pub_row(r, v)` (r < BP) hand dtau and block 0's
+// step on to the back substitution (besides the plain dtau / dcv stores)
+template <typename LoadPart, typename PubTau, typename PubRow>
+__device__ __forceinline__ void cr_top_body(const FteDims& d, FteState* __restrict__ st, const double* __restrict__ W0,
+                                            const double* __restrict__ gmaxp, double* __restrict__ taubuf,
+                                            double* __restrict__ dcv, double* __restrict__ dtau, int* __restrict__ bad,
+                                            double* __restrict__ Xbuf, double* __restrict__ normp, LoadPart loadp,
+                                            PubTau pub_tau, PubRow pub_row) {
   // block 0 has been eliminated by k_cr_level (top_mode): W0 = its W (BP x WL), its tau Schur
   // term is in the Tau sums like every other block's
-  if (st->status != 0) return;
   const int tid = threadIdx.x, nth = blockDim.x;
   const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
   const double lam = st->lam;
@@ -1636,7 +1649,7 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
     for (int c0 = 0; c0 < CR_NCHUNK; c0 += 16) {
       double pv[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) pv[q] = part[(size_t)(c0 + q) * nE + e];
+      for (int q = 0; q < 16; ++q) pv[q] = loadp((size_t)(c0 + q) * nE + e);
 #pragma unroll
       for (int q = 0; q < 16; ++q) v += pv[q];
     }
@@ -1684,27 +1697,43 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
       double v = 0.0;
       for (int c = 0; c < GR; ++c) v += sS[tid * GR + c] * sr[c];
       dtau[tid] = (tid < Cg && !s_held[tid]) ? v : 0.0;
+      if (tid < 32) pub_tau(tid, (tid < Cg && !s_held[tid]) ? v : 0.0);
     }
     __syncthreads();
   }
+  if (tid < 32 && (!Cg || tid >= GR)) pub_tau(tid, 0.0);
   double v0 = 0.0;  // row tid of block 0's step (nth = 1024 > BP)
   if (tid < BP) {
     const double* w = W0 + (size_t)tid * WL + 2 * BP;
     double v = w[Cg];
     for (int c = 0; c < Cg; ++c) v -= w[c] * dtau[c];
     dcv[tid] = v;
+    pub_row(tid, v);
     v0 = v;
   }
   // the single-GPU solve steps block 0 (and the constant delays) here: no k_cr_trial launch
   if (Xbuf) cr_trial_rows(d, st, 0, v0, xpre, dtau, Xbuf, taubuf, normp, d.Cg != 0, s_red);
 }
 
+__global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ W0,
+                                                const double* __restrict__ part, const double* __restrict__ gmaxp,
+                                                double* __restrict__ taubuf, double* __restrict__ dcv,
+                                                double* __restrict__ dtau, int* __restrict__ bad,
+                                                double* __restrict__ Xbuf = nullptr,
+                                                double* __restrict__ normp = nullptr) {
+  if (st->status != 0) return;
+  cr_top_body(
+      d, st, W0, gmaxp, taubuf, dcv, dtau, bad, Xbuf, normp, [&](size_t i) { return part[i]; },
+      [](int, double) {}, [](int, double) {});
+}
+
 // back substitution of eliminated block i at level s (blockDim 1024; every thread calls it).
 // `fetch(l, r)` runs after the W loads are issued and fills sl / sr_ (threads < BP) with the
-// survivors' rows; `publish(row, value)` stores one row of the block's step.
+// survivors' rows and st_ (threads < 32) with dtau (zero past Cg); `publish(row, value)`
+// stores one row of the block's step.
 template <typename Fetch, typename Publish>
 __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, int bend, const double* __restrict__ Wc,
-                                              const double* __restrict__ dtau, double* sl, double* sr_, double* st_,
+                                              double* sl, double* sr_, double* st_,
                                               Fetch fetch, Publish publish) {
   const int l = i - s, r = (i + s <= bend && i + s < d.nblk) ? i + s : -1;
   const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
@@ -1730,7 +1759,6 @@ __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, in
   }
   const double rhs = live ? w[2 * BP + Cg] : 0.0;
   fetch(l, r);
-  if (tid < 32) st_[tid] = tid < Cg ? dtau[tid] : 0.0;
   __syncthreads();
   double v = 0.0;
 #pragma unroll
@@ -1755,46 +1783,101 @@ __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int 
   __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32];
   const int i = a0 + s * (2 * blockIdx.x + 1), BP = d.BP;
   cr_back_block(
-      d, i, s, bend, Wc, dtau, sl, sr_, st_,
+      d, i, s, bend, Wc, sl, sr_, st_,
       [&](int l, int r) {
         if ((int)threadIdx.x < BP) {
           sl[threadIdx.x] = dcv[(size_t)l * BP + threadIdx.x];
           sr_[threadIdx.x] = r >= 0 ? dcv[(size_t)r * BP + threadIdx.x] : 0.0;
         }
+        if (threadIdx.x < 32) st_[threadIdx.x] = (int)threadIdx.x < d.Cg ? dtau[threadIdx.x] : 0.0;
       },
       [&](int row, double v) { dcv[(size_t)i * BP + row] = v; });
 }
 
-// Every back-substitution level of the single-GPU solve in one launch (nblk - 1
-// workgroups, one per eliminated block; block 0 is k_cr_top's). A workgroup takes a ticket
-// at entry; tickets are dealt coarse level first, so a block only ever waits for blocks of
-// lower tickets, whose workgroups have already started: the grid drains whatever the
-// residency (one 1024-thread workgroup per CU). Each workgroup issues its W loads (no
-// dependency) and then waits for the rows of its two survivors, so the levels chain through
-// memory instead of kernel boundaries. Hand-off: the data is the flag
-// (cdna_hip_programming.md §6 Guideline 16, R2; MI355X_MICROARCH.md handoff-1to1): every
-// row goes out as two 8-byte granules {stamp, high word} {stamp, low word}, each ONE
-// relaxed agent-scope store (sc1, written through), and each consumer thread re-reads its
-// survivors' granules with sc1 loads until all carry this launch's stamp - no flag, no
-// drain, no fence, one memory round trip per level. Stamps count launches
-// (ticket / (nblk - 1) + 1; `bk[0]` the ticket counter, the granules `gdcv`, both zeroed by
-// fte_setup). The plain dcv rows are written too (k_cr_trial of the per-frame-delay mode
-// reads them). A spin that outlives ~0.3 s gives up and counts into *bad (the solve then
-// reports a failed factorisation instead of hanging).
-__global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, const FteState* __restrict__ st,
-                                                      const double* __restrict__ Wc, const double* __restrict__ dtau,
-                                                      double* __restrict__ dcv, int* __restrict__ bk,
-                                                      unsigned long long* __restrict__ gdcv, int* __restrict__ bad,
-                                                      double* __restrict__ Xbuf, double* __restrict__ normp) {
+// The end of the single-GPU solve's reduction in one launch: the tau partial sums
+// (k_cr_tau_partial, CR_NCHUNK workgroups), the top block with the tau border (k_cr_top, one
+// workgroup) and every back-substitution level (nblk - 1 workgroups, one per eliminated
+// block). A workgroup takes a ticket at entry; tickets are dealt partials first, then the
+// top, then the back blocks coarse level first, so a workgroup only ever waits for
+// workgroups of lower tickets, which have already started: the grid drains whatever the
+// residency (one 1024-thread workgroup per CU). Hand-offs (MI355X_MICROARCH.md, inter-
+// workgroup visibility, first table row / handoff-1to1):
+//  - partials -> top: every element stored with a relaxed agent-scope store (sc1, written
+//    through), every wave's vmcnt(0), a barrier, then one agent-scope add to the counter
+//    bk[1]; the top polls the counter with sc1 loads until it holds CR_NCHUNK x stamp, and
+//    reads the partials with sc1 loads only;
+//  - top / back blocks -> back blocks: the data is the flag (cdna_hip_programming.md §6
+//    Guideline 16, R2): every row of a step and every dtau entry goes out as two 8-byte
+//    granules {stamp, high word} {stamp, low word}, each ONE sc1 store, and each consumer
+//    thread re-reads its granules with sc1 loads until all carry this launch's stamp.
+// Stamps count launches (ticket / nwork + 1; bk[0] the ticket counter, the granules `gdcv`
+// (rows, then 32 x 2 for dtau), all zeroed by fte_setup). The plain dcv / dtau are written
+// too (k_cr_trial of the per-frame-delay mode reads them). A spin that outlives ~0.3 s gives
+// up and counts into *bad (the solve then reports a failed factorisation, not a hang).
+// Folding the partials and the top into this launch removed two kernel boundaries (r03).
+__device__ __forceinline__ void cr_publish_granules(unsigned long long* g, unsigned long long stamp, double v) {
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+  __hip_atomic_store(g, (stamp << 32) | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g + 1, (stamp << 32) | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, FteState* __restrict__ st,
+                                                      const double* __restrict__ Wc, const double* __restrict__ Hloc,
+                                                      const double* __restrict__ gloc, const double* __restrict__ Tau,
+                                                      const double* __restrict__ Tc, double* __restrict__ part,
+                                                      const double* __restrict__ gmaxp, double* __restrict__ taubuf,
+                                                      double* __restrict__ dtau, double* __restrict__ dcv,
+                                                      int* __restrict__ bk, unsigned long long* __restrict__ gdcv,
+                                                      int* __restrict__ bad, double* __restrict__ Xbuf,
+                                                      double* __restrict__ normp) {
   __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32], sdv[CR_MAXBP], s_red[1024];
   __shared__ int s_tk;
-  const int nwork = d.nblk - 1;
+  const int nwork = CR_NCHUNK + d.nblk;  // partials, top, nblk - 1 back blocks
   if (threadIdx.x == 0) s_tk = atomicAdd(bk, 1);
   __syncthreads();
   const unsigned tk = (unsigned)s_tk;
   if (st->status != 0) return;
   const unsigned long long stamp = tk / (unsigned)nwork + 1u;
-  int w = (int)(tk % (unsigned)nwork), s = 1, i = 1;
+  int w = (int)(tk % (unsigned)nwork);
+  const int BP = d.BP;
+  unsigned long long* gtau = gdcv + (size_t)d.nblk * BP * 2;
+  unsigned long long* partw = reinterpret_cast<unsigned long long*>(part);
+  if (w < CR_NCHUNK) {
+    const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
+    cr_tau_partial_chunk(d, st, Hloc, gloc, Tau, 0, d.N, 0, d.nblk, 1, Tc, w, [&](int e, double v) {
+      __hip_atomic_store(partw + (size_t)w * nE + e, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(bk + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (w == CR_NCHUNK) {
+    if (threadIdx.x == 0) {
+      const int want = CR_NCHUNK * (int)stamp;
+      const unsigned long long t0 = wall_clock64();
+      while (__hip_atomic_load(bk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        if (wall_clock64() - t0 > 30000000ull) {
+          atomicAdd(bad, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    cr_top_body(
+        d, st, Wc, gmaxp, taubuf, dcv, dtau, bad, Xbuf, normp,
+        [&](size_t e) {
+          return __longlong_as_double(
+              (long long)__hip_atomic_load(partw + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        },
+        [&](int c, double v) { cr_publish_granules(gtau + 2 * c, stamp, v); },
+        [&](int r, double v) { cr_publish_granules(gdcv + 2 * r, stamp, v); });
+    return;
+  }
+  w -= CR_NCHUNK + 1;
+  int s = 1, i = 1;
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
     const int sv = 1 << lv, ne = (d.nblk - sv + 2 * sv - 1) / (2 * sv);
     if (w < ne) {
@@ -1804,19 +1887,18 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, const
     }
     w -= ne;
   }
-  const int BP = d.BP;
   const double xpre = cr_trial_x(d, st, i, Xbuf);
   cr_back_block(
-      d, i, s, bend, Wc, dtau, sl, sr_, st_,
+      d, i, s, bend, Wc, sl, sr_, st_,
       [&](int l, int r) {
         const int t = threadIdx.x;
-        if (t >= BP) return;
-        if (l == 0) sl[t] = dcv[t];  // block 0: k_cr_top, an earlier launch
-        const unsigned long long* gl = gdcv + ((size_t)l * BP + t) * 2;
-        const unsigned long long* gr = gdcv + ((size_t)(r > 0 ? r : l) * BP + t) * 2;
-        const bool wl = l > 0, wr = r > 0;
+        if (t >= BP && t >= 32) return;
+        const bool wl = t < BP, wr = t < BP && r > 0, wt = t < 32;
+        const unsigned long long* gl = gdcv + ((size_t)l * BP + (wl ? t : 0)) * 2;
+        const unsigned long long* gr = gdcv + ((size_t)(r > 0 ? r : l) * BP + (wl ? t : 0)) * 2;
+        const unsigned long long* gt = gtau + 2 * (wt ? t : 0);
         const unsigned long long t0 = wall_clock64();
-        unsigned long long a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+        unsigned long long a0 = 0, a1 = 0, b0 = 0, b1 = 0, c0 = 0, c1 = 0;
         for (;;) {
           if (wl) {
             a0 = __hip_atomic_load(gl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1826,8 +1908,13 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, const
             b0 = __hip_atomic_load(gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             b1 = __hip_atomic_load(gr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
+          if (wt) {
+            c0 = __hip_atomic_load(gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c1 = __hip_atomic_load(gt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
           const bool ok = (!wl || ((a0 >> 32) == stamp && (a1 >> 32) == stamp)) &&
-                          (!wr || ((b0 >> 32) == stamp && (b1 >> 32) == stamp));
+                          (!wr || ((b0 >> 32) == stamp && (b1 >> 32) == stamp)) &&
+                          (!wt || ((c0 >> 32) == stamp && (c1 >> 32) == stamp));
           if (ok) break;
           if (wall_clock64() - t0 > 30000000ull) {
             atomicAdd(bad, 1);
@@ -1836,14 +1923,12 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, const
           __builtin_amdgcn_s_sleep(1);
         }
         if (wl) sl[t] = __hiloint2double((int)(unsigned)a0, (int)(unsigned)a1);
-        sr_[t] = wr ? __hiloint2double((int)(unsigned)b0, (int)(unsigned)b1) : 0.0;
+        if (wl) sr_[t] = wr ? __hiloint2double((int)(unsigned)b0, (int)(unsigned)b1) : 0.0;
+        if (wt) st_[t] = __hiloint2double((int)(unsigned)c0, (int)(unsigned)c1);
       },
       [&](int row, double v) {
         const size_t e = (size_t)i * BP + row;
-        const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
-        __hip_atomic_store(gdcv + 2 * e, (stamp << 32) | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gdcv + 2 * e + 1, (stamp << 32) | (bits & 0xffffffffull), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        cr_publish_granules(gdcv + 2 * e, stamp, v);
         dcv[e] = v;
         sdv[row] = v;
       });
@@ -2149,8 +2234,8 @@ struct FteBuffers {
   // per-row max |delay gradient| of the frame the row starts, per-block delay step / state norms
   double *graw, *gmaxt, *normt;
   int* bad;
-  int* bk;                    // k_cr_back_all: ticket counter
-  unsigned long long* gdcv;   // k_cr_back_all: the step rows as {stamp, word} granules
+  int* bk;                    // k_cr_back_all: ticket counter, partials counter
+  unsigned long long* gdcv;   // k_cr_back_all: the step rows, then dtau, as {stamp, word} granules
   FteState* st;
 };
 
@@ -2229,7 +2314,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
                odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)),
                onp = take(2 * (size_t)n), oTc = take(nlin * N * std::max(tc_stride(d.Cg), 1)), oFm = take(N), oFq = take(N), ost = take(16), oint = take(8),
                ogr = take((size_t)M * P), ogt = take(M), ont = take(2 * (size_t)n),
-               obk = take((size_t)n / 2 + 2), ogd = take((size_t)n * BP * 2);
+               obk = take((size_t)n / 2 + 2), ogd = take((size_t)n * BP * 2 + 64);
   // staged inputs (owned mode only)
   const size_t oI = take((n_ints + 1) / 2 + 1), oR = take(n_reals), oC = take((size_t)ACS_CAM_STRIDE * C),
                oMe = take((size_t)N * C * L * 2), oWt = take((size_t)N * C * L), oQ = take(P);
@@ -2315,7 +2400,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
     ts = tau ? b.tau : nullptr;
   }
   const size_t MP = (size_t)M * P;
-  const size_t ngd = (size_t)n * BP * 2;
+  const size_t ngd = (size_t)n * BP * 2 + 64;
   const size_t nI = std::max(std::max(std::max(MP, (size_t)n + 1), ngd), (size_t)std::max(d.NT, GR));
   hipLaunchKernelGGL(k_fte_init_state, dim3(acs_grid((int64_t)nI, 256)), dim3(256), 0, s, b.X, Xs, MP, b.tau, ts,
                      d.NT, b.bad, b.dtau, GR, b.bk, n + 1, b.gdcv, ngd);
@@ -2462,20 +2547,15 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   int sym = 0;
   cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad, false, &sym);
   cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, sym);
-  hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, d, b.st, b.Hloc, b.gloc, b.Tau, b.part, 0,
-                     d.N, 0, d.nblk, 1, (const double*)b.Tc);
-  // constant / no delays: the trial state is stepped by k_cr_top (block 0, delays) and
-  // k_cr_back_all (every other block); variable delays need the neighbours' rows: k_cr_trial
+  // tau partials, the top block and every back-substitution level in one launch, chained by
+  // per-launch stamps (running the top levels' few blocks one after the other inside one
+  // workgroup was tried in r03 and took 30 us: one workgroup streams a block's W at ~2 us, so
+  // the W loads of every block have to be in flight at once). Constant / no delays: the
+  // trial state is stepped there too; variable delays need the neighbours' rows: k_cr_trial
   double* Xt = d.var ? nullptr : b.X;
-  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(1024), 0, s, d, b.st, (const double*)b.Wc, b.part, b.gmaxp, b.tau, b.dcv,
-                     b.dtau, b.bad, Xt, b.normp);
-  // every back-substitution level in one launch, chained by per-block stamps (running the
-  // top levels' few blocks one after the other inside k_cr_top's workgroup was tried in r03
-  // and took 30 us: one workgroup streams a block's W at ~2 us, so the W loads of every
-  // block have to be in flight at once)
-  if (d.nblk > 1)
-    hipLaunchKernelGGL(k_cr_back_all, dim3(d.nblk - 1), dim3(1024), 0, s, d, bend, b.st, (const double*)b.Wc,
-                       (const double*)b.dtau, b.dcv, b.bk, b.gdcv, b.bad, Xt, b.normp);
+  hipLaunchKernelGGL(k_cr_back_all, dim3(CR_NCHUNK + d.nblk), dim3(1024), 0, s, d, bend, b.st, (const double*)b.Wc,
+                     (const double*)b.Hloc, (const double*)b.gloc, (const double*)b.Tau, (const double*)b.Tc, b.part,
+                     (const double*)b.gmaxp, b.tau, b.dtau, b.dcv, b.bk, b.gdcv, b.bad, Xt, b.normp);
   if (d.var)
     hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
                        b.normp, 1, 0, 1);
