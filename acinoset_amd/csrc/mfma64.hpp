@@ -167,6 +167,93 @@ __device__ __forceinline__ void tile16_gj_inverse_v1(double* v, int lane, int* b
   if (nbad && bad && lane == 0) atomicAdd(bad, nbad);
 }
 
+// Block Gauss-Jordan form of the 16x16 tile inverse: four steps of a 4x4 pivot block
+// (rows / columns 4k..4k+3, register k of every lane) instead of sixteen scalar steps. Per
+// step: the pivot block P made uniform (readlanes), its LU without pivoting solved by every
+// lane for column lk of P^-1 (uniform operands, no cross-lane traffic on the chain), then two
+// f64 MFMAs: B' = P^-1 [M_K with identity on columns K] (A operand = P^-1 rows replicated,
+// so every accumulator register holds B' in B layout) and M <- M~ - M_{:,K} B' (rows K set
+// to B', columns K of the other rows to -M_{:,K} P^-1). The column panel M_{:,K} reaches the
+// A layout by ds_bpermute, off the chain. The LU pivots are the scalar form's pivots, so the
+// SPD check and the 1e-300 replacement keep their meaning.
+template <int K, bool SPD>
+__device__ __forceinline__ void tile16_bgj_step(double* v, int lane, int& nbad) {
+  const int li = lane & 15, lk = lane >> 4;
+  // A layout of the column panel: lane (li, lk) <- M[li][4K + lk] = v[li >> 2] of lane
+  // 16 (li & 3) + 4K + lk
+  const int src = (16 * (li & 3) + 4 * K + lk) << 2;
+  double g[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    g[q] = __hiloint2double(__builtin_amdgcn_ds_bpermute(src, __double2hiint(v[q])),
+                            __builtin_amdgcn_ds_bpermute(src, __double2loint(v[q])));
+  double p[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) p[r][c] = read_lane_f64(v[K], 16 * r + 4 * K + c);
+  auto piv = [&](double u) {
+    const bool ok = SPD ? u > 0.0 : fabs(u) > 1e-300;
+    nbad += ok ? 0 : 1;
+    return rcp_nr(ok ? u : 1e-300);
+  };
+  // LU (Doolittle, no pivoting) of the uniform 4x4 pivot block
+  const double i0 = piv(p[0][0]);
+  const double l10 = p[1][0] * i0, l20 = p[2][0] * i0, l30 = p[3][0] * i0;
+  const double a11 = fma(-l10, p[0][1], p[1][1]), a12 = fma(-l10, p[0][2], p[1][2]), a13 = fma(-l10, p[0][3], p[1][3]);
+  const double a21 = fma(-l20, p[0][1], p[2][1]), a22 = fma(-l20, p[0][2], p[2][2]), a23 = fma(-l20, p[0][3], p[2][3]);
+  const double a31 = fma(-l30, p[0][1], p[3][1]), a32 = fma(-l30, p[0][2], p[3][2]), a33 = fma(-l30, p[0][3], p[3][3]);
+  const double i1 = piv(a11);
+  const double l21 = a21 * i1, l31 = a31 * i1;
+  const double b22 = fma(-l21, a12, a22), b23 = fma(-l21, a13, a23);
+  const double b32 = fma(-l31, a12, a32), b33 = fma(-l31, a13, a33);
+  const double i2 = piv(b22);
+  const double l32 = b32 * i2;
+  const double c33 = fma(-l32, b23, b33);
+  const double i3 = piv(c33);
+  // column lk of P^-1: L y = e_lk, U x = y
+  const double y0 = lk == 0 ? 1.0 : 0.0;
+  const double y1 = fma(-l10, y0, lk == 1 ? 1.0 : 0.0);
+  const double y2 = fma(-l21, y1, fma(-l20, y0, lk == 2 ? 1.0 : 0.0));
+  const double y3 = fma(-l32, y2, fma(-l31, y1, fma(-l30, y0, lk == 3 ? 1.0 : 0.0)));
+  const double x3 = y3 * i3;
+  const double x2 = fma(-b23, x3, y2) * i2;
+  const double x1 = fma(-a12, x2, fma(-a13, x3, y1)) * i1;
+  const double x0 = fma(-p[0][1], x1, fma(-p[0][2], x2, fma(-p[0][3], x3, y0))) * i0;
+  const int rr = li & 3;
+  const double pinv = rr == 0 ? x0 : (rr == 1 ? x1 : (rr == 2 ? x2 : x3));  // P^-1[li & 3][lk]
+  const bool colK = (li >> 2) == K;
+  const double bk = colK ? ((li & 3) == lk ? 1.0 : 0.0) : v[K];
+  const dbl4 z = {0.0, 0.0, 0.0, 0.0};
+  const double bp = mfma64(pinv, bk, z)[0];  // B'[lk][li]
+  const double gq = li < 4 ? g[0] : (li < 8 ? g[1] : (li < 12 ? g[2] : g[3]));
+  const double a2 = colK ? 0.0 : -gq;
+  dbl4 c;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) c[q] = q == K ? bp : (colK ? 0.0 : v[q]);
+  c = mfma64(a2, bp, c);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = c[q];
+}
+template <bool SPD, typename Hook, int... K>
+__device__ __forceinline__ void tile16_bgj_steps_hook(double* v, int lane, int& nbad, Hook& hook,
+                                                      std::integer_sequence<int, K...>) {
+  ((tile16_bgj_step<K, SPD>(v, lane, nbad), hook(std::integral_constant<int, 4 * K>{}),
+    hook(std::integral_constant<int, 4 * K + 1>{}), hook(std::integral_constant<int, 4 * K + 2>{}),
+    hook(std::integral_constant<int, 4 * K + 3>{})),
+   ...);
+}
+template <bool SPD, typename Hook>
+__device__ __forceinline__ void tile16_bgj_inverse_hook(double* v, int lane, int* bad, Hook&& hook) {
+  int nbad = 0;
+  tile16_bgj_steps_hook<SPD>(v, lane, nbad, hook, std::make_integer_sequence<int, 4>{});
+  if (nbad && bad && lane == 0) atomicAdd(bad, nbad);
+}
+template <bool SPD>
+__device__ __forceinline__ void tile16_bgj_inverse(double* v, int lane, int* bad) {
+  tile16_bgj_inverse_hook<SPD>(v, lane, bad, [](auto) {});
+}
+
 // In-register Gauss-Jordan inverse of one 16x16 tile held by a wave in accumulator layout
 // (lane l: column l & 15 of rows (l >> 4) + 4q). The pivot (v_readlane), pivot row
 // (permlane swaps) and pivot column (DPP row_newbcast) of each of the 16 steps move on the

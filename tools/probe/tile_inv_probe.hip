@@ -38,7 +38,8 @@ __global__ void k_inv(const double* A, double* out, long long* cyc, int* bad, in
   for (int r = 0; r < reps; ++r) {
     if (MODE == 0) inv_shfl(v, lane);
     else if (MODE == 1) tile16_gj_inverse_v1<true>(v, lane, bad);
-    else tile16_gj_inverse<true>(v, lane, bad);
+    else if (MODE == 2) tile16_gj_inverse<true>(v, lane, bad);
+    else tile16_bgj_inverse<true>(v, lane, bad);
   }
   long long t1 = clock64();
   for (int q = 0; q < 4; ++q) out[blockIdx.x * 256 + (r0 + 4 * q) * 16 + c] = v[q];
@@ -61,6 +62,7 @@ int main() {
   double* o0 = (double*)malloc(NT * 256 * 8);
   double* o1 = (double*)malloc(NT * 256 * 8);
   double* o2 = (double*)malloc(NT * 256 * 8);
+  double* o3 = (double*)malloc(NT * 256 * 8);
   srand(1);
   for (int t = 0; t < NT; ++t) {
     double B[256];
@@ -76,13 +78,14 @@ int main() {
   hipMalloc(&dA, NT * 256 * 8); hipMalloc(&dO, NT * 256 * 8); hipMalloc(&dc, NT * 8); hipMalloc(&db, 4);
   hipMemcpy(dA, hA, NT * 256 * 8, hipMemcpyHostToDevice); hipMemset(db, 0, 4);
   long long cyc[NT];
-  const char* names[3] = {"shfl", "valu-select", "valu-dpp64"};
-  double* outs[3] = {o0, o1, o2};
-  for (int mode = 0; mode < 3; ++mode) {
+  const char* names[4] = {"shfl", "valu-select", "valu-dpp64", "block4-mfma"};
+  double* outs[4] = {o0, o1, o2, o3};
+  for (int mode = 0; mode < 4; ++mode) {
     for (int reps : {1, 1, 9}) {
       if (mode == 0) hipLaunchKernelGGL(k_inv<0>, dim3(NT), dim3(64), 0, 0, dA, dO, dc, db, reps);
       else if (mode == 1) hipLaunchKernelGGL(k_inv<1>, dim3(NT), dim3(64), 0, 0, dA, dO, dc, db, reps);
-      else hipLaunchKernelGGL(k_inv<2>, dim3(NT), dim3(64), 0, 0, dA, dO, dc, db, reps);
+      else if (mode == 2) hipLaunchKernelGGL(k_inv<2>, dim3(NT), dim3(64), 0, 0, dA, dO, dc, db, reps);
+      else hipLaunchKernelGGL(k_inv<3>, dim3(NT), dim3(64), 0, 0, dA, dO, dc, db, reps);
       hipDeviceSynchronize();
       hipMemcpy(cyc, dc, NT * 8, hipMemcpyDeviceToHost);
       if (reps == 1) hipMemcpy(outs[mode], dO, NT * 256 * 8, hipMemcpyDeviceToHost);
@@ -93,16 +96,17 @@ int main() {
   long long ndiff = 0;
   for (int e = 0; e < NT * 256; ++e) ndiff += (o1[e] != o2[e]);
   printf("dpp64 vs select: %lld of %d elements differ\n", ndiff, NT * 256);
-  double e0 = 0, e1 = 0, e01 = 0;
+  double e0 = 0, e1 = 0, e01 = 0, e3 = 0;
   for (int t = 0; t < NT; ++t) {
     double mx = 0; for (int e = 0; e < 256; ++e) mx = fmax(mx, fabs(ref[t * 256 + e]));
     for (int e = 0; e < 256; ++e) {
       e0 = fmax(e0, fabs(o0[t * 256 + e] - ref[t * 256 + e]) / mx);
       e1 = fmax(e1, fabs(o1[t * 256 + e] - ref[t * 256 + e]) / mx);
       e01 = fmax(e01, fabs(o1[t * 256 + e] - o0[t * 256 + e]) / mx);
+      e3 = fmax(e3, fabs(o3[t * 256 + e] - ref[t * 256 + e]) / mx);
     }
   }
   int hb; hipMemcpy(&hb, db, 4, hipMemcpyDeviceToHost);
-  printf("max rel err: shfl vs host %.3e, valu vs host %.3e, valu vs shfl %.3e, bad %d\n", e0, e1, e01, hb);
-  return (e1 < 1e-8 && hb == 0) ? 0 : 1;
+  printf("max rel err: shfl vs host %.3e, valu vs host %.3e, valu vs shfl %.3e, block4 vs host %.3e, bad %d\n", e0, e1, e01, e3, hb);
+  return (e1 < 1e-8 && e3 < 1e-8 && hb == 0) ? 0 : 1;
 }
