@@ -176,6 +176,11 @@ __device__ __forceinline__ void tile16_gj_inverse_v1(double* v, int lane, int* b
 // to B', columns K of the other rows to -M_{:,K} P^-1). The column panel M_{:,K} reaches the
 // A layout by ds_bpermute, off the chain. The LU pivots are the scalar form's pivots, so the
 // SPD check and the 1e-300 replacement keep their meaning.
+// Measured and not adopted (kept for tools/probe/tile_inv_probe.hip): 3,830 ticks per
+// inverse against the scalar DPP64 form's 3,721, and the FTE iteration 331 -> 342 us with it
+// in k_cr_level (profiles/r03/tile_inv_block4.log, fte_breakdown_r03y_blockinv_tried.log):
+// the four LU pivots' reciprocals and the two MFMA round trips per step cost as much as the
+// sixteen scalar steps' chain.
 template <int K, bool SPD>
 __device__ __forceinline__ void tile16_bgj_step(double* v, int lane, int& nbad) {
   const int li = lane & 15, lk = lane >> 4;
