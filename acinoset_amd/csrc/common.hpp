@@ -162,7 +162,12 @@ __device__ __forceinline__ void fisheye_project(const double* __restrict__ c, do
       // r = sqrt(a^2+b^2+eps): dr/da = a/r, same formula with this r
       spr = (dthd * r * rcp_nr(1.0 + r * r) - thd) * (ir * ir * ir);
     } else {
-      spr = big ? (dthd * r * rcp_nr(1.0 + r2) - thd) * (ir * ir * ir) : 0.0;
+      // zero below the guard by a multiply, not a branch (there the factor is exactly 0:
+      // r = 0, thd = 0, ir = 1); the 0/1 factor is opaque to the compiler so that it does
+      // not turn the product back into a branch around the reciprocal
+      double keep = big ? 1.0 : 0.0;
+      asm volatile("" : "+v"(keep));
+      spr = (dthd * r * rcp_nr(1.0 + r2) - thd) * (ir * ir * ir) * keep;
     }
     const double duda = c[0] * (s + a * a * spr);
     const double dudb = c[0] * (a * b * spr);

@@ -72,6 +72,10 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     x2 = pts_in[3 * p + 2];
   }
   for (int i = threadIdx.x; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
+  // the null camera (record C): R = 0, t = (0, 0, 1), K = 0. Slots without an observation
+  // project through it to u = v = 0 with a zero Jacobian, so with a zero observation they add
+  // exact zeros to every sum: linearize() needs no branch around its projection
+  if (threadIdx.x < ACS_CAM_STRIDE) s_cam[C * ACS_CAM_STRIDE + threadIdx.x] = threadIdx.x == 19 ? 1.0 : 0.0;
   __syncthreads();
   if (!live) return;  // whole group leaves together
 
@@ -87,7 +91,7 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     ok[s] = slot < K && mk[s] && cam < C;
     ou[s] = ok[s] ? q[s].x : 0.0;
     ov[s] = ok[s] ? q[s].y : 0.0;
-    oc[s] = s_cam + (ok[s] ? cam : 0) * ACS_CAM_STRIDE;
+    oc[s] = s_cam + (ok[s] ? cam : C) * ACS_CAM_STRIDE;
     if constexpr (HOIST) {
 #pragma unroll
       for (int i = 0; i < ACS_CAM_STRIDE; ++i) cr[s][i] = oc[s][i];
@@ -121,8 +125,7 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     double Fl = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      if (!ok[s]) continue;
-      ProjOut o;
+      ProjOut o;  // slots without an observation: the null camera, exact zero contributions
       if constexpr (HOIST)
         fisheye_project<true>(cr[s], X0, X1, X2, o);
       else
@@ -175,15 +178,17 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     const double dl = 1.0 + lam;
     const double a00 = H[0] * dl, a11 = H[3] * dl, a22 = H[5] * dl;
     bool pd = a00 > 0.0;
-    const double i00 = pd ? rsq_nr(a00) : 1.0;  // reciprocal Cholesky diagonal
+    // reciprocal Cholesky diagonal; the argument, not the result, is selected (rsq_nr(1) = 1):
+    // no branch around the reciprocal square roots
+    const double i00 = rsq_nr(pd ? a00 : 1.0);
     const double L10 = H[1] * i00, L20 = H[2] * i00;
     const double d11 = a11 - L10 * L10;
     pd = pd && d11 > 0.0;
-    const double i11 = pd ? rsq_nr(d11) : 1.0;
+    const double i11 = rsq_nr(pd ? d11 : 1.0);
     const double L21 = (H[4] - L20 * L10) * i11;
     const double d22 = a22 - L20 * L20 - L21 * L21;
     pd = pd && d22 > 0.0;
-    const double i22 = pd ? rsq_nr(d22) : 1.0;
+    const double i22 = rsq_nr(pd ? d22 : 1.0);
     double dx0 = 0.0, dx1 = 0.0, dx2 = 0.0;
     if (pd) {
       const double y0 = -g[0] * i00;
@@ -218,7 +223,7 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     ++nfev;
     // |dx| <= xtol (xtol + |x|), compared squared
     const double xx = x0 * x0 + x1 * x1 + x2 * x2;
-    const double xn = xx > 0.0 ? xx * rsq_nr(xx) : 0.0;
+    const double xn = xx > 0.0 ? xx * rsq_nr(xx > 0.0 ? xx : 1.0) : 0.0;
     const double xb = prm.xtol * (prm.xtol + xn);
     const bool small = dx0 * dx0 + dx1 * dx1 + dx2 * dx2 <= xb * xb;
     if (Fn < F) {
@@ -380,12 +385,12 @@ static void launch_lm_t(acs_ctx* ctx, int blocks, int block, const double* cams,
   if constexpr (S == 1 && !CAMID && G <= 16) {
     if (hoist) {
       hipLaunchKernelGGL((k_sba_lm<G, S, CAMID, true>), dim3(blocks), dim3(block),
-                         sizeof(double) * ACS_CAM_STRIDE * C, ctx->stream, cams, C, K, uv, mask, camid, n_pts, pts_in,
+                         sizeof(double) * ACS_CAM_STRIDE * (C + 1), ctx->stream, cams, C, K, uv, mask, camid, n_pts, pts_in,
                          pts, prm, c0, c1, st);
       return;
     }
   }
-  hipLaunchKernelGGL((k_sba_lm<G, S, CAMID, false>), dim3(blocks), dim3(block), sizeof(double) * ACS_CAM_STRIDE * C,
+  hipLaunchKernelGGL((k_sba_lm<G, S, CAMID, false>), dim3(blocks), dim3(block), sizeof(double) * ACS_CAM_STRIDE * (C + 1),
                      ctx->stream, cams, C, K, uv, mask, camid, n_pts, pts_in, pts, prm, c0, c1, st);
 }
 
