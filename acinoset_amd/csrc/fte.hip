@@ -129,6 +129,36 @@ __device__ double block_sum(double v, double* s_red) {
   if (n > 64) __syncthreads();  // s_red is free for the caller's next reduction
   return r;
 }
+// block_sum of NV values at once (the same tree per value, so each result is bit-identical
+// to its own block_sum; one set of barriers instead of NV). s_red: NV x blockDim doubles.
+template <int NV>
+__device__ void block_sums(double (&v)[NV], double* s_red) {
+  const int t = threadIdx.x, n = blockDim.x, l = t & 63;
+  double r[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) r[j] = v[j];
+  if (n > 64) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s_red[j * n + t] = v[j];
+    __syncthreads();
+    for (int h = n / 2; h >= 128; h >>= 1) {
+      if (t < h) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) s_red[j * n + t] += s_red[j * n + t + h];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) r[j] = s_red[j * n + l] + s_red[j * n + l + 64];
+  }
+#pragma unroll
+  for (int h = 32; h > 0; h >>= 1)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) r[j] += __shfl_down(r[j], h, 64);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = __shfl(r[j], 0, 64);
+  if (n > 64) __syncthreads();
+}
 // acc[s] += x[s][es * k] for k = k0, k0 + st, .. < k1 in that order (the plain strided
 // loop's sums, bit for bit), with eight strides' loads of every stream issued before the
 // first add instead of one dependent round trip per stride
@@ -2134,7 +2164,7 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
                                                 const double* __restrict__ Fm, const double* __restrict__ Fq,
                                                 const double* __restrict__ normp, int spec,
                                                 FteState* __restrict__ snap = nullptr) {
-  __shared__ double s_red[256];
+  __shared__ double s_red[4 * 256];
   const int tid = threadIdx.x;
   // every load is issued before the LM state is read: both copies of the measurement terms
   // (spec: the trial's are in Floc copy cur ^ 1) and the step / state norm partials
@@ -2147,9 +2177,10 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
     const double* xs[2] = {normp, normp + 1};
     strided_sums<2>(xs, 2, tid, d.nblk, blockDim.x, nrm);
   }
-  double dn = nrm[0], xn = nrm[1];
   const double a = (spec && (st->cur ^ 1)) ? acc[1] : acc[0];
-  const double fm = block_sum(a, s_red), fq = block_sum(acc[2], s_red);
+  double sums[4] = {a, acc[2], nrm[0], nrm[1]};
+  block_sums<4>(sums, s_red);
+  const double fm = sums[0], fq = sums[1], dn = sums[2], xn = sums[3];
   if (init) {
     if (tid == 0) {
       st->F = st->F0 = fm + fq;
@@ -2162,8 +2193,6 @@ __global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict_
     if (tid == 0) fte_snapshot(st, snap);
     return;
   }
-  dn = block_sum(dn, s_red);
-  xn = block_sum(xn, s_red);
   if (tid != 0) return;
   if (st->gmax <= o.gtol) {
     st->status = ACS_STATUS_GTOL;
