@@ -1618,6 +1618,27 @@ __device__ __forceinline__ double cr_trial_x(const FteDims& d, const FteState* s
   if (!Xbuf || e >= 3 * P || 3 * i + e / P >= d.M) return 0.0;
   return Xbuf[(size_t)st->cur * d.M * P + (size_t)(3 * i + e / P) * P + e % P];
 }
+// block_sum of a and b where only threads < 128 hold nonzero terms, all >= +0: every level
+// of block_sum's tree above 128 then adds exact zeros, so its result is the wave tree over
+// s[l] + s[l + 64] - computed here with one exchange and two barriers instead of ten
+// (bit-identical). blockDim.x >= 128; s_red: 256 doubles.
+__device__ __forceinline__ void block_sum2_lo128(double& a, double& b, double* s_red) {
+  const int t = threadIdx.x, l = t & 63;
+  if (t < 128) {
+    s_red[t] = a;
+    s_red[128 + t] = b;
+  }
+  __syncthreads();
+  double ra = s_red[l] + s_red[l + 64], rb = s_red[128 + l] + s_red[128 + l + 64];
+#pragma unroll
+  for (int h = 32; h > 0; h >>= 1) {
+    ra += __shfl_down(ra, h, 64);
+    rb += __shfl_down(rb, h, 64);
+  }
+  a = __shfl(ra, 0, 64);
+  b = __shfl(rb, 0, 64);
+  __syncthreads();
+}
 __device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* st, int i, double dv, double x,
                                               const double* __restrict__ dtau, double* __restrict__ Xbuf,
                                               double* __restrict__ taubuf, double* __restrict__ normp, bool taus,
@@ -1641,8 +1662,12 @@ __device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* 
     dn += t * t;
     xn += tau[e] * tau[e];
   }
-  dn = block_sum(dn, s_red);
-  xn = block_sum(xn, s_red);
+  if (3 * P <= 128 && d.C <= 128 && blockDim.x >= 128) {
+    block_sum2_lo128(dn, xn, s_red);
+  } else {
+    dn = block_sum(dn, s_red);
+    xn = block_sum(xn, s_red);
+  }
   if (threadIdx.x == 0) {
     normp[2 * i] = dn;
     normp[2 * i + 1] = xn;
