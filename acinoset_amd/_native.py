@@ -71,7 +71,7 @@ class EkfInitSpec(C.Structure):
     _fields_ = [(k, C.c_int32) for k in ('nose', 'lure', 'x0', 'y0', 'psi0', 'xl', 'yl', 'from_sba')]
 
 
-def ekf_init_spec(table, obs_markers, from_sba=True):
+def ekf_init_spec(table, obs_markers, from_sba=False):
     """The pipeline's init descriptor for EKF skeleton `table` on observations whose marker
     order is `obs_markers`."""
     obs = list(obs_markers)
@@ -403,7 +403,7 @@ class Context:
 
     # ---- configs[4]: SBA + EKF fused ------------------------------------------------
     def sba_ekf_pipeline(self, table, cams, meas, likelihood, obs_markers, fps, thresh, max_pixel_err, r_std_base, Q,
-                         P0, sba_opts=None, from_sba=True, ref_numerics=True, eps=1e-3):
+                         P0, sba_opts=None, from_sba=False, ref_numerics=True, eps=1e-3):
         """acs_sba_ekf_pipeline on host arrays: meas (S, N, C, Lobs, 2), likelihood (S, N, C,
         Lobs) with markers `obs_markers`; the EKF runs skeleton `table` (its markers a subset of
         obs_markers). Returns dict pts (S, N, Lobs, 3), x_est, x_smooth (S, N, 3P), outliers
@@ -433,7 +433,7 @@ class Context:
         return dict(pts=pts, x_est=xe, x_smooth=xs, outliers=outl, sba=rep.as_dict())
 
     def sba_ekf_pipeline_dev(self, table, obs_markers, cams_p, n_cams, meas_p, lik_p, S, N, fps, thresh,
-                             max_pixel_err, rstd_p, Q_p, P0_p, pts_p, xe_p, xs_p, sba_opts=None, from_sba=True,
+                             max_pixel_err, rstd_p, Q_p, P0_p, pts_p, xe_p, xs_p, sba_opts=None, from_sba=False,
                              ref_numerics=True, eps=1e-3, report=False):
         """acs_sba_ekf_pipeline on HBM-resident arrays (device pointers, asynchronous unless
         `report`: then waits and returns (sba report dict, outliers (S,)))."""

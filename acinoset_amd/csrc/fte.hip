@@ -2859,6 +2859,8 @@ __global__ void k_dist_decide(FteState* __restrict__ st, FteOptsDev o, const dou
     st->F = st->F0 = fm + fq;
     st->Fmeas = fm;
     st->Fmodel = fq;
+    // max_iters = 0: no step at all, as acs_fte_solve (X0 back, iters 0)
+    if (o.max_iters <= 0) st->status = ACS_STATUS_MAXITER;
     return;
   }
   if (st->status != 0 || !st->pending) return;

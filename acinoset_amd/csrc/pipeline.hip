@@ -220,9 +220,9 @@ int acs_sba_ekf_pipeline(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints,
   // 6. the EKF model's observations
   const double *dMe = (const double*)dM, *dLe = (const double*)dL;
   if (!ident) {
-    int* dmap = (int*)acs_ws(ctx, WS_PIPE6, sizeof(int) * Le + sizeof(double) * SN * n_cams * Le * 3);
+    int* dmap = (int*)acs_ws(ctx, WS_PIPE6, sizeof(int) * ((Le + 3) & ~3) + sizeof(double) * SN * n_cams * Le * 3);
     if (!dmap) return ACS_E_NOMEM;
-    double* me = (double*)(dmap + ((Le + 1) & ~1));
+    double* me = (double*)(dmap + ((Le + 3) & ~3));  // 16-byte aligned: stored through double2
     double* le = me + SN * n_cams * Le * 2;
     ACS_HIP(ctx, hipMemcpyAsync(dmap, ekf_markers, sizeof(int) * Le, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_pipe_ekf_gather, dim3(acs_grid(SN * n_cams * Le, 256)), dim3(256), 0, s, (const double*)dM,

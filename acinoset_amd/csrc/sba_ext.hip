@@ -727,6 +727,7 @@ __global__ void k_ext_decide(ExtDims d, ExtState* __restrict__ st, ExtOpts o, co
   if (st->first) {
     st->first = 0;
     st->F = st->F0 = p3[0];
+    if (o.max_iters <= 0) st->status = ACS_STATUS_MAXITER;  // no step at all
     return;
   }
   if (st->status != 0 || !st->pending) return;
@@ -1015,6 +1016,7 @@ int acs_sba_ext_dist_init(acs_sba_ext_dist* h, double* payload) {
 int acs_sba_ext_dist_round(acs_sba_ext_dist* h, const double* in, double* out) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
+  ACS_CHECK(ctx, in && out && in != out, "sba_ext_dist_round: in and out must be distinct buffers");
   hipStream_t s = ctx->stream;
   const int NC = 6 * h->d.C, n1 = NC * NC + 3 * NC + h->R;
   int rc;

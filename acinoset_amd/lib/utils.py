@@ -219,6 +219,67 @@ def save_optimised_cheetah(positions, out_fpath, extra_data=None, for_matlab=Tru
         print('Saved', os.path.splitext(out_fpath)[0] + '.mat')
 
 
+def _write_h5(df, fpath, key):
+    """`DataFrame.to_hdf(format='table')` where pandas can (PyTables installed); otherwise
+    the .csv beside it is the output. Returns whether the .h5 was written."""
+    try:
+        df.to_hdf(fpath, key=key, format='table', mode='w')
+        return True
+    except ImportError:
+        return False
+
+
+def save_3d_cheetah_as_2d(position3d_arr, out_dir, scene_fpath, bodyparts, project_func, start_frame,
+                          save_as_csv=True, out_fname=None):
+    """`src/lib/utils.py:237-286`: reproject 3-D markers into every camera as DLC-format
+    tables, `cam{n}_{out_fname}.h5` (+ `.csv`), one per `cam[1-9].mp4` found in `out_dir`
+    or its parent. Columns are (bodyparts × [x, y, likelihood]) with likelihood NaN; a
+    projection with u or v outside [0, cam_res] is NaN in both. `position3d_arr` is one
+    (n_frames, L, 3) array for every camera or a per-camera list (the FTE's shutter-delay
+    shifted positions). `project_func` is the GPU projection (`calib.project_points_fisheye`)
+    in the drop-in; any callable with the reference's signature works. Without PyTables the
+    `.h5` is skipped (said once) and the `.csv` is written whatever `save_as_csv` says.
+    Returns the per-camera DataFrames ([] when no video is found)."""
+    assert os.path.dirname(os.path.dirname(scene_fpath)) in out_dir, \
+        'scene_fpath does not belong to the same parent folder as out_dir'
+    video_fpaths = sorted(glob(os.path.join(out_dir, 'cam[1-9].mp4')))
+    if not video_fpaths:
+        video_fpaths = sorted(glob(os.path.join(os.path.dirname(out_dir), 'cam[1-9].mp4')))
+    if not video_fpaths:
+        print('Could not save 3D cheetah to 2D - No videos were found in', out_dir, 'or', os.path.dirname(out_dir))
+        return []
+    k_arr, d_arr, r_arr, t_arr, cam_res = load_scene(scene_fpath, verbose=False)
+    assert len(k_arr) == len(video_fpaths)
+    if not isinstance(position3d_arr, list):
+        position3d_arr = [position3d_arr] * len(video_fpaths)
+    pdindex = pd.MultiIndex.from_product([list(bodyparts), ['x', 'y', 'likelihood']], names=['bodyparts', 'coords'])
+    out_fname = os.path.basename(out_dir) if out_fname is None else out_fname
+    res = np.asarray(cam_res, np.float64)
+    result_dfs, h5_ok = [], True
+    for i, vid in enumerate(video_fpaths):
+        position3d = np.asarray(position3d_arr[i], np.float64)
+        n_frames = len(position3d)
+        prj = np.array(project_func(position3d, k_arr[i], d_arr[i], r_arr[i], t_arr[i]), np.float64).reshape(-1, 2)
+        with np.errstate(invalid='ignore'):
+            out = ((prj > res) | (prj < 0.0)).any(axis=1)
+        prj[out] = np.nan
+        data = np.full(position3d.shape, np.nan)
+        data[:, :, 0:2] = prj.reshape((n_frames, -1, 2))
+        cam_name = os.path.splitext(os.path.basename(vid))[0]
+        fpath = os.path.join(out_dir, f'{cam_name}_{out_fname}.h5')
+        df = pd.DataFrame(data.reshape((n_frames, -1)), columns=pdindex, index=range(start_frame, start_frame + n_frames))
+        h5_ok = _write_h5(df, fpath, f'{out_fname}_df') and h5_ok
+        if save_as_csv or not h5_ok:
+            df.to_csv(os.path.splitext(fpath)[0] + '.csv')
+        result_dfs.append(df)
+    pattern = os.path.join(out_dir, f'cam*_{out_fname}')
+    print('Saved', pattern + ('.h5' if h5_ok else '.csv (no PyTables: .h5 skipped)'))
+    if save_as_csv and h5_ok:
+        print('Saved', pattern + '.csv')
+    print()
+    return result_dfs
+
+
 def create_board_object_pts(board_shape, square_edge_length):
     obj = np.zeros((board_shape[0] * board_shape[1], 3), np.float32)
     obj[:, :2] = np.mgrid[0:board_shape[0], 0:board_shape[1]].T.reshape(-1, 2) * square_edge_length

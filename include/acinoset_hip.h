@@ -205,7 +205,9 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
  * rows, n_blocks x BP doubles = payload_sizes[1], once per solve) before result(). Every
  * rank runs the same reduced solve and takes the same decisions; the result equals
  * acs_fte_solve up to summation order.
- * shutter_delay with sd_mode 1 ('variable') is single-GPU only (ACS_E_INVALID here).   */
+ * shutter_delay with sd_mode 1 ('variable'): each frame's delays are interior unknowns of
+ * the rank that owns the frame, eliminated in its rows and stepped by that rank; they are
+ * gathered with the solution rows by p2, and result() returns tau as (n_frames, n_cams).  */
 typedef struct acs_fte_dist acs_fte_dist;
 int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
                         int64_t n_reals, const double* cams, int32_t n_cams, const double* meas,

@@ -104,6 +104,8 @@ class OracleFteRank:
         if self.first:
             self.first = False
             self.F = self.F0 = float(p3[0] + p3[1])
+            if self.opts['max_iters'] <= 0:       # no step at all (X0 back, iters 0)
+                self.status = 5
         elif self.status == 0 and self.pending:
             self.pending = False
             skip = self.phase4(p3) == 0 and not self.relin          # rejected: re-form only

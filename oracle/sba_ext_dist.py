@@ -54,6 +54,8 @@ class OracleSbaExtRank:
         if self.first:
             self.first = False
             self.F = self.F0 = float(p3[0])
+            if self.opts['max_iters'] <= 0:       # no step at all
+                self.status = 5
             return False
         if self.status or not self.pending:
             return False

@@ -588,8 +588,173 @@ def dlc_fixture():
     np.savez_compressed(os.path.join(HERE, 'dlc.npz'), **out)
 
 
+def _load_ref_app_and_tri():
+    """The reference's `lib.app` (src/lib/app.py) and `core.tri` (src/core/tri.py), loaded
+    from their files. Stand-ins only for what they import but do not compute with on this
+    path: `lib.plotting` / `lib.vid` / `lib.points` (GUI, video, checkerboard detection),
+    pyomo / seaborn (imported by core.tri, unused) and `core.metrics.save_error_dists`
+    (PDF histograms; it also fails on residual_error's string columns).
+    `create_labeled_videos` is replaced by a no-op (rendering)."""
+    import importlib.util
+    import types
+    from unittest import mock
+    for name in ('pyomo', 'pyomo.environ', 'pyomo.opt', 'seaborn', 'lib.plotting', 'lib.vid', 'lib.points'):
+        sys.modules[name] = mock.MagicMock()
+    import lib
+    spec = importlib.util.spec_from_file_location('lib.app', os.path.join(REF_SRC, 'lib', 'app.py'))
+    ref_app = importlib.util.module_from_spec(spec)
+    sys.modules['lib.app'] = ref_app
+    spec.loader.exec_module(ref_app)
+    lib.app = ref_app
+    ref_app.create_labeled_videos = lambda *a, **k: None
+    core = types.ModuleType('core')
+    core.__path__ = [os.path.join(REF_SRC, 'core')]
+    metrics = types.ModuleType('core.metrics')
+    metrics.save_error_dists = lambda *a, **k: 0.0
+    sys.modules['core'] = core
+    sys.modules['core.metrics'] = metrics
+    spec = importlib.util.spec_from_file_location('core.tri', os.path.join(REF_SRC, 'core', 'tri.py'))
+    ref_tri = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ref_tri)
+    return ref_app, ref_tri
+
+
+class _HdfCapture:
+    """`DataFrame.to_hdf` needs PyTables (absent): capture (path, key, frame) instead."""
+
+    def __init__(self):
+        import pandas as pd
+        self.pd = pd
+        self.frames = []
+
+    def __enter__(self):
+        self.orig = self.pd.DataFrame.to_hdf
+        frames = self.frames
+
+        def to_hdf(df, path, key, *a, **k):
+            frames.append((os.path.basename(path), key, df.copy()))
+        self.pd.DataFrame.to_hdf = to_hdf
+        return self
+
+    def __exit__(self, *exc):
+        self.pd.DataFrame.to_hdf = self.orig
+
+
+def _frame_arrays(prefix, frames, out_dir, out):
+    """Per camera: values (n_frames, 3 L), index, column tuples, and the CSV text the
+    reference wrote beside the (captured) .h5."""
+    out[f'{prefix}_n'] = np.array(len(frames))
+    for i, (fname, key, df) in enumerate(frames):
+        out[f'{prefix}{i}_fname'] = np.array(fname)
+        out[f'{prefix}{i}_key'] = np.array(key)
+        out[f'{prefix}{i}_values'] = df.to_numpy(np.float64)
+        out[f'{prefix}{i}_index'] = df.index.to_numpy(np.int64)
+        out[f'{prefix}{i}_columns'] = np.array(['|'.join(c) for c in df.columns])
+        out[f'{prefix}{i}_col_names'] = np.array([str(n) for n in df.columns.names])
+        with open(os.path.join(out_dir, os.path.splitext(fname)[0] + '.csv')) as f:
+            out[f'{prefix}{i}_csv'] = np.array(f.read())
+
+
+def save2d_tri_fixture(n_frames=12, seed=53):
+    """`save_3d_cheetah_as_2d` (src/lib/utils.py:237-286) and `core.tri` + `app.save_tri`
+    (src/core/tri.py:27-64, src/lib/app.py:238-268), the reference functions themselves.
+
+    * tri: a 6-camera synthetic sequence (20 keypoints + NaN rows) through the reference's
+      `core.tri` with cam1..6.mp4 beside the output: tri.pickle's contents (captured at
+      `utils.save_optimised_cheetah`), and the cam*_tri frames / CSVs.
+    * save2d: per-camera position lists (FTE style: one array per camera) with NaN points,
+      points outside the image and points behind a camera, projected by the reference
+      into cam*_fte frames; also the single-array (SBA / EKF) form with `out_fname`."""
+    import pandas as pd
+    ref_app, ref_tri = _load_ref_app_and_tri()
+    root = '/tmp/golden_save2d'
+    import shutil
+    shutil.rmtree(root, ignore_errors=True)
+    data_dir = os.path.join(root, 'data', '2019_03_09', 'run')
+    calib_dir = os.path.join(root, 'data', '2019_03_09', 'extrinsic_calib')
+    os.makedirs(data_dir)
+    os.makedirs(calib_dir)
+    scene = synth.load_scene_file()
+    C = scene.n_cams
+    scene_path = os.path.join(calib_dir, f'{C}_cam_scene_sba.json')
+    scene.to_json(scene_path)
+    for c in range(C):
+        open(os.path.join(data_dir, f'cam{c + 1}.mp4'), 'wb').close()
+    seq = synth.make_sequence(n_frames, scene, mode='default_nolure', seed=seed)
+    start_frame = 3
+    df = seq.to_df(start_frame=start_frame)
+    df = df[np.isfinite(df['x']) & np.isfinite(df['y'])].reset_index(drop=True)
+    out = dict(K=scene.K, D=scene.D, R=scene.R, t=scene.t, res=np.array(scene.res), n_frames=n_frames,
+               start_frame=start_frame, thresh=0.5, marker_names=np.array(seq.markers),
+               **_df_arrays(df, seq.markers))
+
+    # --- core.tri -> app.save_tri -> utils.save_3d_cheetah_as_2d
+    cap = {}
+    orig_save = ref_tri.utils.save_optimised_cheetah
+
+    def save_spy(positions, out_fpath, extra_data=None, **k):
+        cap.update(positions=np.array(positions, np.float64), fname=os.path.basename(out_fpath),
+                   extra=dict(extra_data or {}))
+    ref_tri.utils.save_optimised_cheetah = save_spy
+    cam_params = (scene.K, scene.D, scene.R, scene.t, tuple(scene.res), C)
+    try:
+        with _HdfCapture() as hc:
+            fp = ref_tri.tri(data_dir, df, start_frame, start_frame + n_frames - 1, 0.5, cam_params, scene_path)
+    finally:
+        ref_tri.utils.save_optimised_cheetah = orig_save
+    out['tri_out_fname'] = np.array(os.path.relpath(fp, data_dir))
+    out['tri_positions'] = cap['positions']
+    out['tri_pickle_fname'] = np.array(cap['fname'])
+    out['tri_start_frame'] = np.array(cap['extra']['start_frame'])
+    out['tri_extra_keys'] = np.array(sorted(cap['extra']))
+    tri_markers = ref_misc.get_markers(mode='all') + ['coe', 'gaze_target']
+    out['tri_markers'] = np.array(tri_markers)
+    for c, e in cap['extra']['errors'].items():
+        out[f'tri_err{c}'] = e[['frame', 'camera_distance', 'pixel_residual', 'pck_threshold', 'error_u',
+                               'error_v']].to_numpy().astype(np.float64)
+        out[f'tri_err{c}_marker'] = e['marker'].to_numpy().astype(str)
+    with open(os.path.join(data_dir, 'tri', 'reconstruction_params.json')) as f:
+        out['tri_params_json'] = np.array(f.read())
+    _frame_arrays('tri2d', hc.frames, os.path.join(data_dir, 'tri'), out)
+
+    # --- save_3d_cheetah_as_2d, FTE-style list of per-camera arrays
+    rng = np.random.default_rng(seed + 7)
+    fte_dir = os.path.join(data_dir, 'fte')
+    os.makedirs(fte_dir)
+    L2 = 5
+    bodyparts = ['nose', 'r_eye', 'l_eye', 'coe', 'gaze_target']
+    pos = []
+    for c in range(C):
+        p = np.array([1.9, 6.4, 0.6]) + rng.normal(0, 0.4, (n_frames, L2, 3))
+        p[rng.random((n_frames, L2)) < 0.1] = np.nan                      # missing points
+        p[0, 1] = [1.9, 6.4, 40.0]                                        # far above: outside the image
+        p[1, 2] = (-scene.R[c].T @ scene.t[c]).ravel() - 0.5 * scene.R[c][2]  # behind camera c
+        p[2, 0] = [1.9 + 30.0 * (c % 2), 6.4 - 30.0 * (c // 3), 0.6]        # wide angle
+        pos.append(p)
+    with _HdfCapture() as hc:
+        ref_utils.save_3d_cheetah_as_2d(pos, fte_dir, scene_path, list(bodyparts), ref_calib.project_points_fisheye,
+                                        start_frame)
+    out['fte_pos'] = np.array(pos)
+    out['fte_bodyparts'] = np.array(bodyparts)
+    _frame_arrays('fte2d', hc.frames, fte_dir, out)
+
+    # --- single array (save_sba / save_ekf form), out_fname given, no CSV
+    with _HdfCapture() as hc:
+        ref_utils.save_3d_cheetah_as_2d(pos[0], fte_dir, scene_path, list(bodyparts), ref_calib.project_points_fisheye,
+                                        start_frame, save_as_csv=False, out_fname='custom')
+    out['one_n'] = np.array(len(hc.frames))
+    for i, (fname, key, d) in enumerate(hc.frames):
+        out[f'one{i}_fname'] = np.array(fname)
+        out[f'one{i}_key'] = np.array(key)
+        out[f'one{i}_values'] = d.to_numpy(np.float64)
+    np.savez_compressed(os.path.join(HERE, 'save2d_tri.npz'), **out)
+    print(f'save2d_tri: tri {cap["positions"].shape}, {len(out["fte_pos"])} cameras of fte-style projections')
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['loss', 'fk', 'tri', 'cfg1', 'cfg2', 'ext']
+    if 'save2d' in which:
+        save2d_tri_fixture()
     if 'dlc' in which:
         dlc_fixture()
     if 'fte' in which:
