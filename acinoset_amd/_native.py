@@ -71,6 +71,19 @@ class EkfInitSpec(C.Structure):
     _fields_ = [(k, C.c_int32) for k in ('nose', 'lure', 'x0', 'y0', 'psi0', 'xl', 'yl', 'from_sba')]
 
 
+def ekf_numerics_mode(ref_numerics, jacobian):
+    """The C ABI's EKF measurement-model mode: 1 = the reference's float32 numerics with the
+    forward-difference H, 0 = the same H in float64, ACS_EKF_ANALYTIC_H (2) = the analytic H
+    (float64 only)."""
+    if jacobian == 'analytic':
+        if ref_numerics:
+            raise ValueError("jacobian='analytic' runs in float64: pass ref_numerics=False")
+        return 2
+    if jacobian != 'fd':
+        raise ValueError(f"jacobian must be 'fd' or 'analytic', not {jacobian!r}")
+    return int(bool(ref_numerics))
+
+
 def ekf_init_spec(table, obs_markers, from_sba=False):
     """The pipeline's init descriptor for EKF skeleton `table` on observations whose marker
     order is `obs_markers`."""
@@ -371,7 +384,7 @@ class Context:
 
     # ---- f2: EKF + RTS smoother ----------------------------------------------------------
     def ekf_run(self, table, cams, meas, likelihood, fps, thresh, max_pixel_err, r_std_base, Q, P0, s0,
-                ref_numerics=True, eps=1e-3, covariances=False):
+                ref_numerics=True, eps=1e-3, covariances=False, jacobian='fd'):
         """meas (S, N, C, L, 2) or (N, C, L, 2); returns dict of x_pred, x_est, x_smooth
         (S, N, n) [, P_est, P_smooth (S, N, n, n)], outliers (S,)."""
         cams = _c64(cams)
@@ -393,7 +406,7 @@ class Context:
         self.check(self.lib.acs_ekf_run(self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), _ptr(cams), Cn,
                                         _ptr(meas), _ptr(lik), S, N, float(fps), float(thresh), float(max_pixel_err),
                                         _ptr(_c64(r_std_base)), _ptr(_c64(Q)), _ptr(_c64(P0)), _ptr(s0),
-                                        int(bool(ref_numerics)), float(eps), _ptr(out['x_pred']), _ptr(out['x_est']),
+                                        ekf_numerics_mode(ref_numerics, jacobian), float(eps), _ptr(out['x_pred']), _ptr(out['x_est']),
                                         _ptr(out['x_smooth']), _ptr(out.get('P_est')), _ptr(out.get('P_smooth')),
                                         _ptr(outl), 0), 'acs_ekf_run')
         out['outliers'] = outl
@@ -403,7 +416,7 @@ class Context:
 
     # ---- configs[4]: SBA + EKF fused ------------------------------------------------
     def sba_ekf_pipeline(self, table, cams, meas, likelihood, obs_markers, fps, thresh, max_pixel_err, r_std_base, Q,
-                         P0, sba_opts=None, from_sba=False, ref_numerics=True, eps=1e-3):
+                         P0, sba_opts=None, from_sba=False, ref_numerics=True, eps=1e-3, jacobian='fd'):
         """acs_sba_ekf_pipeline on host arrays: meas (S, N, C, Lobs, 2), likelihood (S, N, C,
         Lobs) with markers `obs_markers`; the EKF runs skeleton `table` (its markers a subset of
         obs_markers). Returns dict pts (S, N, Lobs, 3), x_est, x_smooth (S, N, 3P), outliers
@@ -428,13 +441,13 @@ class Context:
         self.check(self.lib.acs_sba_ekf_pipeline(
             self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), _ptr(cams), Cn, _ptr(meas), _ptr(lik), S, N, Lo,
             _ptr(emap), float(fps), float(thresh), float(max_pixel_err), _ptr(_c64(r_std_base)), _ptr(_c64(Q)),
-            _ptr(_c64(P0)), C.byref(opts), C.byref(spec), int(bool(ref_numerics)), float(eps), _ptr(pts), _ptr(xe),
+            _ptr(_c64(P0)), C.byref(opts), C.byref(spec), ekf_numerics_mode(ref_numerics, jacobian), float(eps), _ptr(pts), _ptr(xe),
             _ptr(xs), _ptr(outl), C.byref(rep), 0), 'acs_sba_ekf_pipeline')
         return dict(pts=pts, x_est=xe, x_smooth=xs, outliers=outl, sba=rep.as_dict())
 
     def sba_ekf_pipeline_dev(self, table, obs_markers, cams_p, n_cams, meas_p, lik_p, S, N, fps, thresh,
                              max_pixel_err, rstd_p, Q_p, P0_p, pts_p, xe_p, xs_p, sba_opts=None, from_sba=False,
-                             ref_numerics=True, eps=1e-3, report=False):
+                             ref_numerics=True, eps=1e-3, report=False, jacobian='fd'):
         """acs_sba_ekf_pipeline on HBM-resident arrays (device pointers, asynchronous unless
         `report`: then waits and returns (sba report dict, outliers (S,)))."""
         obs = list(obs_markers)
@@ -449,7 +462,7 @@ class Context:
         self.check(self.lib.acs_sba_ekf_pipeline(
             self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), P_(cams_p), n_cams, P_(meas_p), P_(lik_p), S, N,
             len(obs), _ptr(emap), float(fps), float(thresh), float(max_pixel_err), P_(rstd_p), P_(Q_p), P_(P0_p),
-            C.byref(opts), C.byref(spec), int(bool(ref_numerics)), float(eps), P_(pts_p), P_(xe_p), P_(xs_p),
+            C.byref(opts), C.byref(spec), ekf_numerics_mode(ref_numerics, jacobian), float(eps), P_(pts_p), P_(xe_p), P_(xs_p),
             _ptr(outl), C.byref(rep) if report else None, ACS_DEVICE_PTRS), 'acs_sba_ekf_pipeline')
         return (rep.as_dict(), outl) if report else None
 

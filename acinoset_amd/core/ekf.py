@@ -119,9 +119,11 @@ def initial_state(points_3d_df, mode, start_frame, fps):
 
 
 def run(meas, likelihood, camera_params, mode, fps, s0, dlc_thresh=0.5, ref_numerics=True, cal_covs=None,
-        covariances=False, ctx=None):
+        covariances=False, ctx=None, jacobian='fd'):
     """The filter + smoother on (N, C, L, 2) observations from state s0: returns the
-    dict of acinoset_amd._native.Context.ekf_run."""
+    dict of acinoset_amd._native.Context.ekf_run. `jacobian`: 'fd' = the reference's
+    forward-difference H (src/core/ekf.py:81-96), 'analytic' = H from the FK Jacobian
+    (float64, so with ref_numerics=False)."""
     ctx = ctx or _native.default_context()
     k_arr, d_arr, r_arr, t_arr, cam_res, n_cams = camera_params
     cams = _native.pack_cameras(k_arr, np.asarray(d_arr).reshape(-1, 4), r_arr, np.asarray(t_arr).reshape(-1, 3))
@@ -130,14 +132,16 @@ def run(meas, likelihood, camera_params, mode, fps, s0, dlc_thresh=0.5, ref_nume
     sT = 1.0 / fps
     return ctx.ekf_run(table, cams, meas, likelihood, fps, dlc_thresh, float(cam_res[0]),
                        measurement_std(n_cams, cal_covs), process_covariance(P, sT), initial_covariance(mode), s0,
-                       ref_numerics=ref_numerics, covariances=covariances)
+                       ref_numerics=ref_numerics, covariances=covariances, jacobian=jacobian)
 
 
 def ekf(DATA_DIR, points_2d_df, marker_mode, camera_params, start_frame, end_frame, dlc_thresh, scene_fpath,
-        params: Dict = {}, ref_numerics=True, cal_covs=None) -> str:
+        params: Dict = {}, ref_numerics=True, cal_covs=None, jacobian='fd') -> str:
     """`src/core/ekf.py:26` signature and outputs (OUT_DIR/ekf/ekf.pickle). `cal_covs`
     (extension): per-camera calibration covariances; None = the reference's six values,
-    or `ring_cal_covs(n_cams)` for a rig that is not six cameras."""
+    or `ring_cal_covs(n_cams)` for a rig that is not six cameras. `jacobian` (extension):
+    'analytic' replaces the forward-difference H by the FK Jacobian (needs
+    ref_numerics=False)."""
     OUT_DIR = os.path.join(DATA_DIR, 'ekf')
     os.makedirs(OUT_DIR, exist_ok=True)
     app.start_logging(os.path.join(OUT_DIR, 'ekf.log'))
@@ -159,7 +163,7 @@ def ekf(DATA_DIR, points_2d_df, marker_mode, camera_params, start_frame, end_fra
         cal_covs = ring_cal_covs(n_cams)
         print(f'\t{n_cams} cameras: calibration covariances {cal_covs} (reference values by camera mod 6)')
     out = run(meas[start_frame:end_frame + 1], lik[start_frame:end_frame + 1], camera_params, marker_mode, fps, s0,
-              dlc_thresh, ref_numerics, cal_covs=cal_covs)
+              dlc_thresh, ref_numerics, cal_covs=cal_covs, jacobian=jacobian)
     opt_time = time() - t0
     app.stop_logging()
     xe, xs = out['x_est'], out['x_smooth']

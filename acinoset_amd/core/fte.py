@@ -157,6 +157,10 @@ def fte(OUT_DIR, points_2d_df, mode, camera_params, start_frame, end_frame, dlc_
             'z': pos[:, :len(markers), 2].T.ravel()}))
     pix_errors = metric.residual_error(points_2d_df, points_3d_dfs, markers, camera_params)
     states['reprj_errors'] = pix_errors
-    states['solver_report'] = rep
+    # fte.pickle keeps the reference's schema (src/core/fte.py:540-579); the LM report (status,
+    # iterations, costs) goes beside it
+    with open(os.path.join(OUT_DIR, 'solver_report.json'), 'w') as f:
+        json.dump({k: (v.tolist() if isinstance(v, np.ndarray) else v) for k, v in rep.items()}, f,
+                  default=lambda o: o.item() if hasattr(o, 'item') else str(o))
     return app.save_fte(states, mode, OUT_DIR, scene_fpath, start_frame, directions=True, intermode=intermode,
                         save_videos=video)

@@ -205,7 +205,7 @@ struct Walk2 {
   }
 };
 
-template <bool F32>
+template <bool F32, bool AH>
 __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __restrict__ I,
                                                     const double* __restrict__ Rl, const double* __restrict__ cams,
                                                     const double* __restrict__ meas, const double* __restrict__ lik,
@@ -320,6 +320,27 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     }
 
     EKF_TICK(1);
+    const int CL = d.C * d.L;
+    if constexpr (AH) {
+      // ---- 2'. analytic H: one FK with its Jacobian (fk.hpp) and the
+      // projection with its 2x3 world Jacobian; H row r = J_proj(obs) . d pos / d x_q.
+      // hpose[0, m): h(x); hpose[m + 6 o ..]: the projection Jacobian of observation o
+      FkShared& fsh = *reinterpret_cast<FkShared*>(fkb);
+      fk_frame<false>(sk, ss, fsh, tid, nth);
+      __syncthreads();
+      for (int o = tid; o < CL; o += nth) {
+        const int c = o / d.L, l = o - c * d.L;
+        const double* x = fsh.pos[sk.outn[l]];
+        ProjOut po;
+        fisheye_project<true>(cams + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
+        hpose[2 * o] = po.u;
+        hpose[2 * o + 1] = po.v;
+        double* jo = hpose + m + 6 * (size_t)o;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) jo[k] = po.J[k];
+      }
+      __syncthreads();
+    } else {
     // ---- 2. poses of the forward-difference Jacobian --------------------------------
     {
 #ifdef EKF_PROFILE
@@ -330,7 +351,6 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       if (tid == 0) s_prof[7] += clock64() - tf0;  // FK share of the FK/proj phase
 #endif
       const double* pos = fkb + FK_MAXJ * 9 + (FK_MAXP + 1) * 9 + (size_t)(P + 1) * d.J * 9;
-      const int CL = d.C * d.L;
       for (int e = tid; e < (P + 1) * CL; e += nth) {
         const int q = e / CL, o = e - q * CL;
         const int c = o / d.L, l = o - c * d.L;
@@ -341,6 +361,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
         hpose[(size_t)q * m + 2 * o + 1] = po.v;
       }
       __syncthreads();
+    }
     }
     EKF_TICK(2);
     // residual and R^-1 per row (row r = 2 (c L + l) + d, the reference's ordering; rows
@@ -363,7 +384,17 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     for (int e = tid; e < mp * Pp; e += nth) {
       const int r = e / Pp, q = e - r * Pp;
       double hq = 0.0;
-      if (r < m && q < P) hq = (hpose[(size_t)(q + 1) * m + r] - hpose[r]) / d.eps;
+      if constexpr (AH) {
+        if (r < m && q < P) {
+          const int o = r >> 1, l = o % d.L;
+          const double* jr = hpose + m + 6 * (size_t)o + 3 * (r & 1);
+          double dp[3];
+          fk_dpos(sk, *reinterpret_cast<const FkShared*>(fkb), sk.outn[l], q, dp);
+          hq = jr[0] * dp[0] + jr[1] * dp[1] + jr[2] * dp[2];
+        }
+      } else {
+        if (r < m && q < P) hq = (hpose[(size_t)(q + 1) * m + r] - hpose[r]) / d.eps;
+      }
       H[e] = hq;
       HW[e] = wr[r] * hq;
     }
@@ -871,12 +902,19 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
   const size_t lds_f = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + U + d.npad +
                                           n_reals + (n_ints + 1) / 2 + 1);
   ACS_CHECK(ctx, lds_f <= 160 * 1024, "ekf: P = %d needs %zu bytes of LDS", P, lds_f);
-  if (ref_numerics)
-    hipLaunchKernelGGL(k_ekf_filter<true>, dim3(n_seq), dim3(512), lds_f, s, d, io.I, io.R, io.cams, io.meas, io.lik,
-                       io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof);
+  ACS_CHECK(ctx, ref_numerics >= 0 && ref_numerics <= ACS_EKF_ANALYTIC_H, "ekf: numerics mode %d", ref_numerics);
+  // analytic H: the FkShared of one FK lives in the batched-FK region of the LDS union
+  ACS_CHECK(ctx, ekf_fk_lds(P, Jn, L) * sizeof(double) >= sizeof(FkShared), "ekf: FK region too small");
+#define EKF_FILTER(f32, ah)                                                                                       \
+  hipLaunchKernelGGL((k_ekf_filter<f32, ah>), dim3(n_seq), dim3(512), lds_f, s, d, io.I, io.R, io.cams, io.meas, \
+                     io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof)
+  if (ref_numerics == ACS_EKF_ANALYTIC_H)
+    EKF_FILTER(false, true);
+  else if (ref_numerics)
+    EKF_FILTER(true, false);
   else
-    hipLaunchKernelGGL(k_ekf_filter<false>, dim3(n_seq), dim3(512), lds_f, s, d, io.I, io.R, io.cams, io.meas, io.lik,
-                       io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof);
+    EKF_FILTER(false, false);
+#undef EKF_FILTER
   ACS_HIP(ctx, hipGetLastError());
   const size_t lds_s = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + 512 + d.npad);
   if (dPs) {

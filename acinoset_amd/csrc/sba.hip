@@ -104,11 +104,13 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
       pts[3 * p] = x0;
       pts[3 * p + 1] = x1;
       pts[3 * p + 2] = x2;
-      cost0[p] = 0.0;
-      cost1[p] = 0.0;
-      stat[3 * p] = ACS_STATUS_NOOBS;
-      stat[3 * p + 1] = 0;
-      stat[3 * p + 2] = 0;
+      if (stat) {
+        cost0[p] = 0.0;
+        cost1[p] = 0.0;
+        stat[3 * p] = ACS_STATUS_NOOBS;
+        stat[3 * p + 1] = 0;
+        stat[3 * p + 2] = 0;
+      }
     }
     return;
   }
@@ -254,11 +256,15 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     pts[3 * p] = x0;
     pts[3 * p + 1] = x1;
     pts[3 * p + 2] = x2;
-    cost0[p] = F_before;
-    cost1[p] = F;
-    stat[3 * p] = status;
-    stat[3 * p + 1] = iters;
-    stat[3 * p + 2] = nfev;
+    // the per-point costs and status feed k_sba_report only: not written (28 B per point)
+    // when no report is asked for
+    if (stat) {
+      cost0[p] = F_before;
+      cost1[p] = F;
+      stat[3 * p] = status;
+      stat[3 * p + 1] = iters;
+      stat[3 * p + 2] = nfev;
+    }
   }
 }
 
@@ -415,7 +421,7 @@ static int launch_lm_g(acs_ctx* ctx, int G, int blocks, int block, const double*
 // from dpts_in, solution to dpts (may alias).
 static int run_lm(acs_ctx* ctx, const double* dcams, int C, int K, const double2* duv, const uint8_t* dmask,
                   const uint8_t* dcamid, int64_t n_pts, const double* dpts_in, double* dpts,
-                  const acs_sba_opts* opts, double** c0_out,
+                  const acs_sba_opts* opts, bool report, double** c0_out,
                   double** c1_out, int** st_out) {
   acs_sba_opts o;
   acs_sba_default_opts(&o);
@@ -424,10 +430,14 @@ static int run_lm(acs_ctx* ctx, const double* dcams, int C, int K, const double2
   ACS_CHECK(ctx, K >= 1 && K <= 256, "observations per point (%d) must be in [1, 256]", K);
   ACS_CHECK(ctx, C >= 1 && C <= 255, "n_cams (%d) must be in [1, 255]", C);
   SbaParams prm{o.max_iters, o.f_scale, o.ftol, o.xtol, o.gtol};
-  double* c0 = (double*)acs_ws(ctx, WS_PERPT_F0, sizeof(double) * n_pts);
-  double* c1 = (double*)acs_ws(ctx, WS_PERPT_F1, sizeof(double) * n_pts);
-  int* st = (int*)acs_ws(ctx, WS_PERPT_I, sizeof(int) * 3 * n_pts);
-  if (!c0 || !c1 || !st) return ACS_E_NOMEM;
+  double *c0 = nullptr, *c1 = nullptr;
+  int* st = nullptr;
+  if (report) {
+    c0 = (double*)acs_ws(ctx, WS_PERPT_F0, sizeof(double) * n_pts);
+    c1 = (double*)acs_ws(ctx, WS_PERPT_F1, sizeof(double) * n_pts);
+    st = (int*)acs_ws(ctx, WS_PERPT_I, sizeof(int) * 3 * n_pts);
+    if (!c0 || !c1 || !st) return ACS_E_NOMEM;
+  }
   int G = next_pow2(K < 2 ? 2 : K);
   int S = 1;
   if (G > 64) {
@@ -479,7 +489,9 @@ int acs_sba_dense_enqueue(acs_ctx* ctx, const double* dcams, int C, const double
   double *c0, *c1;
   int* st;
   int rc;
-  if ((rc = run_lm(ctx, dcams, C, C, duv, dmask, nullptr, n_pts, dpts_in, dpts_out, opts, &c0, &c1, &st))) return rc;
+  if ((rc = run_lm(ctx, dcams, C, C, duv, dmask, nullptr, n_pts, dpts_in, dpts_out, opts, report != nullptr, &c0, &c1,
+                   &st)))
+    return rc;
   if (report) return run_report(ctx, c0, c1, st, n_pts, report);
   return ACS_OK;
 }
@@ -555,7 +567,7 @@ int acs_sba_points_dense_io(acs_ctx* ctx, const double* cams, int32_t n_cams, co
   double *c0, *c1;
   int* st;
   if ((rc = run_lm(ctx, (const double*)dc, n_cams, n_cams, (const double2*)duv, (const uint8_t*)dm, nullptr, n_pts,
-                   (const double*)dpi, dpo, opts, &c0, &c1, &st)))
+                   (const double*)dpi, dpo, opts, report != nullptr, &c0, &c1, &st)))
     return rc;
   if ((rc = acs_stage_out(ctx, pts_out, dpo, sizeof(double) * 3 * n_pts, flags))) return rc;
   if (report) {
@@ -611,8 +623,8 @@ int acs_sba_points(acs_ctx* ctx, const double* cams, int32_t n_cams, const doubl
 
   double *c0, *c1;
   int* st;
-  if ((rc = run_lm(ctx, (const double*)dc, n_cams, K, uvp, mk, cid, n_pts, (const double*)dp, (double*)dp, opts, &c0,
-                   &c1, &st)))
+  if ((rc = run_lm(ctx, (const double*)dc, n_cams, K, uvp, mk, cid, n_pts, (const double*)dp, (double*)dp, opts,
+                   report != nullptr, &c0, &c1, &st)))
     return rc;
 
   double* dra = nullptr;

@@ -515,7 +515,8 @@ def bench_pipeline(ctx, torch, stream, world, rank, n_seq=80, n_frames=250, n_ca
     frames (80 x 250 = 20,000 frames, ~2.8 s clips at 90 fps) on the synthesised 12-camera ring,
     20 DLC keypoints per frame. One step = acs_sba_ekf_pipeline on the HBM-resident observation
     tensor: pairwise triangulation + points-only SBA of every keypoint (core.sba), the EKF initial
-    state fitted on the SBA points, and the EKF + RTS smoother (core.ekf) with the head model on
+    state fitted on the pairwise-triangulated points as core.ekf does (src/core/ekf.py:121-157;
+    from_sba=False, the reference's semantics), and the EKF + RTS smoother (core.ekf) with the head model on
     its three markers (the 29-parameter 'default' model loses these sequences; see the ekf legs).
     Weak scaling: every rank runs its own clips (the EKF is sequential in time; clips are the
     parallel unit, no collective)."""

@@ -45,6 +45,9 @@ extern "C" {
 #define ACS_DEVICE_PTRS 1u  /* array arguments are device pointers; call is async */
 
 /* per-problem convergence status (acs_report.status_counts index / oracle/sba.py) */
+/* acs_ekf_run / acs_sba_ekf_pipeline measurement-model mode (their ref_numerics argument) */
+#define ACS_EKF_ANALYTIC_H 2
+
 #define ACS_STATUS_RUNNING 0
 #define ACS_STATUS_GTOL 1
 #define ACS_STATUS_FTOL 2
@@ -291,8 +294,12 @@ int acs_sba_ext_dist_destroy(acs_sba_ext_dist* h);
  * [x, dx, ddx]. meas (n_seq, n_frames, n_cams, L, 2) pixels (NaN = missing), likelihood
  * (n_seq, n_frames, n_cams, L); R = diag(s^2) with s = r_std_base[cam] (the reference's
  * 2 cov_c / min cov, :244-248) or max_pixel_err below `thresh`. Q, P0: n x n; s0: (n_seq, n).
- * ref_numerics != 0 reproduces the reference's float32 prediction cast and float32
- * Jacobian perturbation (:79, :81-96); eps = the forward-difference step (1e-3).
+ * ref_numerics (the measurement-model mode): 1 reproduces the reference's float32
+ * prediction cast and float32 Jacobian perturbation (:79, :81-96; eps = the forward-
+ * difference step, 1e-3); 0 is the same forward-difference H in float64;
+ * ACS_EKF_ANALYTIC_H (2) replaces the P+1 forward-difference poses by the analytic H
+ * (SURVEY §8(f)2): one FK with its Jacobian d pos / d x, times the projection's 2 x 3
+ * Jacobian, in float64 (eps unused).
  * Outputs (n_seq, n_frames, n) x_pred (may be NULL), x_est, x_smooth; (.., n, n) P_est,
  * P_smooth (may be NULL); outliers (n_seq) = the reference's 3-sigma count (may be NULL). */
 int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,

@@ -120,12 +120,27 @@ def initial_state(mode, frames, markers_idx, xyz, start_frame, sT):
     return s
 
 
+def analytic_jacobian(x, mode, K, D, R, t):
+    """The analytic measurement Jacobian (replacing :81-96): h(x) and
+    H = d proj / d X (oracle.fisheye.project_jac) times d pos / d x (the exact FK Jacobian,
+    oracle.kinematics.marker_jacobian), float64. Returns (h (2L,), H (2L, P))."""
+    from .fisheye import project_jac
+    from .kinematics import marker_jacobian
+    x = np.asarray(x, np.float64)
+    pos = marker_positions(mode, x[None])[0]                       # (L, 3)
+    Jfk = marker_jacobian(mode, x[None])[0]                        # (L, 3, P)
+    uv, Jp = project_jac(pos, K, D, R, t)                          # (L, 2), (L, 2, 3)
+    return uv.ravel(), np.einsum('lik,lkp->lip', Jp, Jfk).reshape(-1, x.size)
+
+
 def ekf(meas, likelihood, K, D, R, t, mode, fps, s0, thresh=0.5, max_pixel_err=2704.0, ref_numerics=True,
-        cal_covs=None):
+        cal_covs=None, jacobian='fd'):
     """meas (N, C, L, 2) pixels (NaN = missing), likelihood (N, C, L). Returns a dict with
     the filtered / predicted / smoothed states and covariances and the outlier count.
     `cal_covs`: per-camera calibration covariances (default: the reference's six, :210;
-    the reference asserts six cameras, :213, other rigs pass their own)."""
+    the reference asserts six cameras, :213, other rigs pass their own). `jacobian`:
+    'fd' (the reference's forward differences) or 'analytic' (float64 only)."""
+    assert jacobian == 'fd' or not ref_numerics, 'the analytic H runs in float64'
     N, C, L, _ = meas.shape
     P = len(POSE[mode])
     n = 3 * P
@@ -147,9 +162,11 @@ def ekf(meas, likelihood, K, D, R, t, mode, fps, s0, thresh=0.5, max_pixel_err=2
         H = np.zeros((2 * C * L, n))
         h = np.zeros(2 * C * L)
         for c in range(C):
-            h[c * 2 * L:(c + 1) * 2 * L], H[c * 2 * L:(c + 1) * 2 * L, :P] = fd_jacobian(s[:P], mode, K[c], D[c],
-                                                                                        R[c], t[c],
-                                                                                        ref_numerics=ref_numerics)
+            if jacobian == 'analytic':
+                hc, Hc = analytic_jacobian(s[:P], mode, K[c], D[c], R[c], t[c])
+            else:
+                hc, Hc = fd_jacobian(s[:P], mode, K[c], D[c], R[c], t[c], ref_numerics=ref_numerics)
+            h[c * 2 * L:(c + 1) * 2 * L], H[c * 2 * L:(c + 1) * 2 * L, :P] = hc, Hc
         r_std = base.copy()
         r_std[np.repeat(likelihood[i].ravel() < thresh, 2)] = max_pixel_err
         Rm = np.diag(r_std ** 2)

@@ -178,3 +178,35 @@ def test_core_ekf_dropin_12cam(ctx, tmp_path):
     pos = np.array(d['smoothed_positions'])[:, :3]
     err = np.sqrt(np.mean(np.sum((pos - seq.pos3d[:, 0, :3]) ** 2, -1)))
     assert err < 0.05, err
+
+
+@pytest.mark.parametrize('n_cams,mode,N', [(6, 'head', 40), (12, 'head', 40), (6, 'default', 8), (12, 'default', 8)])
+def test_ekf_analytic_h_matches_oracle(ctx, n_cams, mode, N):
+    """The analytic measurement Jacobian (H from the FK Jacobian instead of
+    the P+1 forward-difference poses of src/core/ekf.py:81-96), float64, against the
+    oracle's restatement (oracle.ekf.analytic_jacobian: the exact FK Jacobian by complex
+    step times the projection Jacobian) at the float64 tolerances above."""
+    if n_cams == 12:
+        scene, seq, s0, cp, covs = _setup_ring(mode, N)
+        uv, lik = seq.uv, seq.likelihood
+        K, D, R, t, res = scene.K, scene.D, scene.R, scene.t, scene.res
+    else:
+        g, s0, cp = _setup(mode)
+        uv, lik, covs = g['uv'][:N], g['likelihood'][:N], None
+        K, D, R, t, res = g['K'], g['D'], g['R'], g['t'], g['res']
+    out = cekf.run(uv, lik, cp, mode, 90.0, s0, ref_numerics=False, cal_covs=covs, covariances=True, ctx=ctx,
+                   jacobian='analytic')
+    o = oekf.ekf(uv, lik, K, D, R, t, mode, 90.0, s0, 0.5, float(res[0]), ref_numerics=False, cal_covs=covs,
+                 jacobian='analytic')
+    P = len(pkin.get_pose_params(mode))
+    _check(out, P, o['x_est'][:, :P], o['x_est'][:, P:2 * P], o['x_est'][:, 2 * P:], o['x_smooth'][:, :P],
+           scale=1.0 if mode == 'head' else 10.0)
+    assert abs(int(out['outliers']) - o['outliers']) <= 1
+    sc = np.abs(o['P_est'][:3]).max()
+    np.testing.assert_allclose(out['P_est'][:3], o['P_est'][:3], atol=(1e-6 if mode == 'head' else 1e-4) * sc, rtol=0)
+
+
+def test_ekf_analytic_h_rejects_reference_numerics(ctx):
+    g, s0, cp = _setup('head')
+    with pytest.raises(ValueError, match='float64'):
+        cekf.run(g['uv'][:3], g['likelihood'][:3], cp, 'head', 90.0, s0, ctx=ctx, jacobian='analytic')

@@ -1,0 +1,79 @@
+"""Oracle parity at the benched sizes (configs[3] and configs[4]), not only at reduced sizes.
+
+* configs[3]: the 6-cam x 10,000-frame FTE of the bench's `fte_window` leg
+  (`workloads.fte_workload`, seed 77, shutter delay 'const', interpolation 'vel') solved by
+  `acs_fte_solve` and by the oracle LM (oracle/fte.py, the restatement of
+  src/core/fte.py:176-555) from the same reference initialisation (:254-292). Tolerances as
+  configs[2] (`test_gpu_fte_cfg2.py`): same status and iteration count, keypoints < 1e-6 m
+  RMS, reprojection RMS within 1e-3 px, tau within 1e-6 s, final cost 1e-9 relative. The
+  oracle needs about a minute of one host core for this size.
+* configs[4]: the bench's `sba_ekf_pipeline` step itself (80 clips x 250 frames on the
+  12-camera ring, rank 0's seeds) through `acs_sba_ekf_pipeline`; four clips drawn at random
+  (seeded) are re-run through the oracle pieces chained (pairwise triangulation ->
+  points-only SBA -> EKF initial state -> EKF + RTS, src/core/sba.py:27-70 then
+  src/core/ekf.py:26-298) at `test_gpu_pipeline.py`'s tolerances.
+"""
+import importlib
+
+import numpy as np
+import pytest
+
+from oracle import fte as ofte, kinematics as okin
+from acinoset_amd import _native, kinematics as pkin, synth, workloads
+
+from test_gpu_pipeline import TOL, _oracle
+
+pytestmark = pytest.mark.gpu
+cekf = importlib.import_module('acinoset_amd.core.ekf')
+
+
+@pytest.mark.timeout(600)
+def test_cfg3_fte_10k_frames_matches_oracle(ctx):
+    wl = workloads.fte_workload(ctx, 10000)
+    sc = wl.scene
+    X, tau, rep = ctx.fte_solve(wl.table, wl.cams, wl.meas, wl.w, wl.Ts, wl.qinv, wl.X0, shutter_delay=True,
+                                intermode=1)
+    prob = ofte.Problem('default_nolure', wl.meas, wl.w, sc.K, sc.D, sc.R, sc.t, wl.Ts, sd=True, intermode='vel')
+    Xo, to, info = ofte.solve(prob, wl.X0)
+    assert rep['status_name'] == info['status'], (rep, info)
+    assert rep['iters'] == info['iters'] and rep['n_accepted'] == info['n_accepted'], (rep, info)
+    pg = okin.marker_positions('default_nolure', X[2:])
+    po = okin.marker_positions('default_nolure', Xo[2:])
+    kp_rms = float(np.sqrt(np.mean(np.sum((pg - po) ** 2, -1))))
+    assert kp_rms < 1e-6, kp_rms
+    rg = workloads.fte_reproj_rms(ctx, wl, X, tau)
+    ro = workloads.fte_reproj_rms(ctx, wl, Xo, to)
+    assert abs(rg - ro) < 1e-3, (rg, ro)
+    np.testing.assert_allclose(tau, to, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(rep['cost_after'], info['cost_after'], rtol=1e-9)
+    assert float(np.sqrt(np.mean(np.sum((pg - wl.seq.pos3d[:, 0]) ** 2, -1)))) < 0.01
+
+
+@pytest.mark.timeout(600)
+def test_cfg4_benched_pipeline_clips_match_oracle(ctx):
+    n_seq, n_frames, n_cams = 80, 250, 12          # bench.py bench_pipeline defaults, rank 0
+    scene = synth.ring_scene(n_cams)
+    seqs = [synth.make_sequence(n_frames, scene, mode='default_nolure', seed=3000 + k) for k in range(n_seq)]
+    uv = np.stack([q.uv for q in seqs])
+    lik = np.stack([q.likelihood for q in seqs])
+    table = pkin.build_table('head')
+    covs = cekf.ring_cal_covs(n_cams)
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    P = table.P
+    out = ctx.sba_ekf_pipeline(table, cams, uv, lik, seqs[0].markers, 90.0, 0.5, float(scene.res[0]),
+                               cekf.measurement_std(n_cams, covs), cekf.process_covariance(P, 1 / 90.0),
+                               cekf.initial_covariance('head'))
+    assert out['sba']['n_problems'] == n_seq * n_frames * 20
+    for k in np.random.default_rng(2024).choice(n_seq, 4, replace=False):
+        pts, s0, o = _oracle(scene, uv[k], lik[k], seqs[k].markers, 'head', 0.5, False, True, covs)
+        g = out['pts'][k]
+        np.testing.assert_array_equal(np.isnan(g), np.isnan(pts))
+        m = ~np.isnan(pts)
+        np.testing.assert_allclose(g[m], pts[m], rtol=0, atol=1e-7)
+        xe, xs = out['x_est'][k], out['x_smooth'][k]
+        np.testing.assert_allclose(xe[0], o['x_est'][0], rtol=0, atol=1e-9)
+        np.testing.assert_allclose(xe[:, :P], o['x_est'][:, :P], rtol=0, atol=TOL['x'])
+        np.testing.assert_allclose(xe[:, P:2 * P], o['x_est'][:, P:2 * P], rtol=0, atol=TOL['dx'])
+        np.testing.assert_allclose(xe[:, 2 * P:], o['x_est'][:, 2 * P:], rtol=0, atol=TOL['ddx'])
+        np.testing.assert_allclose(xs[:, :P], o['x_smooth'][:, :P], rtol=0, atol=TOL['smoothed_x'])
+        assert abs(int(out['outliers'][k]) - o['outliers']) <= 1

@@ -230,6 +230,37 @@ def test_oracle_ekf_matches_reference_default_early_frames():
     np.testing.assert_allclose(out['x_est'][:2, :29], g['out_x'][:2], atol=1e-8, rtol=0)
 
 
+
+@pytest.mark.parametrize('mode', ['head', 'default'])
+def test_oracle_ekf_analytic_jacobian_matches_fd(mode):
+    """The analytic H against central differences of the same float64
+    measurement function, and the analytic-H filter tracking the reference's FD-H run on
+    the head fixture (the two Jacobians differ by the FD truncation, O(eps))."""
+    from oracle import ekf as oekf
+    from acinoset_amd import synth
+    sc = synth.load_scene_file()
+    P = len(pkin.get_pose_params(mode))
+    x = np.random.default_rng(5).normal(0, 0.1, P)
+    x[:3] = [1.9, 6.4, 0.6]
+    for c in range(sc.n_cams):
+        h, H = oekf.analytic_jacobian(x, mode, sc.K[c], sc.D[c], sc.R[c], sc.t[c])
+        Hc = np.empty_like(H)
+        for i in range(P):
+            d = np.zeros(P)
+            d[i] = 1e-6
+            hp = oekf.h_function(x + d, mode, sc.K[c], sc.D[c], sc.R[c], sc.t[c], ref_numerics=False).ravel()
+            hm = oekf.h_function(x - d, mode, sc.K[c], sc.D[c], sc.R[c], sc.t[c], ref_numerics=False).ravel()
+            Hc[:, i] = (hp - hm) / 2e-6
+        np.testing.assert_allclose(h, oekf.h_function(x, mode, sc.K[c], sc.D[c], sc.R[c], sc.t[c],
+                                                      ref_numerics=False).ravel(), rtol=0, atol=1e-9)
+        np.testing.assert_allclose(H, Hc, rtol=0, atol=1e-6 * np.abs(H).max())
+    if mode == 'head':
+        g, s0 = _ekf_golden('head')
+        out = oekf.ekf(g['uv'], g['likelihood'], g['K'], g['D'], g['R'], g['t'], 'head', 90.0, s0, 0.5,
+                       float(g['res'][0]), ref_numerics=False, jacobian='analytic')
+        assert np.sqrt(np.mean((out['x_smooth'][:, :6] - g['out_smoothed_x']) ** 2)) < 1e-2
+
+
 # ---- FTE objective (parity unpinned vs IPOPT, oracle/fte.py): exact gradient and the
 # shutter-delay modes (src/core/fte.py:236-238, :304-318, :447-450)
 def _fte_small(sd_mode, inter, N=6, tau_max=0.004):

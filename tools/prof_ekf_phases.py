@@ -1,6 +1,8 @@
 """Per-phase cycle counts of k_ekf_filter from a library built with -DEKF_PROFILE (the same
 libprof.so as tools/prof_fte_phases.py, with ekf.hip compiled with -DEKF_PROFILE):
-python tools/prof_ekf_phases.py [mode] [n_cams] [frames]   (default: default 6 200)."""
+python tools/prof_ekf_phases.py [mode] [n_cams] [frames] [fd|analytic]   (default: default 6 200 fd;
+'fd' = the reference numerics with the forward-difference H, 'analytic' = the analytic H in float64).
+Build: tools/build_prof.sh ekf."""
 import ctypes as C
 import importlib
 import os
@@ -18,6 +20,7 @@ cekf = importlib.import_module('acinoset_amd.core.ekf')
 mode = sys.argv[1] if len(sys.argv) > 1 else 'default'
 n_cams = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 N = int(sys.argv[3]) if len(sys.argv) > 3 else 200
+jac = sys.argv[4] if len(sys.argv) > 4 else 'fd'
 ctx = _native.Context(0)
 buf = torch.zeros(8, dtype=torch.int64, device='cuda')
 ctx.lib.acs_ekf_prof.argtypes = [C.c_void_p]
@@ -33,10 +36,10 @@ s0[0, :P] = seq.x[0]
 s0[0, P:2 * P] = (seq.x[1] - seq.x[0]) / seq.Ts
 ctx.ekf_run(table, cams, seq.uv[None], seq.likelihood[None],
             90.0, 0.5, float(scene.res[0]), cekf.measurement_std(n_cams, covs), cekf.process_covariance(P, 1 / 90.),
-            cekf.initial_covariance(mode), s0)
+            cekf.initial_covariance(mode), s0, ref_numerics=jac == 'fd', jacobian=jac)
 v = buf.cpu().numpy() / N
 names = ["predict+PFPt", "FK/proj", "H build", "A,G,b,outl", "aug", "GJ", "update", "store+FK-only"]
-print(f'{mode}, {n_cams} cams, {N} frames, one sequence')
+print(f'{mode}, {n_cams} cams, {N} frames, one sequence, H: {jac}')
 for nm, x in zip(names, v):
     print(f'{nm:14s} {x:10.0f} cycles/frame  ({x / 2.4e3:.1f} us @2.4GHz)')
 print(f'{"total":14s} {v.sum():10.0f} cycles/frame  ({v.sum() / 2.4e3:.1f} us @2.4GHz)')
