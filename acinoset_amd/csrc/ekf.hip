@@ -665,6 +665,359 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   if (tid == 0) outliers[seq] = (long long)s_out;
 }
 
+// ---------------------------------------------------------------------------------------
+// Small-state filter: the head model (P = EKF_W1_P = 6 parameters, n = 18) with ONE wave per
+// sequence and the parameter count a compile-time constant. At 6 parameters the per-frame
+// algebra is a few thousand flops, and the 8-wave workgroup of k_ekf_filter spent its frame
+// on barriers and LDS round trips (24 us per 12-camera frame,
+// profiles/r03/ekf_phases_head12.log). Here:
+//   * prediction and the measurement model as k_ekf_filter (same device code: the P F P^T
+//     passes, ekf_fk_batch / fk_frame, the fisheye projection), all scratch in LDS;
+//   * A = H^T R^-1 H and b = H^T R^-1 r one entry per lane (rows split over the half-waves,
+//     one shuffle); the 3-sigma test one observation per lane with P_xx in registers;
+//   * the augmented [I + A P_xx | A P[x,:] | b] column-per-lane (P + n + 1 = 25 columns) and
+//     Gauss-Jordan with partial pivoting on registers: the pivot column's lane finds the
+//     pivot row in its own registers, that column reaches the other lanes by readlane; no
+//     step needs an LDS round trip or a barrier;
+//   * the state / covariance update from register copies of the solution rows.
+// Same algorithm and pivoting rule (largest |a|, lowest row on ties) as k_ekf_filter; the
+// sums are in another order, so results agree to rounding (tests/test_gpu_ekf.py).
+#define EKF_W1_P 6
+
+__host__ __device__ inline size_t ekf_w1_fk_doubles(int P, int J, int L) {
+  const size_t a = ekf_fk_lds(P, J, L), b = (sizeof(FkShared) + 7) / 8;
+  return a > b ? a : b;
+}
+// LDS doubles of k_ekf_filter_w1
+__host__ __device__ inline size_t ekf_w1_lds(const EkfDims& d) {
+  const size_t n = d.n, P = d.P, m = d.m;
+  return n * (n + 1) + d.npad + (P + 1) * m + m * P + 2 * m + n * P + P * (n + 1) + P * P + P +
+         ekf_w1_fk_doubles(d.P, d.J, d.L) + d.n_reals + (d.n_ints + 1) / 2 + 1;
+}
+
+template <bool F32, bool AH, int PM>
+__global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __restrict__ I,
+                                                      const double* __restrict__ Rl, const double* __restrict__ cams,
+                                                      const double* __restrict__ meas, const double* __restrict__ lik,
+                                                      const double* __restrict__ rbase, const double* __restrict__ Q,
+                                                      const double* __restrict__ P0, const double* __restrict__ s0,
+                                                      double* __restrict__ xpred, double* __restrict__ xest,
+                                                      double* __restrict__ Ppred, double* __restrict__ Pest,
+                                                      long long* __restrict__ outliers,
+                                                      unsigned long long* ekf_prof) {
+  constexpr int P = PM, n = 3 * PM, LDP = n + 1, NZ1 = n + 1, NCOL = P + n + 1;
+  static_assert(NCOL <= 64, "one column per lane");
+  const int seq = blockIdx.x;
+  const int tid = threadIdx.x, nth = 64;
+  const int m = d.m, CL = d.C * d.L;
+  extern __shared__ double lds[];
+  double* sP = lds;                                     // n x LDP: covariance
+  double* ss = sP + (size_t)n * LDP;                    // npad: state
+  double* hp = ss + d.npad;                             // (P+1) x m: FD poses' pixels | AH: h + 6 CL Jacobians
+  double* sH = hp + (size_t)(P + 1) * m;                // m x P
+  double* sr = sH + (size_t)m * P;                      // m: residuals
+  double* sw = sr + m;                                  // m: 1 / sd^2
+  double* sPx = sw + m;                                 // n x P: P[:, x] before the update
+  double* sZ = sPx + (size_t)n * P;                     // P x (n + 1): [Z_G | Z_b]
+  double* sA = sZ + (size_t)P * NZ1;                    // P x P, then b (P)
+  double* fkb = sA + P * P + P;                         // FK scratch
+  double* sRl = fkb + ekf_w1_fk_doubles(P, d.J, d.L);   // skeleton table (reals, then ints)
+  int* sI = reinterpret_cast<int*>(sRl + d.n_reals);
+#ifdef EKF_PROFILE
+  unsigned long long s_prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = 0;
+#define EKF_TICK1(k)                                                              \
+  do {                                                                            \
+    __syncthreads();                                                              \
+    const unsigned long long t_now = clock64();                                   \
+    if (t_last) s_prof[(k + 7) % 8] += t_now - t_last;                            \
+    t_last = t_now;                                                               \
+  } while (0)
+#else
+#define EKF_TICK1(k) \
+  do {               \
+  } while (0)
+#endif
+  for (int e = tid; e < d.n_ints; e += nth) sI[e] = I[e];
+  for (int e = tid; e < d.n_reals; e += nth) sRl[e] = Rl[e];
+  for (int e = tid; e < n * LDP; e += nth) {
+    const int r = e / LDP, c = e - r * LDP;
+    sP[e] = c < n ? P0[r * n + c] : 0.0;
+  }
+  for (int r = tid; r < d.npad; r += nth) ss[r] = r < n ? s0[(size_t)seq * n + r] : 0.0;
+  __syncthreads();
+  const SkelView sk = skel_view(sI, sRl);
+  const double sT = d.sT, h2 = 0.5 * sT * sT;
+  const size_t fstride = (size_t)CL;
+  long long nout = 0;
+  constexpr int nA = P * (P + 1) / 2, nAb = nA + P;
+  static_assert(nAb <= 32, "one A / b entry per lane of a half-wave");
+  // this lane's A / b entry: (ea, eb), ea <= eb, row-major upper triangle, then b_ea (eb < 0)
+  int ea = 0, eb = -1;
+  {
+    const int t = tid & 31;
+    if (t < nA) {
+      int tt = t;
+      while (tt >= P - ea) {
+        tt -= P - ea;
+        ++ea;
+      }
+      eb = ea + tt;
+    } else if (t < nAb) {
+      ea = t - nA;
+    }
+  }
+  for (int i = 0; i < d.N; ++i) {
+    const size_t fo = (size_t)seq * d.N + i;
+    EKF_TICK1(0);
+    // ---- 1. prediction (k_ekf_filter's arithmetic) ------------------------------------
+    double sn = 0.0;
+    if (tid < n) {
+      if (tid >= 2 * P) {
+        sn = ss[tid];
+      } else if (tid >= P) {
+        sn = ss[tid] + sT * ss[tid + P];
+      } else {
+        const double vel = ss[tid + P] + sT * ss[tid + 2 * P];
+        sn = ss[tid] + sT * vel + h2 * ss[tid + 2 * P];
+      }
+      if (F32) sn = (double)(float)sn;
+    }
+    __syncthreads();
+    if (tid < n) {
+      ss[tid] = sn;
+      xpred[fo * n + tid] = sn;
+    }
+    for (Walk2 w(tid, nth, n); w.e < P * n; w.next())
+      sP[w.r * LDP + w.c] += sT * sP[(w.r + P) * LDP + w.c] + h2 * sP[(w.r + 2 * P) * LDP + w.c];
+    __syncthreads();
+    for (Walk2 w(tid, nth, n); w.e < P * n; w.next()) sP[(P + w.r) * LDP + w.c] += sT * sP[(w.r + 2 * P) * LDP + w.c];
+    __syncthreads();
+    for (Walk2 w(tid, nth, P); w.e < P * n; w.next())
+      sP[w.r * LDP + w.c] += sT * sP[w.r * LDP + w.c + P] + h2 * sP[w.r * LDP + w.c + 2 * P];
+    __syncthreads();
+    for (Walk2 w(tid, nth, P); w.e < P * n; w.next()) sP[w.r * LDP + P + w.c] += sT * sP[w.r * LDP + w.c + 2 * P];
+    __syncthreads();
+    for (Walk2 w(tid, nth, n); w.e < n * n; w.next()) {
+      const double v = sP[w.r * LDP + w.c] + Q[w.e];
+      sP[w.r * LDP + w.c] = v;
+      Ppred[fo * n * n + w.e] = v;
+    }
+    EKF_TICK1(1);
+    // ---- 2. measurement model ---------------------------------------------------------
+    if constexpr (AH) {
+      FkShared& fsh = *reinterpret_cast<FkShared*>(fkb);
+      fk_frame<false>(sk, ss, fsh, tid, nth);
+      __syncthreads();
+      for (int o = tid; o < CL; o += nth) {
+        const int c = o / d.L, l = o - c * d.L;
+        const double* x = fsh.pos[sk.outn[l]];
+        ProjOut po;
+        fisheye_project<true>(cams + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
+        hp[2 * o] = po.u;
+        hp[2 * o + 1] = po.v;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) hp[m + 6 * o + k] = po.J[k];
+      }
+    } else {
+      ekf_fk_batch<F32>(sk, ss, d.eps, fkb, tid, nth);
+      const double* pos = fkb + FK_MAXJ * 9 + (FK_MAXP + 1) * 9 + (size_t)(P + 1) * d.J * 9;
+      for (int e = tid; e < (P + 1) * CL; e += nth) {
+        const int q = e / CL, o = e - q * CL;
+        const int c = o / d.L, l = o - c * d.L;
+        const double* x = pos + ((size_t)q * d.L + l) * 3;
+        ProjOut po;
+        fisheye_project<false>(cams + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
+        hp[(size_t)q * m + 2 * o] = po.u;
+        hp[(size_t)q * m + 2 * o + 1] = po.v;
+      }
+    }
+    __syncthreads();
+    EKF_TICK1(2);
+    for (int r = tid; r < m; r += nth) {
+      const int o = r >> 1, c = o / d.L;
+      double e = meas[fo * fstride * 2 + r] - hp[r];
+      if (!isfinite(e)) e = (e != e) ? 0.0 : (e > 0 ? 1.7976931348623157e308 : -1.7976931348623157e308);
+      const double lk = lik[fo * fstride + o];
+      const double sd = (lk < d.thresh) ? d.maxpix : rbase[c];
+      sr[r] = e;
+      sw[r] = 1.0 / (sd * sd);
+    }
+    // H rows, one row per lane pass (P entries in registers, stored together)
+    for (int r = tid; r < m; r += nth) {
+      double hr[P];
+      if constexpr (AH) {
+        const int o = r >> 1, l = o % d.L;
+        const double* jr = hp + m + 6 * (size_t)o + 3 * (r & 1);
+        const double j0 = jr[0], j1 = jr[1], j2 = jr[2];
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          double dp[3];
+          fk_dpos(sk, *reinterpret_cast<const FkShared*>(fkb), sk.outn[l], q, dp);
+          hr[q] = j0 * dp[0] + j1 * dp[1] + j2 * dp[2];
+        }
+      } else {
+        const double h0 = hp[r];
+#pragma unroll
+        for (int q = 0; q < P; ++q) hr[q] = (hp[(size_t)(q + 1) * m + r] - h0) / d.eps;
+      }
+#pragma unroll
+      for (int q = 0; q < P; ++q) sH[r * P + q] = hr[q];
+    }
+    __syncthreads();
+    EKF_TICK1(3);
+    // ---- 3. A = H^T R^-1 H, b = H^T R^-1 r (entry per lane), 3-sigma outliers ----------
+    {
+      const int t = tid & 31, part = tid >> 5, mh = (m + 1) >> 1;
+      const int r0 = part ? mh : 0, r1 = part ? m : mh;
+      double v = 0.0;
+      if (t < nAb)
+        for (int r = r0; r < r1; ++r) v = fma(sw[r] * sH[r * P + ea], eb >= 0 ? sH[r * P + eb] : sr[r], v);
+      v += __shfl_xor(v, 32);
+      if (part == 0 && t < nAb) {
+        if (eb >= 0) {
+          sA[ea * P + eb] = v;
+          sA[eb * P + ea] = v;
+        } else {
+          sA[P * P + ea] = v;
+        }
+      }
+    }
+    {
+      // outliers: q_r = h_r P_xx h_r^T + sd_r^2 per row, an observation if either row fails;
+      // P_xx (uniform) in registers
+      double pxx[P][P];
+#pragma unroll
+      for (int a = 0; a < P; ++a)
+#pragma unroll
+        for (int b = 0; b < P; ++b) pxx[a][b] = sP[a * LDP + b];
+      for (int o = tid; o < CL; o += nth) {
+        bool out = false;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+          const int r = 2 * o + side;
+          double h[P];
+#pragma unroll
+          for (int a = 0; a < P; ++a) h[a] = sH[r * P + a];
+          double q = 0.0;
+#pragma unroll
+          for (int a = 0; a < P; ++a) {
+            double tv = 0.0;
+#pragma unroll
+            for (int b = 0; b < P; ++b) tv = fma(pxx[a][b], h[b], tv);
+            q = fma(h[a], tv, q);
+          }
+          const double Srr = q + 1.0 / sw[r];
+          out = out || fabs(sr[r]) > 3.0 * sqrt(Srr);
+        }
+        const unsigned long long bal = __ballot(out);
+        if (tid == 0) nout += __popcll(bal);
+      }
+    }
+    for (int e = tid; e < n * P; e += nth) {
+      const int r = e / P, c = e - r * P;
+      sPx[e] = sP[r * LDP + c];
+    }
+    __syncthreads();
+    EKF_TICK1(4);
+    // ---- 4. [I + A P_xx | A P[x,:] | b], column c on lane c --------------------------
+    double a[P];
+    {
+      const int c = tid;
+      double av[P][P];
+#pragma unroll
+      for (int r = 0; r < P; ++r)
+#pragma unroll
+        for (int k = 0; k < P; ++k) av[r][k] = sA[r * P + k];
+      double col[P];
+      const int j = c < P ? c : (c < P + n ? c - P : 0);
+#pragma unroll
+      for (int k = 0; k < P; ++k) col[k] = sP[k * LDP + j];
+#pragma unroll
+      for (int r = 0; r < P; ++r) {
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < P; ++k) v = fma(av[r][k], col[k], v);
+        if (c == r) v += 1.0;
+        a[r] = c < P + n ? v : (c == P + n ? sA[P * P + r] : 0.0);
+      }
+    }
+    EKF_TICK1(5);
+    // ---- 5. Gauss-Jordan with partial pivoting, in registers --------------------------
+    {
+      unsigned used = 0;
+      int pvk[P];
+      double pk[P];
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        // the pivot column's lane: largest |a[r]| over the unused rows, lowest row on ties
+        double best = -1.0;
+        int bi = 0;
+#pragma unroll
+        for (int r = 0; r < P; ++r) {
+          const bool cand = !((used >> r) & 1u) && fabs(a[r]) > best;
+          best = cand ? fabs(a[r]) : best;
+          bi = cand ? r : bi;
+        }
+        const int pv = __builtin_amdgcn_readlane(bi, k);
+        double colv[P];
+#pragma unroll
+        for (int r = 0; r < P; ++r) colv[r] = read_lane_f64(a[r], k);
+        double p = 0.0, prow = 0.0;
+#pragma unroll
+        for (int r = 0; r < P; ++r) {
+          p = r == pv ? colv[r] : p;
+          prow = r == pv ? a[r] : prow;
+        }
+        const bool upd_col = tid > k;
+#pragma unroll
+        for (int r = 0; r < P; ++r) {
+          const double nv = fma(-(colv[r] / p), prow, a[r]);
+          a[r] = (r != pv && upd_col) ? nv : a[r];
+        }
+        used |= 1u << pv;
+        pvk[k] = pv;
+        pk[k] = p;
+      }
+      // solution row k = row pv_k over its pivot: the right-hand-side columns (lanes >= P)
+      if (tid >= P && tid < NCOL) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          double v = 0.0;
+#pragma unroll
+          for (int r = 0; r < P; ++r) v = r == pvk[k] ? a[r] : v;
+          sZ[k * NZ1 + tid - P] = v * (1.0 / pk[k]);
+        }
+      }
+    }
+    __syncthreads();
+    EKF_TICK1(6);
+    // ---- 6. s += P[:, x] Z_b ; P -= P[:, x] Z_G ---------------------------------------
+    if (tid < n) {
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < P; ++k) v += sPx[tid * P + k] * sZ[k * NZ1 + n];
+      ss[tid] += v;
+    }
+    for (Walk2 w(tid, nth, n); w.e < n * n; w.next()) {
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < P; ++k) v = fma(sPx[w.r * P + k], sZ[k * NZ1 + w.c], v);
+      sP[w.r * LDP + w.c] -= v;
+    }
+    __syncthreads();
+    EKF_TICK1(7);
+    if (tid < n) xest[fo * n + tid] = ss[tid];
+    for (Walk2 w(tid, nth, n); w.e < n * n; w.next()) Pest[fo * n * n + w.e] = sP[w.r * LDP + w.c];
+    __syncthreads();
+  }
+#ifdef EKF_PROFILE
+  if (tid == 0 && ekf_prof)
+    for (int k = 0; k < 8; ++k) ekf_prof[seq * 8 + k] = s_prof[k];
+#endif
+#undef EKF_TICK1
+  if (tid == 0) outliers[seq] = nout;
+}
+
 // RTS smoother with the smoothed covariances (src/core/ekf.py:292-296), one workgroup per
 // sequence walking back through the frames (k_ekf_gain + k_ekf_smooth_x when the
 // covariances are not wanted).
@@ -901,13 +1254,25 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
                             (size_t)d.npad * d.Ppad + (size_t)d.Ppad * (d.Ppad + d.npad + 1) + (size_t)d.Ppad * d.Ppad);
   const size_t lds_f = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + U + d.npad +
                                           n_reals + (n_ints + 1) / 2 + 1);
-  ACS_CHECK(ctx, lds_f <= 160 * 1024, "ekf: P = %d needs %zu bytes of LDS", P, lds_f);
+  const size_t lds_w1 = sizeof(double) * ekf_w1_lds(d);
+  // ACS_EKF_WG=1 keeps the 8-wave kernel for every model (A/B measurements, tools/ekf_drift.py)
+  static const bool force_wg = [] {
+    const char* e = std::getenv("ACS_EKF_WG");
+    return e && e[0] == '1';
+  }();
+  const bool w1 = P == EKF_W1_P && lds_w1 <= 64 * 1024 && !force_wg;
+  ACS_CHECK(ctx, w1 || lds_f <= 160 * 1024, "ekf: P = %d needs %zu bytes of LDS", P, lds_f);
   ACS_CHECK(ctx, ref_numerics >= 0 && ref_numerics <= ACS_EKF_ANALYTIC_H, "ekf: numerics mode %d", ref_numerics);
   // analytic H: the FkShared of one FK lives in the batched-FK region of the LDS union
   ACS_CHECK(ctx, ekf_fk_lds(P, Jn, L) * sizeof(double) >= sizeof(FkShared), "ekf: FK region too small");
-#define EKF_FILTER(f32, ah)                                                                                       \
-  hipLaunchKernelGGL((k_ekf_filter<f32, ah>), dim3(n_seq), dim3(512), lds_f, s, d, io.I, io.R, io.cams, io.meas, \
-                     io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof)
+  // small states (the head model): one wave per sequence (k_ekf_filter_w1)
+#define EKF_FILTER(f32, ah)                                                                                         \
+  if (w1)                                                                                                           \
+    hipLaunchKernelGGL((k_ekf_filter_w1<f32, ah, EKF_W1_P>), dim3(n_seq), dim3(64), lds_w1, s, d, io.I, io.R,      \
+                       io.cams, io.meas, io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, dout, g_ekf_prof); \
+  else                                                                                                              \
+    hipLaunchKernelGGL((k_ekf_filter<f32, ah>), dim3(n_seq), dim3(512), lds_f, s, d, io.I, io.R, io.cams, io.meas, \
+                       io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof)
   if (ref_numerics == ACS_EKF_ANALYTIC_H)
     EKF_FILTER(false, true);
   else if (ref_numerics)

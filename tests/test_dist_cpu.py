@@ -207,6 +207,26 @@ def test_ext_dist_protocol_matches_monolithic(world):
     np.testing.assert_allclose(t, tm, rtol=0, atol=1e-9)
 
 
+def test_dist_max_iters_zero_takes_no_step():
+    """max_iters = 0: no LM step on any rank, as the monolithic solve (X0 back, iters 0,
+    status 'maxiter') - the first round stops before stepping (frame-window FTE and
+    points + extrinsics SBA)."""
+    prob, X0 = _problem('head', 20, True, 'vel')
+    ref = ofte.solve(prob, X0, max_iters=0)
+    assert ref[2]['iters'] == 0 and np.array_equal(ref[0], X0)
+    ranks = [odist.OracleFteRank(prob, X0, None, r, 2, max_iters=0) for r in range(2)]
+    assert dist.lm_loop(ranks, dist.local_allreduce) == 5
+    Xd, taud, info = ranks[0].result()
+    assert info['iters'] == 0 and info['n_accepted'] == 0
+    np.testing.assert_array_equal(Xd, X0)
+    ranks = _ext_ranks(2, max_iters=0)
+    assert dist.lm_loop(ranks, dist.local_allreduce) == 5
+    g, uv, X, pi, ci = _ext_problem()
+    R, t, Xr, info = ranks[0].result()
+    assert info['iters'] == 0
+    np.testing.assert_array_equal(np.concatenate([r.result()[2] for r in ranks]), X)
+
+
 def _gloo_ext_worker(rank, world, port, out_dir):
     import torch
     import torch.distributed as tdist

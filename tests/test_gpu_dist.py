@@ -156,6 +156,26 @@ def test_sba_ext_dist_virtual_matches_single(ctx, world):
     np.testing.assert_allclose(cd[:, 17:], c1[:, 17:], rtol=0, atol=1e-9)
 
 
+def test_dist_max_iters_zero_takes_no_step(ctx):
+    """max_iters = 0 over ranks: no step (X0 back, iters 0), as acs_fte_solve /
+    acs_sba_extrinsics - the first round stops before stepping."""
+    prob, cams, X0 = _problem(31, 'head', True, 'vel')
+    table = pkin.build_table('head')
+    o = ctx.fte_default_opts(max_iters=0)
+    X1, t1, r1 = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, shutter_delay=True,
+                               intermode=prob.im, opts=o)
+    Xd, td, rd = dist.fte_solve_virtual(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
+                                        shutter_delay=True, intermode=prob.im, opts=o, world=2)
+    assert r1['iters'] == 0 and rd['iters'] == 0, (r1, rd)
+    np.testing.assert_array_equal(Xd, X1)
+    g, cams = _ext()
+    oe = ctx.sba_ext_opts(max_iters=0)
+    cd, Xe, re_ = dist.sba_extrinsics_virtual(ctx, cams, g['points_2d'], g['point_indices'], g['camera_indices'],
+                                              g['points_3d'], oe, world=2)
+    assert re_['iters'] == 0
+    np.testing.assert_array_equal(Xe, g['points_3d'])
+
+
 def _ext_worker(rank, world, port, out_dir):
     import torch.distributed as tdist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
