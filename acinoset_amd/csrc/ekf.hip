@@ -32,9 +32,22 @@ struct EkfDims {
   double sT, thresh, maxpix, eps;
 };
 
+// doubles of an FkShared (the analytic-H FK); its FkDeriv follows it
+__host__ __device__ constexpr size_t ekf_fk_shared_doubles() { return (sizeof(FkShared) + 7) / 8; }
+__host__ __device__ constexpr size_t ekf_fk_ah_doubles() {
+  return ekf_fk_shared_doubles() + (sizeof(FkDeriv) + 7) / 8;
+}
+
 // LDS doubles of the batched FK of the P+1 Jacobian poses (ekf_fk_batch)
 __host__ __device__ inline size_t ekf_fk_lds(int P, int J, int L) {
   return (size_t)FK_MAXJ * 9 + (size_t)(FK_MAXP + 1) * 9 + (size_t)(P + 1) * (9 * J + 3 * L + 6) + 4 * FK_MAXP;
+}
+
+// LDS doubles of the measurement model's FK region: the batched FK of the forward
+// differences, or the analytic H's FkShared + FkDeriv, whichever is larger
+__host__ __device__ inline size_t ekf_w1_fk_doubles(int P, int J, int L) {
+  const size_t a = ekf_fk_lds(P, J, L), b = ekf_fk_ah_doubles();
+  return a > b ? a : b;
 }
 
 // Parameter p of Jacobian pose q (q = 0: the predicted state; q > 0: parameter q-1 moved by
@@ -227,7 +240,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   double* aug = sPx + (size_t)d.npad * Pp;            // Pp x AW
   double* sA = aug + (size_t)Pp * AW;                 // Pp x Pp
   // the FK and algebra phases share U; what follows must start past the larger of the two
-  const size_t u_fk = ekf_fk_lds(P, d.J, d.L);
+  const size_t u_fk = ekf_w1_fk_doubles(P, d.J, d.L);  // batched FK, or FkShared + FkDeriv
   const size_t u_la = (size_t)d.npad * Pp + (size_t)Pp * AW + (size_t)Pp * Pp;
   double* ss = U + (u_fk > u_la ? u_fk : u_la);      // n: state
   double* sRl = ss + d.npad;                          // skeleton table (reals, then ints)
@@ -328,6 +341,8 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       FkShared& fsh = *reinterpret_cast<FkShared*>(fkb);
       fk_frame<false>(sk, ss, fsh, tid, nth);
       __syncthreads();
+      // per-parameter derivative data resolved once (fk_deriv_prep: no table walk per entry)
+      if (tid < P) fk_deriv_prep(sk, fsh, *reinterpret_cast<FkDeriv*>(fkb + ekf_fk_shared_doubles()), tid);
       for (int o = tid; o < CL; o += nth) {
         const int c = o / d.L, l = o - c * d.L;
         const double* x = fsh.pos[sk.outn[l]];
@@ -381,22 +396,33 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       wr[r] = w;
     }
     __syncthreads();
-    for (int e = tid; e < mp * Pp; e += nth) {
-      const int r = e / Pp, q = e - r * Pp;
-      double hq = 0.0;
-      if constexpr (AH) {
-        if (r < m && q < P) {
-          const int o = r >> 1, l = o % d.L;
-          const double* jr = hpose + m + 6 * (size_t)o + 3 * (r & 1);
+    if constexpr (AH) {
+      // both rows of an observation from one d pos / d x_q (mp is even)
+      const FkShared& fsh = *reinterpret_cast<const FkShared*>(fkb);
+      const FkDeriv& fkd = *reinterpret_cast<const FkDeriv*>(fkb + ekf_fk_shared_doubles());
+      for (int e = tid; e < (mp >> 1) * Pp; e += nth) {
+        const int o = e / Pp, q = e - o * Pp, r = 2 * o;
+        double hu = 0.0, hv = 0.0;
+        if (o < CL && q < P) {
+          const double* jr = hpose + m + 6 * (size_t)o;
           double dp[3];
-          fk_dpos(sk, *reinterpret_cast<const FkShared*>(fkb), sk.outn[l], q, dp);
-          hq = jr[0] * dp[0] + jr[1] * dp[1] + jr[2] * dp[2];
+          fk_dpos_fast(sk, fsh, fkd, sk.outn[o % d.L], q, dp);
+          hu = jr[0] * dp[0] + jr[1] * dp[1] + jr[2] * dp[2];
+          hv = jr[3] * dp[0] + jr[4] * dp[1] + jr[5] * dp[2];
         }
-      } else {
-        if (r < m && q < P) hq = (hpose[(size_t)(q + 1) * m + r] - hpose[r]) / d.eps;
+        H[(size_t)r * Pp + q] = hu;
+        H[(size_t)(r + 1) * Pp + q] = hv;
+        HW[(size_t)r * Pp + q] = wr[r] * hu;
+        HW[(size_t)(r + 1) * Pp + q] = wr[r + 1] * hv;
       }
-      H[e] = hq;
-      HW[e] = wr[r] * hq;
+    } else {
+      for (int e = tid; e < mp * Pp; e += nth) {
+        const int r = e / Pp, q = e - r * Pp;
+        double hq = 0.0;
+        if (r < m && q < P) hq = (hpose[(size_t)(q + 1) * m + r] - hpose[r]) / d.eps;
+        H[e] = hq;
+        HW[e] = wr[r] * hq;
+      }
     }
     __syncthreads();
     EKF_TICK(3);
@@ -684,10 +710,6 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
 // sums are in another order, so results agree to rounding (tests/test_gpu_ekf.py).
 #define EKF_W1_P 6
 
-__host__ __device__ inline size_t ekf_w1_fk_doubles(int P, int J, int L) {
-  const size_t a = ekf_fk_lds(P, J, L), b = (sizeof(FkShared) + 7) / 8;
-  return a > b ? a : b;
-}
 // LDS doubles of k_ekf_filter_w1
 __host__ __device__ inline size_t ekf_w1_lds(const EkfDims& d) {
   const size_t n = d.n, P = d.P, m = d.m;
@@ -808,6 +830,7 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
       FkShared& fsh = *reinterpret_cast<FkShared*>(fkb);
       fk_frame<false>(sk, ss, fsh, tid, nth);
       __syncthreads();
+      if (tid < P) fk_deriv_prep(sk, fsh, *reinterpret_cast<FkDeriv*>(fkb + ekf_fk_shared_doubles()), tid);
       for (int o = tid; o < CL; o += nth) {
         const int c = o / d.L, l = o - c * d.L;
         const double* x = fsh.pos[sk.outn[l]];
@@ -842,26 +865,31 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
       sr[r] = e;
       sw[r] = 1.0 / (sd * sd);
     }
-    // H rows, one row per lane pass (P entries in registers, stored together)
-    for (int r = tid; r < m; r += nth) {
-      double hr[P];
-      if constexpr (AH) {
-        const int o = r >> 1, l = o % d.L;
-        const double* jr = hp + m + 6 * (size_t)o + 3 * (r & 1);
-        const double j0 = jr[0], j1 = jr[1], j2 = jr[2];
+    // H rows (P entries in registers, stored together); analytic: both rows of an
+    // observation from one d pos / d x_q
+    if constexpr (AH) {
+      const FkShared& fsh = *reinterpret_cast<const FkShared*>(fkb);
+      const FkDeriv& fkd = *reinterpret_cast<const FkDeriv*>(fkb + ekf_fk_shared_doubles());
+      for (int o = tid; o < CL; o += nth) {
+        const double* jr = hp + m + 6 * (size_t)o;
+        const int node = sk.outn[o % d.L];
 #pragma unroll
         for (int q = 0; q < P; ++q) {
           double dp[3];
-          fk_dpos(sk, *reinterpret_cast<const FkShared*>(fkb), sk.outn[l], q, dp);
-          hr[q] = j0 * dp[0] + j1 * dp[1] + j2 * dp[2];
+          fk_dpos_fast(sk, fsh, fkd, node, q, dp);
+          sH[2 * o * P + q] = jr[0] * dp[0] + jr[1] * dp[1] + jr[2] * dp[2];
+          sH[(2 * o + 1) * P + q] = jr[3] * dp[0] + jr[4] * dp[1] + jr[5] * dp[2];
         }
-      } else {
+      }
+    } else {
+      for (int r = tid; r < m; r += nth) {
+        double hr[P];
         const double h0 = hp[r];
 #pragma unroll
         for (int q = 0; q < P; ++q) hr[q] = (hp[(size_t)(q + 1) * m + r] - h0) / d.eps;
-      }
 #pragma unroll
-      for (int q = 0; q < P; ++q) sH[r * P + q] = hr[q];
+        for (int q = 0; q < P; ++q) sH[r * P + q] = hr[q];
+      }
     }
     __syncthreads();
     EKF_TICK1(3);
@@ -1250,7 +1278,7 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
   io.outliers = dout;
   int* dbad = (int*)(dout + n_seq);
   ACS_HIP(ctx, hipMemsetAsync(dbad, 0, sizeof(int), s));
-  const size_t U = std::max(ekf_fk_lds(P, Jn, L),
+  const size_t U = std::max(ekf_w1_fk_doubles(P, Jn, L),
                             (size_t)d.npad * d.Ppad + (size_t)d.Ppad * (d.Ppad + d.npad + 1) + (size_t)d.Ppad * d.Ppad);
   const size_t lds_f = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + U + d.npad +
                                           n_reals + (n_ints + 1) / 2 + 1);
@@ -1264,7 +1292,6 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
   ACS_CHECK(ctx, w1 || lds_f <= 160 * 1024, "ekf: P = %d needs %zu bytes of LDS", P, lds_f);
   ACS_CHECK(ctx, ref_numerics >= 0 && ref_numerics <= ACS_EKF_ANALYTIC_H, "ekf: numerics mode %d", ref_numerics);
   // analytic H: the FkShared of one FK lives in the batched-FK region of the LDS union
-  ACS_CHECK(ctx, ekf_fk_lds(P, Jn, L) * sizeof(double) >= sizeof(FkShared), "ekf: FK region too small");
   // small states (the head model): one wave per sequence (k_ekf_filter_w1)
 #define EKF_FILTER(f32, ah)                                                                                         \
   if (w1)                                                                                                           \

@@ -277,6 +277,8 @@ def main():
         # kept only as a cost figure for the bigger state
         leg('ekf', lambda: bench_ekf(ctx, torch, args.ekf_seqs, args.ekf_frames, args.ekf_cams, world, rank,
                                      mode='head'))
+        leg('ekf_analytic_h', lambda: bench_ekf(ctx, torch, args.ekf_seqs, args.ekf_frames, args.ekf_cams, world,
+                                                rank, mode='head', jacobian='analytic'))
         leg('ekf_default_model_diverges', lambda: bench_ekf(ctx, torch, args.ekf_seqs, args.ekf_frames,
                                                             args.ekf_cams, world, rank, mode='default'))
     if args.pipeline_seqs > 0:
@@ -456,7 +458,7 @@ def _fte_problem(ctx, n_frames, seed=77):
     return wl.seq, wl.cams, wl.meas, wl.w, wl.X0, wl.table, wl.qinv
 
 
-def bench_ekf(ctx, torch, n_seq, n_frames, n_cams, world, rank, mode='default', steps=2):
+def bench_ekf(ctx, torch, n_seq, n_frames, n_cams, world, rank, mode='default', steps=2, jacobian='fd'):
     """EKF + RTS smoother (the EKF half of configs[4]): `n_seq`
     independent synthetic sequences per rank (replicas: the filter is sequential in time),
     `n_cams`-camera ring, reference numerics. Reports the smoothed keypoints' RMS error
@@ -483,12 +485,13 @@ def bench_ekf(ctx, torch, n_seq, n_frames, n_cams, world, rank, mode='default', 
     covs = cekf.ring_cal_covs(n_cams)
     args = (90.0, 0.5, float(scene.res[0]), cekf.measurement_std(n_cams, covs), cekf.process_covariance(P, 1 / 90.0),
             cekf.initial_covariance(mode))
-    out = ctx.ekf_run(table, cams, meas, lik, *args, s0)                 # warm-up
+    kw = dict(ref_numerics=jacobian == 'fd', jacobian=jacobian)
+    out = ctx.ekf_run(table, cams, meas, lik, *args, s0, **kw)          # warm-up
     if world > 1:
         tdist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        ctx.ekf_run(table, cams, meas, lik, *args, s0)
+        ctx.ekf_run(table, cams, meas, lik, *args, s0, **kw)
     dt = (time.perf_counter() - t0) / steps
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
@@ -507,7 +510,9 @@ def bench_ekf(ctx, torch, n_seq, n_frames, n_cams, world, rank, mode='default', 
             'us_per_frame_per_seq': dt / n_frames * 1e6, 'scaling': 'weak (replicas)',
             'smoothed_rms_vs_truth_m': rms, 'filter': 'tracks' if rms < 0.05 else 'diverged',
             'outliers_frac': float(np.mean(out['outliers'])) / max(1.0, float(np.sum(lik > 0.5)) * 2 / n_seq),
-            'numerics': 'reference (float32 state rounding, FD Jacobian eps 1e-3)'}
+            'numerics': ('reference (float32 state rounding, FD Jacobian eps 1e-3)' if jacobian == 'fd' else
+                         'float64, analytic H from the FK Jacobian (SURVEY §8(f)2)'),
+            'kernel': 'k_ekf_filter_w1 (one wave per sequence)' if P == 6 else 'k_ekf_filter (8 waves per sequence)'}
 
 
 def bench_pipeline(ctx, torch, stream, world, rank, n_seq=80, n_frames=250, n_cams=12, steps=3):
