@@ -50,6 +50,28 @@ __host__ __device__ inline size_t ekf_w1_fk_doubles(int P, int J, int L) {
   return a > b ? a : b;
 }
 
+// Analytic H in marker space (k_ekf_filter<*, true>): rows of the per-marker operands
+// (3 L padded to a multiple of 16), and the LDS doubles of FkShared + FkDeriv followed by
+// D = d pos / d x, T = M D, S = D P_xx (R3 x (Ppad + 1) each), g (R3), N (9 L), M (6 L)
+__host__ __device__ inline int ekf_ah_rows(int L) { return (3 * L + 15) & ~15; }
+__host__ __device__ inline size_t ekf_ah_base() { return (ekf_fk_ah_doubles() + 3) & ~(size_t)3; }
+__host__ __device__ inline size_t ekf_ah_alg_doubles(int L, int Ppad) {
+  const size_t R3 = ekf_ah_rows(L);
+  return ekf_ah_base() + 3 * R3 * (Ppad + 1) + R3 + 15 * (size_t)L;
+}
+// the 8-wave filter's algebra region: P[:, x] (npad x (Ppad + 1)), aug (Ppad x AW) and A
+// (Ppad x (Ppad + 1)); the odd row stride keeps the MFMA A-operand reads (16 rows, one
+// column) on distinct LDS banks
+__host__ __device__ inline size_t ekf_wg_la_doubles(int npad, int Ppad) {
+  return (size_t)npad * (Ppad + 1) + (size_t)Ppad * (Ppad + npad + 1) + (size_t)Ppad * (Ppad + 1);
+}
+// the 8-wave filter's measurement-model region: batched FK (forward differences) or the
+// analytic H's FK and marker-space operands, whichever is larger
+__host__ __device__ inline size_t ekf_wg_fk_doubles(int P, int J, int L, int Ppad) {
+  const size_t a = ekf_w1_fk_doubles(P, J, L), b = ekf_ah_alg_doubles(L, Ppad);
+  return a > b ? a : b;
+}
+
 // Parameter p of Jacobian pose q (q = 0: the predicted state; q > 0: parameter q-1 moved by
 // eps, in float32 with the reference numerics, src/core/ekf.py:81-96).
 template <bool F32>
@@ -236,12 +258,13 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   double* sP = lds;                                   // npad x LDP: covariance
   double* U = sP + (size_t)d.npad * LDP;              // union: FK phase / algebra phase
   double* fkb = U;                                    // batched FK of the P+1 poses
-  double* sPx = U;                                    // npad x Pp: P[:, x] before the update
-  double* aug = sPx + (size_t)d.npad * Pp;            // Pp x AW
-  double* sA = aug + (size_t)Pp * AW;                 // Pp x Pp
+  const int LPx = Pp + 1;                             // row stride of sPx and sA
+  double* sPx = U;                                    // npad x LPx: P[:, x] before the update
+  double* aug = sPx + (size_t)d.npad * LPx;           // Pp x AW
+  double* sA = aug + (size_t)Pp * AW;                 // Pp x LPx
   // the FK and algebra phases share U; what follows must start past the larger of the two
-  const size_t u_fk = ekf_w1_fk_doubles(P, d.J, d.L);  // batched FK, or FkShared + FkDeriv
-  const size_t u_la = (size_t)d.npad * Pp + (size_t)Pp * AW + (size_t)Pp * Pp;
+  const size_t u_fk = ekf_wg_fk_doubles(P, d.J, d.L, Pp);  // batched FK, or the analytic H's region
+  const size_t u_la = ekf_wg_la_doubles(d.npad, Pp);
   double* ss = U + (u_fk > u_la ? u_fk : u_la);      // n: state
   double* sRl = ss + d.npad;                          // skeleton table (reals, then ints)
   int* sI = reinterpret_cast<int*>(sRl + d.n_reals);
@@ -396,25 +419,106 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       wr[r] = w;
     }
     __syncthreads();
+    // operands of the A / b products below: A = opW^T opH, b = opW^T opr over nks k-steps of
+    // 4 rows (forward differences: H rows of every observation; analytic: per-marker rows)
+    const double* opW = HW;
+    const double* opH = H;
+    const double* opr = res;
+    int nks = mp >> 2, ldo = Pp;
     if constexpr (AH) {
-      // both rows of an observation from one d pos / d x_q (mp is even)
+      // Marker space. Row r of H is j_r D_l (j_r: a row of the observation's 2x3 projection
+      // Jacobian, D_l = d pos_l / d x: 3 x P, the same for every camera), so
+      //   A = sum_l D_l^T M_l D_l,  M_l = sum_c J^T W J (3x3),
+      //   b = sum_l D_l^T g_l,      g_l = sum_c J^T W r,
+      //   diag(H P_xx H^T)_r = j_r N_l j_r^T,  N_l = D_l P_xx D_l^T (3x3):
+      // the products run over 3 L rows instead of 2 C L (the same sums in another order)
       const FkShared& fsh = *reinterpret_cast<const FkShared*>(fkb);
       const FkDeriv& fkd = *reinterpret_cast<const FkDeriv*>(fkb + ekf_fk_shared_doubles());
-      for (int e = tid; e < (mp >> 1) * Pp; e += nth) {
-        const int o = e / Pp, q = e - o * Pp, r = 2 * o;
-        double hu = 0.0, hv = 0.0;
-        if (o < CL && q < P) {
-          const double* jr = hpose + m + 6 * (size_t)o;
-          double dp[3];
-          fk_dpos_fast(sk, fsh, fkd, sk.outn[o % d.L], q, dp);
-          hu = jr[0] * dp[0] + jr[1] * dp[1] + jr[2] * dp[2];
-          hv = jr[3] * dp[0] + jr[4] * dp[1] + jr[5] * dp[2];
-        }
-        H[(size_t)r * Pp + q] = hu;
-        H[(size_t)(r + 1) * Pp + q] = hv;
-        HW[(size_t)r * Pp + q] = wr[r] * hu;
-        HW[(size_t)(r + 1) * Pp + q] = wr[r + 1] * hv;
+      const int L = d.L, R3 = ekf_ah_rows(L), LD = Pp + 1;  // odd row stride: MFMA A reads
+      double* sD = fkb + ekf_ah_base();
+      double* sTm = sD + (size_t)R3 * LD;
+      double* sS = sTm + (size_t)R3 * LD;
+      double* sg = sS + (size_t)R3 * LD;
+      double* sN = sg + R3;
+      double* sM = sN + 9 * L;
+      for (int e = tid; e < L * Pp; e += nth) {  // D rows 3 l + k (zero padding columns)
+        const int l = e / Pp, q = e - l * Pp;
+        double dp[3] = {0.0, 0.0, 0.0};
+        if (q < P) fk_dpos_fast(sk, fsh, fkd, sk.outn[l], q, dp);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sD[(3 * l + k) * LD + q] = dp[k];
       }
+      for (int e = tid; e < (R3 - 3 * L) * Pp; e += nth) {  // padding rows
+        const int r = e / Pp;
+        sD[(3 * L + r) * LD + e - r * Pp] = 0.0;
+      }
+      for (int e = tid; e < 9 * L; e += nth) {  // M_l (6 entries of the symmetric 3x3), g_l (3)
+        const int l = e / 9, k = e - 9 * l;
+        const int a = k < 3 ? 0 : (k < 5 ? 1 : (k < 6 ? 2 : k - 6));
+        const int b = k < 3 ? k : (k < 5 ? k - 2 : 2);
+        double v = 0.0;
+        for (int c = 0; c < d.C; ++c) {
+          const int o = c * L + l;
+          const double* J = hpose + m + 6 * (size_t)o;
+          const double wu = wr[2 * o], wv = wr[2 * o + 1];
+          if (k < 6)
+            v += wu * J[a] * J[b] + wv * J[3 + a] * J[3 + b];
+          else
+            v += wu * J[a] * res[2 * o] + wv * J[3 + a] * res[2 * o + 1];
+        }
+        if (k < 6)
+          sM[6 * l + k] = v;
+        else
+          sg[3 * l + a] = v;
+      }
+      for (int r = 3 * L + tid; r < R3; r += nth) sg[r] = 0.0;
+      __syncthreads();
+      for (int e = tid; e < R3 * Pp; e += nth) {  // T = M D
+        const int row = e / Pp, q = e - row * Pp;
+        double t = 0.0;
+        if (row < 3 * L) {
+          const int l = row / 3, k = row - 3 * l;
+          const double* Ml = sM + 6 * l;
+          const double m0 = k == 0 ? Ml[0] : (k == 1 ? Ml[1] : Ml[2]);
+          const double m1 = k == 0 ? Ml[1] : (k == 1 ? Ml[3] : Ml[4]);
+          const double m2 = k == 0 ? Ml[2] : (k == 1 ? Ml[4] : Ml[5]);
+          t = m0 * sD[(3 * l) * LD + q] + m1 * sD[(3 * l + 1) * LD + q] + m2 * sD[(3 * l + 2) * LD + q];
+        }
+        sTm[row * LD + q] = t;
+      }
+      // S = D P[0:Pp, 0:Pp] on MFMA (D is zero past column P; S is read only below column P)
+      wg_mgemm<false, false>(sS, LD, sD, LD, sP, LDP, R3, Pp, Pp, 1.0, 0.0);
+      for (int e = tid; e < 9 * L; e += nth) {  // N_l = S_l D_l^T
+        const int l = e / 9, k = e - 9 * l, a = k / 3, b = k - 3 * a;
+        double v = 0.0;
+        for (int q = 0; q < P; ++q) v = fma(sS[(3 * l + a) * LD + q], sD[(3 * l + b) * LD + q], v);
+        sN[e] = v;
+      }
+      __syncthreads();
+      // 3-sigma outlier count (:259-264), an observation if either of its rows fails
+      unsigned long long cnt = 0;
+      for (int o = tid; o < CL; o += nth) {
+        const double* J = hpose + m + 6 * (size_t)o;
+        const double* N = sN + 9 * (o % L);
+        bool outl = false;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+          const double* j = J + 3 * side;
+          const double q = j[0] * (N[0] * j[0] + N[1] * j[1] + N[2] * j[2]) +
+                           j[1] * (N[3] * j[0] + N[4] * j[1] + N[5] * j[2]) +
+                           j[2] * (N[6] * j[0] + N[7] * j[1] + N[8] * j[2]);
+          const int r = 2 * o + side;
+          const double Srr = q + 1.0 / wr[r];
+          outl = outl || fabs(res[r]) > 3.0 * sqrt(Srr);
+        }
+        if (outl) ++cnt;
+      }
+      if (cnt) atomicAdd(&s_out, cnt);
+      opW = sD;
+      opH = sTm;
+      opr = sg;
+      nks = R3 >> 2;
+      ldo = LD;
     } else {
       for (int e = tid; e < mp * Pp; e += nth) {
         const int r = e / Pp, q = e - r * Pp;
@@ -433,7 +537,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       // of operands loaded before their MFMAs; the KS partial tiles are summed in a fixed
       // tree through LDS (sPx / aug are free until the products below)
       const int li = lane & 15, lk = lane >> 4;
-      const int NTt = Pp >> 4, nAt = NTt * (NTt + 1) / 2, nt = nAt + NTt, nks = mp >> 2;
+      const int NTt = Pp >> 4, nAt = NTt * (NTt + 1) / 2, nt = nAt + NTt;
       const size_t avail = (size_t)d.npad * Pp + (size_t)Pp * AW;
       int KS = EKF_WAVES;
       while (KS > 1 && (size_t)(KS / 2) * nt * 256 > avail) KS >>= 1;
@@ -461,10 +565,10 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
             const bool ok = s0 + u * KS < nks;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-              av[u][h] = (ok && h < NTt) ? HW[(size_t)k * Pp + 16 * h + li] : 0.0;
-              bv[u][h] = (ok && h < NTt) ? H[(size_t)k * Pp + 16 * h + li] : 0.0;
+              av[u][h] = (ok && h < NTt) ? opW[(size_t)k * ldo + 16 * h + li] : 0.0;
+              bv[u][h] = (ok && h < NTt) ? opH[(size_t)k * ldo + 16 * h + li] : 0.0;
             }
-            rv[u] = (ok && li == 0) ? res[k] : 0.0;
+            rv[u] = (ok && li == 0) ? opr[k] : 0.0;
           }
 #pragma unroll
           for (int u = 0; u < UB; ++u)
@@ -480,6 +584,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
         }
       }
       // fixed-order tree over the KS partials
+      if constexpr (AH) __syncthreads();  // the tree's buffer overlaps the marker-space operands
       for (int h = KS >> 1; h >= 1; h >>= 1) {
         if (wave >= h && wave < 2 * h)
 #pragma unroll
@@ -506,8 +611,8 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
           for (int q = 0; q < 4; ++q) {
             const int row = i0 + lk + 4 * q;
             if (j0 >= 0) {
-              sA[row * Pp + j0 + li] = acc[t][q];
-              sA[(j0 + li) * Pp + row] = acc[t][q];  // lower triangle (symmetric)
+              sA[row * LPx + j0 + li] = acc[t][q];
+              sA[(j0 + li) * LPx + row] = acc[t][q];  // lower triangle (symmetric)
             } else if (li == 0) {
               aug[row * AW + Pp + d.npad] = row < P ? acc[t][q] : 0.0;
             }
@@ -518,7 +623,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       // H P_xx on MFMA (operands loaded first), each row's dot with its own H row summed
       // across the 16 column lanes (DPP) and the column tiles
       unsigned long long cnt = 0;
-      for (int rt = wave; rt < (mp >> 4); rt += EKF_WAVES) {
+      for (int rt = wave; rt < (AH ? 0 : (mp >> 4)); rt += EKF_WAVES) {
         const int i0 = rt << 4;
         double ha[8];
 #pragma unroll
@@ -556,14 +661,14 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       if (cnt) atomicAdd(&s_out, cnt);
       for (int e = tid; e < d.npad * Pp; e += nth) {  // P[:, x] (after the tree used sPx)
         const int r = e / Pp, c = e % Pp;
-        sPx[e] = (r < n && c < P) ? sP[r * LDP + c] : 0.0;
+        sPx[r * LPx + c] = (r < n && c < P) ? sP[r * LDP + c] : 0.0;
       }
       __syncthreads();
     }
     EKF_TICK(4);
     // aug = [I + A P_xx | A P[x, :] | b]: G2 = A P[0:Pp, :] on MFMA (A is zero outside
     // P x P), then the M block gets the identity and its padding columns are cleared
-    wg_mgemm<false, false>(aug + Pp, AW, sA, Pp, sP, LDP, Pp, d.npad, Pp, 1.0, 0.0);
+    wg_mgemm<false, false>(aug + Pp, AW, sA, LPx, sP, LDP, Pp, d.npad, Pp, 1.0, 0.0);
     for (int e = tid; e < Pp * d.npad; e += nth) {  // G2 columns >= n must be zero
       const int a = e / d.npad, c = e % d.npad;
       if (c >= n) aug[a * AW + Pp + c] = 0.0;
@@ -633,7 +738,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
           // pv carries the pivot), so after the barrier every lane needs two independent
           // LDS reads and no division
           const double p = read_lane_f64(colv, bi + 32 * half);
-          colb[buf * 32 + gr] = gr == bi ? p : colv / p;
+          colb[buf * 32 + gr] = gr == bi ? p : colv * (1.0 / p);  // one reciprocal, uniform
           if (gr == 0) pvb[buf] = bi;
         }
         __syncthreads();
@@ -675,10 +780,10 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     // s += P[:, x] Z_b ;  P -= P[:, x] Z_G  (MFMA; sPx / Z are zero outside the live block)
     if (tid < n) {
       double v = 0.0;
-      for (int k = 0; k < P; ++k) v += sPx[tid * Pp + k] * aug[k * AW + Pp + d.npad];
+      for (int k = 0; k < P; ++k) v += sPx[tid * LPx + k] * aug[k * AW + Pp + d.npad];
       ss[tid] += v;
     }
-    wg_mgemm<false, false>(sP, LDP, sPx, Pp, aug + Pp, AW, d.npad, d.npad, Pp, -1.0, 1.0);
+    wg_mgemm<false, false>(sP, LDP, sPx, LPx, aug + Pp, AW, d.npad, d.npad, Pp, -1.0, 1.0);
     EKF_TICK(7);
     if (tid < n) xest[fo * n + tid] = ss[tid];
     for (Walk2 w(tid, nth, n); w.e < n * n; w.next()) Pest[fo * n * n + w.e] = sP[w.r * LDP + w.c];
@@ -692,33 +797,36 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
 }
 
 // ---------------------------------------------------------------------------------------
-// Small-state filter: the head model (P = EKF_W1_P = 6 parameters, n = 18) with ONE wave per
-// sequence and the parameter count a compile-time constant. At 6 parameters the per-frame
-// algebra is a few thousand flops, and the 8-wave workgroup of k_ekf_filter spent its frame
-// on barriers and LDS round trips (24 us per 12-camera frame,
-// profiles/r03/ekf_phases_head12.log). Here:
+// Small-state filter: the head model (P = EKF_W1_P = 6 parameters, n = 18), the parameter
+// count a compile-time constant, NW = 4 waves per sequence (1 for A/B: ACS_EKF_W1_WAVES=1). At
+// 6 parameters the per-frame algebra is a few thousand flops, and the 8-wave workgroup of
+// k_ekf_filter spent its frame on barriers, LDS round trips and MFMA tiles that are mostly
+// padding (24 us per 12-camera frame, profiles/r03/ekf_phases_head12.log). Here:
 //   * prediction and the measurement model as k_ekf_filter (same device code: the P F P^T
 //     passes, ekf_fk_batch / fk_frame, the fisheye projection), all scratch in LDS;
-//   * A = H^T R^-1 H and b = H^T R^-1 r one entry per lane (rows split over the half-waves,
-//     one shuffle); the 3-sigma test one observation per lane with P_xx in registers;
-//   * the augmented [I + A P_xx | A P[x,:] | b] column-per-lane (P + n + 1 = 25 columns) and
-//     Gauss-Jordan with partial pivoting on registers: the pivot column's lane finds the
-//     pivot row in its own registers, that column reaches the other lanes by readlane; no
-//     step needs an LDS round trip or a barrier;
-//   * the state / covariance update from register copies of the solution rows.
+//   * A = H^T R^-1 H and b = H^T R^-1 r one entry per lane of wave 0 (rows split over its
+//     half-waves, one shuffle); the 3-sigma test one observation per lane with P_xx in
+//     registers, compared squared (r^2 > 9 S_rr: no square root, no division);
+//   * the augmented [I + A P_xx | A P[x,:] | b] column-per-lane of wave 0 (P + n + 1 = 25
+//     columns) and Gauss-Jordan with partial pivoting in its registers: the pivot column's
+//     lane finds the pivot row in its own registers, that column reaches the other lanes by
+//     readlane, the row factors by one reciprocal; no step needs an LDS round trip or a
+//     barrier;
+//   * the state / covariance update from the solution rows in LDS.
 // Same algorithm and pivoting rule (largest |a|, lowest row on ties) as k_ekf_filter; the
-// sums are in another order, so results agree to rounding (tests/test_gpu_ekf.py).
+// sums are in another order, so results agree to rounding (tests/test_gpu_ekf.py;
+// tools/ekf_drift.py: the same drift against the oracle as the 8-wave kernel over 250 frames).
 #define EKF_W1_P 6
 
 // LDS doubles of k_ekf_filter_w1
 __host__ __device__ inline size_t ekf_w1_lds(const EkfDims& d) {
   const size_t n = d.n, P = d.P, m = d.m;
-  return n * (n + 1) + d.npad + (P + 1) * m + m * P + 2 * m + n * P + P * (n + 1) + P * P + P +
+  return n * (n + 1) + d.npad + (P + 1) * m + m * P + 3 * m + n * P + P * (n + 1) + P * P + P +
          ekf_w1_fk_doubles(d.P, d.J, d.L) + d.n_reals + (d.n_ints + 1) / 2 + 1;
 }
 
-template <bool F32, bool AH, int PM>
-__global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __restrict__ I,
+template <bool F32, bool AH, int PM, int NW>
+__global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int* __restrict__ I,
                                                       const double* __restrict__ Rl, const double* __restrict__ cams,
                                                       const double* __restrict__ meas, const double* __restrict__ lik,
                                                       const double* __restrict__ rbase, const double* __restrict__ Q,
@@ -730,8 +838,10 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
   constexpr int P = PM, n = 3 * PM, LDP = n + 1, NZ1 = n + 1, NCOL = P + n + 1;
   static_assert(NCOL <= 64, "one column per lane");
   const int seq = blockIdx.x;
-  const int tid = threadIdx.x, nth = 64;
+  const int tid = threadIdx.x, nth = 64 * NW;
   const int m = d.m, CL = d.C * d.L;
+  __shared__ long long s_nout;
+  if (tid == 0) s_nout = 0;
   extern __shared__ double lds[];
   double* sP = lds;                                     // n x LDP: covariance
   double* ss = sP + (size_t)n * LDP;                    // npad: state
@@ -739,7 +849,8 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
   double* sH = hp + (size_t)(P + 1) * m;                // m x P
   double* sr = sH + (size_t)m * P;                      // m: residuals
   double* sw = sr + m;                                  // m: 1 / sd^2
-  double* sPx = sw + m;                                 // n x P: P[:, x] before the update
+  double* sd2 = sw + m;                                 // m: sd^2
+  double* sPx = sd2 + m;                                // n x P: P[:, x] before the update
   double* sZ = sPx + (size_t)n * P;                     // P x (n + 1): [Z_G | Z_b]
   double* sA = sZ + (size_t)P * NZ1;                    // P x P, then b (P)
   double* fkb = sA + P * P + P;                         // FK scratch
@@ -864,6 +975,7 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
       const double sd = (lk < d.thresh) ? d.maxpix : rbase[c];
       sr[r] = e;
       sw[r] = 1.0 / (sd * sd);
+      sd2[r] = sd * sd;
     }
     // H rows (P entries in registers, stored together); analytic: both rows of an
     // observation from one d pos / d x_q
@@ -894,7 +1006,7 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
     __syncthreads();
     EKF_TICK1(3);
     // ---- 3. A = H^T R^-1 H, b = H^T R^-1 r (entry per lane), 3-sigma outliers ----------
-    {
+    if (tid < 64) {  // wave 0
       const int t = tid & 31, part = tid >> 5, mh = (m + 1) >> 1;
       const int r0 = part ? mh : 0, r1 = part ? m : mh;
       double v = 0.0;
@@ -934,11 +1046,12 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
             for (int b = 0; b < P; ++b) tv = fma(pxx[a][b], h[b], tv);
             q = fma(h[a], tv, q);
           }
-          const double Srr = q + 1.0 / sw[r];
-          out = out || fabs(sr[r]) > 3.0 * sqrt(Srr);
+          // |r| > 3 sqrt(S_rr), S_rr = q + sd^2, compared squared (no sqrt, no division)
+          const double Srr = q + sd2[r];
+          out = out || sr[r] * sr[r] > 9.0 * Srr;
         }
         const unsigned long long bal = __ballot(out);
-        if (tid == 0) nout += __popcll(bal);
+        if ((tid & 63) == 0) nout += __popcll(bal);
       }
     }
     for (int e = tid; e < n * P; e += nth) {
@@ -947,9 +1060,9 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
     }
     __syncthreads();
     EKF_TICK1(4);
-    // ---- 4. [I + A P_xx | A P[x,:] | b], column c on lane c --------------------------
+    // ---- 4. [I + A P_xx | A P[x,:] | b], column c on lane c of wave 0 ----------------
     double a[P];
-    {
+    if (tid < 64) {
       const int c = tid;
       double av[P][P];
 #pragma unroll
@@ -970,8 +1083,8 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
       }
     }
     EKF_TICK1(5);
-    // ---- 5. Gauss-Jordan with partial pivoting, in registers --------------------------
-    {
+    // ---- 5. Gauss-Jordan with partial pivoting, in wave 0's registers -----------------
+    if (tid < 64) {
       unsigned used = 0;
       int pvk[P];
       double pk[P];
@@ -996,10 +1109,12 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
           p = r == pv ? colv[r] : p;
           prow = r == pv ? a[r] : prow;
         }
+        // row factors a[r][k] / p by one reciprocal (the divisions were half of a step)
         const bool upd_col = tid > k;
+        const double ip = 1.0 / p;
 #pragma unroll
         for (int r = 0; r < P; ++r) {
-          const double nv = fma(-(colv[r] / p), prow, a[r]);
+          const double nv = fma(-(colv[r] * ip), prow, a[r]);
           a[r] = (r != pv && upd_col) ? nv : a[r];
         }
         used |= 1u << pv;
@@ -1043,7 +1158,9 @@ __global__ __launch_bounds__(64) void k_ekf_filter_w1(EkfDims d, const int* __re
     for (int k = 0; k < 8; ++k) ekf_prof[seq * 8 + k] = s_prof[k];
 #endif
 #undef EKF_TICK1
-  if (tid == 0) outliers[seq] = nout;
+  if ((tid & 63) == 0 && nout) atomicAdd(reinterpret_cast<unsigned long long*>(&s_nout), (unsigned long long)nout);
+  __syncthreads();
+  if (tid == 0) outliers[seq] = s_nout;
 }
 
 // RTS smoother with the smoothed covariances (src/core/ekf.py:292-296), one workgroup per
@@ -1278,8 +1395,7 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
   io.outliers = dout;
   int* dbad = (int*)(dout + n_seq);
   ACS_HIP(ctx, hipMemsetAsync(dbad, 0, sizeof(int), s));
-  const size_t U = std::max(ekf_w1_fk_doubles(P, Jn, L),
-                            (size_t)d.npad * d.Ppad + (size_t)d.Ppad * (d.Ppad + d.npad + 1) + (size_t)d.Ppad * d.Ppad);
+  const size_t U = std::max(ekf_wg_fk_doubles(P, Jn, L, d.Ppad), ekf_wg_la_doubles(d.npad, d.Ppad));
   const size_t lds_f = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + U + d.npad +
                                           n_reals + (n_ints + 1) / 2 + 1);
   const size_t lds_w1 = sizeof(double) * ekf_w1_lds(d);
@@ -1289,14 +1405,26 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
     return e && e[0] == '1';
   }();
   const bool w1 = P == EKF_W1_P && lds_w1 <= 64 * 1024 && !force_wg;
+  // ACS_EKF_W1_WAVES: waves per sequence of the small-state filter (4 by default; 1 for A/B)
+  static const int w1_waves = [] {
+    const char* e = std::getenv("ACS_EKF_W1_WAVES");
+    return e && e[0] == '1' ? 1 : 4;
+  }();
   ACS_CHECK(ctx, w1 || lds_f <= 160 * 1024, "ekf: P = %d needs %zu bytes of LDS", P, lds_f);
   ACS_CHECK(ctx, ref_numerics >= 0 && ref_numerics <= ACS_EKF_ANALYTIC_H, "ekf: numerics mode %d", ref_numerics);
   // analytic H: the FkShared of one FK lives in the batched-FK region of the LDS union
-  // small states (the head model): one wave per sequence (k_ekf_filter_w1)
+  // small states (the head model): k_ekf_filter_w1
+#define EKF_W1_NW(f32, ah, nw)                                                                                     \
+  hipLaunchKernelGGL((k_ekf_filter_w1<f32, ah, EKF_W1_P, nw>), dim3(n_seq), dim3(64 * nw), lds_w1, s, d, io.I, \
+                     io.R, io.cams, io.meas, io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, dout, g_ekf_prof)
+#define EKF_W1(f32, ah)          \
+  if (w1_waves == 4)             \
+    EKF_W1_NW(f32, ah, 4);       \
+  else                           \
+    EKF_W1_NW(f32, ah, 1)
 #define EKF_FILTER(f32, ah)                                                                                         \
   if (w1)                                                                                                           \
-    hipLaunchKernelGGL((k_ekf_filter_w1<f32, ah, EKF_W1_P>), dim3(n_seq), dim3(64), lds_w1, s, d, io.I, io.R,      \
-                       io.cams, io.meas, io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, dout, g_ekf_prof); \
+    EKF_W1(f32, ah);                                                                                                \
   else                                                                                                              \
     hipLaunchKernelGGL((k_ekf_filter<f32, ah>), dim3(n_seq), dim3(512), lds_f, s, d, io.I, io.R, io.cams, io.meas, \
                        io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof)
