@@ -12,8 +12,11 @@
 //      (ekf_fk_batch), then the fisheye projection of (P+1) x C x L markers
 //   3. Kalman update in information form on the pose block: with H = [H_x 0 0] and R
 //      diagonal, K r = P[:,x] (I + A P_xx)^-1 b and (I - K H) P = P - P[:,x] (I + A P_xx)^-1
-//      A P[x,:], A = H_x^T R^-1 H_x, b = H_x^T R^-1 r (Woodbury; one P x P solve by
-//      Gauss-Jordan with partial pivoting instead of inverting the 2CL x 2CL S of :267)
+//      A P[x,:], A = H_x^T R^-1 H_x, b = H_x^T R^-1 r (Woodbury, instead of inverting the
+//      2CL x 2CL S of :267). (I + A P_xx)^-1 = W^-1 P_xx with W = P_xx + P_xx A P_xx
+//      symmetric positive definite: one P x P Gauss-Jordan with the pivots on the diagonal
+//      (no pivot search). Analytic H: A, b and the outlier diagonal in marker space (3 L
+//      rows, not 2 C L).
 //   4. the reference's 3-sigma outlier count from diag(S) = diag(H_x P_xx H_x^T) + diag R
 // With F32 (the reference numerics) the predicted state is rounded to float32 (:79), the
 // FK trig runs in float32, and the Jacobian perturbation is x + 1e-3 in float32.
@@ -59,11 +62,13 @@ __host__ __device__ inline size_t ekf_ah_alg_doubles(int L, int Ppad) {
   const size_t R3 = ekf_ah_rows(L);
   return ekf_ah_base() + 3 * R3 * (Ppad + 1) + R3 + 15 * (size_t)L;
 }
-// the 8-wave filter's algebra region: P[:, x] (npad x (Ppad + 1)), aug (Ppad x AW) and A
-// (Ppad x (Ppad + 1)); the odd row stride keeps the MFMA A-operand reads (16 rows, one
-// column) on distinct LDS banks
+// the 8-wave filter's algebra region: P[:, x] (npad x (Ppad + 1); before it, C and A C of the
+// update's solve, 2 Ppad rows), aug (Ppad x AW) and A (Ppad x (Ppad + 1)); the odd row stride
+// keeps the MFMA A-operand reads (16 rows, one column) on distinct LDS banks
+__host__ __device__ inline int ekf_wg_px_rows(int npad, int Ppad) { return npad > 2 * Ppad ? npad : 2 * Ppad; }
 __host__ __device__ inline size_t ekf_wg_la_doubles(int npad, int Ppad) {
-  return (size_t)npad * (Ppad + 1) + (size_t)Ppad * (Ppad + npad + 1) + (size_t)Ppad * (Ppad + 1);
+  return (size_t)ekf_wg_px_rows(npad, Ppad) * (Ppad + 1) + (size_t)Ppad * (Ppad + npad + 1) +
+         (size_t)Ppad * (Ppad + 1);
 }
 // the 8-wave filter's measurement-model region: batched FK (forward differences) or the
 // analytic H's FK and marker-space operands, whichever is larger
@@ -260,7 +265,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   double* fkb = U;                                    // batched FK of the P+1 poses
   const int LPx = Pp + 1;                             // row stride of sPx and sA
   double* sPx = U;                                    // npad x LPx: P[:, x] before the update
-  double* aug = sPx + (size_t)d.npad * LPx;           // Pp x AW
+  double* aug = sPx + (size_t)ekf_wg_px_rows(d.npad, Pp) * LPx;  // Pp x AW
   double* sA = aug + (size_t)Pp * AW;                 // Pp x LPx
   // the FK and algebra phases share U; what follows must start past the larger of the two
   const size_t u_fk = ekf_wg_fk_doubles(P, d.J, d.L, Pp);  // batched FK, or the analytic H's region
@@ -659,101 +664,58 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
         }
       }
       if (cnt) atomicAdd(&s_out, cnt);
-      for (int e = tid; e < d.npad * Pp; e += nth) {  // P[:, x] (after the tree used sPx)
-        const int r = e / Pp, c = e % Pp;
-        sPx[r * LPx + c] = (r < n && c < P) ? sP[r * LDP + c] : 0.0;
-      }
       __syncthreads();
     }
     EKF_TICK(4);
-    // aug = [I + A P_xx | A P[x, :] | b]: G2 = A P[0:Pp, :] on MFMA (A is zero outside
-    // P x P), then the M block gets the identity and its padding columns are cleared
-    wg_mgemm<false, false>(aug + Pp, AW, sA, LPx, sP, LDP, Pp, d.npad, Pp, 1.0, 0.0);
-    for (int e = tid; e < Pp * d.npad; e += nth) {  // G2 columns >= n must be zero
-      const int a = e / d.npad, c = e % d.npad;
-      if (c >= n) aug[a * AW + Pp + c] = 0.0;
-    }
-    __syncthreads();
+    // The update needs (I + A C)^-1 [A P[x, :] | b], C = P_xx. With W = C + C A C = C (I + A C),
+    // symmetric positive definite, (I + A C)^-1 = W^-1 C: a Gauss-Jordan on [W | C] with the
+    // pivots on the diagonal (no pivot search; the pivot row of step k is row k) gives
+    // V = (I + A C)^-1, then Z_G = (V A) P[x, :] and Z_b = V b on MFMA / per thread.
+    // Scratch: C, then V, in sPx's first Ppad x LPx; A C, then V A, in the next; [W | C] in
+    // aug's first 2 Ppad columns (P[:, x] is copied into sPx once they are consumed).
+    double* sC = sPx;
+    double* sAC = sPx + (size_t)Pp * LPx;
     for (int e = tid; e < Pp * Pp; e += nth) {
-      const int a = e / Pp, c = e % Pp;
-      aug[a * AW + c] = (c < P ? aug[a * AW + Pp + c] : 0.0) + (a == c ? 1.0 : 0.0);
+      const int r = e / Pp, c = e - r * Pp;
+      const double v = (r < P && c < P) ? sP[r * LDP + c] : 0.0;
+      sC[r * LPx + c] = v;
+      aug[r * AW + c] = v;
+      aug[r * AW + Pp + c] = v;
     }
-    if (tid >= P && tid < Pp) aug[tid * AW + Pp + d.npad] = 0.0;
     __syncthreads();
+    wg_mgemm<false, false>(sAC, LPx, sA, LPx, sC, LPx, Pp, Pp, Pp, 1.0, 0.0);  // A C
+    wg_mgemm<false, false>(aug, AW, sC, LPx, sAC, LPx, Pp, Pp, Pp, 1.0, 1.0);  // W = C + C (A C)
     EKF_TICK(5);
-    // Gauss-Jordan with partial pivoting on the P x P block, register-resident and one
-    // barrier per pivot. Thread (row gr = tid & 31, column group cg = tid >> 5) holds
-    // aug[gr][cg + 16 j]; pivoting is implicit (rows stay in place, a row is "used" once it
-    // has been a pivot). Step k: the 32 lanes owning column k pick the unused row with the
-    // largest |a[r][k]| (ties: lowest row), publish the row factors and the pivot row index
-    // in LDS; after the barrier every other row subtracts f_r = a[r][k] / a[pv][k] times the pivot
-    // row (read from the owning lane of the same wave by ds_bpermute). Columns <= k of the
-    // P x P block are finished and left stale. At the end row pv_k, divided by its pivot,
-    // is the solution row k.
+    // Gauss-Jordan on [W | C], register-resident, one barrier per pivot. Thread (row
+    // gr = tid & 31, column group cg = tid >> 5) holds aug[gr][cg + 16 j]. Step k: the 32
+    // lanes owning column k publish the row factors a[r][k] / a[k][k] (slot k carries the
+    // pivot); after the barrier every other row subtracts its factor times row k (read from
+    // the owning lane of the same wave by ds_bpermute). At the end row k over its pivot is
+    // row k of V.
     {
-      constexpr int NCG = 9;  // AW <= Ppad + npad + 1 <= 32 + 96 + 1 <= 16 * NCG
+      constexpr int NCG = 4;  // 2 Ppad <= 64 columns
       const int gr = tid & 31, cg = tid >> 5, half = cg & 1;
       double av[NCG];
 #pragma unroll
       for (int j = 0; j < NCG; ++j) {
         const int c = cg + 16 * j;
-        av[j] = (c < AW && gr < Pp) ? aug[gr * AW + c] : 0.0;
+        av[j] = (c < 2 * Pp && gr < Pp) ? aug[gr * AW + c] : 0.0;
       }
-      double* colb = sA;                          // 2 x 32 doubles (A is consumed)
-      int* pvb = reinterpret_cast<int*>(sA + 64);  // 2 ints
-      bool used = gr >= P;
-      int myk = -1;
+      double* colb = sAC;                           // 2 x 32 doubles (A C is consumed)
       double myp = 1.0;
-      __syncthreads();  // sA free
+      __syncthreads();  // sAC free
       for (int k = 0; k < P; ++k) {
         const int buf = k & 1;
         if (cg == (k & 15)) {
           const double colv = (k >> 4) ? av[1] : av[0];  // k < P <= FK_MAXP = 32 (checked on entry)
-          // arg max over the 32 lanes on the VALU: DPP inside each 16-lane row, then the
-          // row pair by v_permlane16_swap ((max, lowest row) is commutative and associative)
-          double best = used ? -1.0 : fabs(colv);
-          int bi = gr;
-          auto take = [&](double ob, int oi) {
-            const bool t = (ob > best) | ((ob == best) & (oi < bi));  // no short-circuit branches
-            best = t ? ob : best;
-            bi = t ? oi : bi;
-          };
-          take(dpp_f64<0xB1>(best), __builtin_amdgcn_mov_dpp(bi, 0xB1, 0xF, 0xF, false));
-          take(dpp_f64<0x4E>(best), __builtin_amdgcn_mov_dpp(bi, 0x4E, 0xF, 0xF, false));
-          take(dpp_f64<0x141>(best), __builtin_amdgcn_mov_dpp(bi, 0x141, 0xF, 0xF, false));
-          take(dpp_f64<0x140>(best), __builtin_amdgcn_mov_dpp(bi, 0x140, 0xF, 0xF, false));
-          {
-            const auto bh = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(best),
-                                                             (unsigned)__double2hiint(best), false, false);
-            const auto bl = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(best),
-                                                             (unsigned)__double2loint(best), false, false);
-            const auto bx = __builtin_amdgcn_permlane16_swap((unsigned)bi, (unsigned)bi, false, false);
-            // [0]: the even row's value, [1]: the odd row's, in every lane of the pair
-            const double b0 = __hiloint2double((int)bh[0], (int)bl[0]), b1 = __hiloint2double((int)bh[1], (int)bl[1]);
-            best = b0;
-            bi = (int)bx[0];
-            take(b1, (int)bx[1]);
-          }
-          // the column owner forms the row factors f_r = a[r][k] / a[pv][k] itself (slot
-          // pv carries the pivot), so after the barrier every lane needs two independent
-          // LDS reads and no division
-          const double p = read_lane_f64(colv, bi + 32 * half);
-          colb[buf * 32 + gr] = gr == bi ? p : colv * (1.0 / p);  // one reciprocal, uniform
-          if (gr == 0) pvb[buf] = bi;
+          const double p = read_lane_f64(colv, k + 32 * half);
+          colb[buf * 32 + gr] = gr == k ? p : colv * rcp_nr(p);  // one reciprocal (rcp + Newton), uniform
         }
         __syncthreads();
-        const int pv = pvb[buf];
         const double f = colb[buf * 32 + gr];
-        const bool piv = gr == pv;
-        if (piv) {
-          used = true;
-          myk = k;
-          myp = f;
-        }
-        const bool upd = !piv && gr < P;
-        const int src = (pv + 32 * half) << 2;  // the pivot row's lane of this half-wave
-        // every permute is issued before the first wait, and the update is a select (a
-        // branch per column put one LDS round trip per column on the critical path)
+        if (gr == k) myp = f;
+        const bool upd = gr != k && gr < P;
+        const int src = (k + 32 * half) << 2;  // row k's lane of this half-wave
         double prow[NCG];
 #pragma unroll
         for (int j = 0; j < NCG; ++j)
@@ -765,22 +727,37 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
           av[j] = (upd && (cg + 16 * j > k)) ? nv : av[j];
         }
       }
-      __syncthreads();  // every thread past its last read of aug
-      if (myk >= 0) {
-        const double ip = 1.0 / myp;
+      if (gr < P) {  // V rows into sC (every thread read sC into aug above)
+        const double ip = rcp_nr(myp);
 #pragma unroll
         for (int j = 0; j < NCG; ++j) {
           const int c = cg + 16 * j;
-          if (c >= Pp && c < AW) aug[myk * AW + c] = av[j] * ip;
+          if (c >= Pp && c < Pp + P) sC[gr * LPx + c - Pp] = av[j] * ip;
         }
       }
       __syncthreads();
     }
+    wg_mgemm<false, false>(sAC, LPx, sC, LPx, sA, LPx, Pp, Pp, Pp, 1.0, 0.0);  // Y = V A
+    if (tid < P) {  // Z_b = V b -> sA (A is consumed)
+      double v = 0.0;
+      for (int k = 0; k < P; ++k) v = fma(sC[tid * LPx + k], aug[k * AW + Pp + d.npad], v);
+      sA[tid] = v;
+    }
+    wg_mgemm<false, false>(aug + Pp, AW, sAC, LPx, sP, LDP, Pp, d.npad, Pp, 1.0, 0.0);  // Z_G = Y P[0:Pp, :]
+    for (int e = tid; e < d.npad * Pp; e += nth) {  // P[:, x] (V and Y are consumed)
+      const int r = e / Pp, c = e % Pp;
+      sPx[r * LPx + c] = (r < n && c < P) ? sP[r * LDP + c] : 0.0;
+    }
+    for (int e = tid; e < Pp * d.npad; e += nth) {  // Z_G columns >= n must be zero
+      const int r = e / d.npad, c = e % d.npad;
+      if (c >= n) aug[r * AW + Pp + c] = 0.0;
+    }
+    __syncthreads();
     EKF_TICK(6);
     // s += P[:, x] Z_b ;  P -= P[:, x] Z_G  (MFMA; sPx / Z are zero outside the live block)
     if (tid < n) {
       double v = 0.0;
-      for (int k = 0; k < P; ++k) v += sPx[tid * LPx + k] * aug[k * AW + Pp + d.npad];
+      for (int k = 0; k < P; ++k) v += sPx[tid * LPx + k] * sA[k];
       ss[tid] += v;
     }
     wg_mgemm<false, false>(sP, LDP, sPx, LPx, aug + Pp, AW, d.npad, d.npad, Pp, -1.0, 1.0);
@@ -807,21 +784,21 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
 //   * A = H^T R^-1 H and b = H^T R^-1 r one entry per lane of wave 0 (rows split over its
 //     half-waves, one shuffle); the 3-sigma test one observation per lane with P_xx in
 //     registers, compared squared (r^2 > 9 S_rr: no square root, no division);
-//   * the augmented [I + A P_xx | A P[x,:] | b] column-per-lane of wave 0 (P + n + 1 = 25
-//     columns) and Gauss-Jordan with partial pivoting in its registers: the pivot column's
-//     lane finds the pivot row in its own registers, that column reaches the other lanes by
-//     readlane, the row factors by one reciprocal; no step needs an LDS round trip or a
-//     barrier;
+//   * [W | P_xx], W = P_xx + P_xx A P_xx, column-per-lane of wave 0 (2 P = 12 columns) and
+//     Gauss-Jordan with the pivots on the diagonal in its registers (W is symmetric positive
+//     definite: no pivot search), the column-k entries by readlane, one reciprocal per step:
+//     V = (I + A P_xx)^-1 with no LDS round trip or barrier; meanwhile wave 1 forms
+//     [A P[x,:] | b], and [Z_G | Z_b] = V [A P[x,:] | b] column per thread;
 //   * the state / covariance update from the solution rows in LDS.
-// Same algorithm and pivoting rule (largest |a|, lowest row on ties) as k_ekf_filter; the
-// sums are in another order, so results agree to rounding (tests/test_gpu_ekf.py;
-// tools/ekf_drift.py: the same drift against the oracle as the 8-wave kernel over 250 frames).
+// Same algebra as k_ekf_filter; the sums are in another order, so results agree to rounding
+// (tests/test_gpu_ekf.py; tools/ekf_drift.py: the same drift against the oracle as the
+// 8-wave kernel over 250 frames).
 #define EKF_W1_P 6
 
 // LDS doubles of k_ekf_filter_w1
 __host__ __device__ inline size_t ekf_w1_lds(const EkfDims& d) {
   const size_t n = d.n, P = d.P, m = d.m;
-  return n * (n + 1) + d.npad + (P + 1) * m + m * P + 3 * m + n * P + P * (n + 1) + P * P + P +
+  return n * (n + 1) + d.npad + (P + 1) * m + m * P + 3 * m + n * P + P * (n + 1) + 2 * P * P + P +
          ekf_w1_fk_doubles(d.P, d.J, d.L) + d.n_reals + (d.n_ints + 1) / 2 + 1;
 }
 
@@ -835,8 +812,8 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
                                                       double* __restrict__ Ppred, double* __restrict__ Pest,
                                                       long long* __restrict__ outliers,
                                                       unsigned long long* ekf_prof) {
-  constexpr int P = PM, n = 3 * PM, LDP = n + 1, NZ1 = n + 1, NCOL = P + n + 1;
-  static_assert(NCOL <= 64, "one column per lane");
+  constexpr int P = PM, n = 3 * PM, LDP = n + 1, NZ1 = n + 1;
+  static_assert(n + 1 <= 64 && 2 * P <= 64, "one column per lane");
   const int seq = blockIdx.x;
   const int tid = threadIdx.x, nth = 64 * NW;
   const int m = d.m, CL = d.C * d.L;
@@ -853,7 +830,8 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
   double* sPx = sd2 + m;                                // n x P: P[:, x] before the update
   double* sZ = sPx + (size_t)n * P;                     // P x (n + 1): [Z_G | Z_b]
   double* sA = sZ + (size_t)P * NZ1;                    // P x P, then b (P)
-  double* fkb = sA + P * P + P;                         // FK scratch
+  double* sV = sA + P * P + P;                          // P x P: (I + A P_xx)^-1
+  double* fkb = sV + P * P;                             // FK scratch
   double* sRl = fkb + ekf_w1_fk_doubles(P, d.J, d.L);   // skeleton table (reals, then ints)
   int* sI = reinterpret_cast<int*>(sRl + d.n_reals);
 #ifdef EKF_PROFILE
@@ -1030,7 +1008,8 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
       for (int a = 0; a < P; ++a)
 #pragma unroll
         for (int b = 0; b < P; ++b) pxx[a][b] = sP[a * LDP + b];
-      for (int o = tid; o < CL; o += nth) {
+      // the observations go to waves 1.. first (wave 0 forms A and b meanwhile)
+      for (int o = NW > 1 ? (tid + nth - 64) % nth : tid; o < CL; o += nth) {
         bool out = false;
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
@@ -1060,76 +1039,89 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
     }
     __syncthreads();
     EKF_TICK1(4);
-    // ---- 4. [I + A P_xx | A P[x,:] | b], column c on lane c of wave 0 ----------------
+    // ---- 4. [W | C], W = C + C A C (C = P_xx), column c on lane c of wave 0 ----------
+    // (I + A C)^-1 = W^-1 C with W = C (I + A C) symmetric positive definite, so the solve
+    // needs no pivot search: Gauss-Jordan on the diagonal, every pivot row known in advance
     double a[P];
     if (tid < 64) {
       const int c = tid;
-      double av[P][P];
+      if (c < P) {
+        double ac[P];  // (A C)[:, c]
 #pragma unroll
-      for (int r = 0; r < P; ++r)
+        for (int r = 0; r < P; ++r) {
+          double v = 0.0;
 #pragma unroll
-        for (int k = 0; k < P; ++k) av[r][k] = sA[r * P + k];
-      double col[P];
-      const int j = c < P ? c : (c < P + n ? c - P : 0);
+          for (int k = 0; k < P; ++k) v = fma(sA[r * P + k], sP[k * LDP + c], v);
+          ac[r] = v;
+        }
 #pragma unroll
-      for (int k = 0; k < P; ++k) col[k] = sP[k * LDP + j];
+        for (int r = 0; r < P; ++r) {
+          double v = sP[r * LDP + c];
+#pragma unroll
+          for (int k = 0; k < P; ++k) v = fma(sP[r * LDP + k], ac[k], v);
+          a[r] = v;
+        }
+      } else {
+        const int j = c < 2 * P ? c - P : 0;
+#pragma unroll
+        for (int r = 0; r < P; ++r) a[r] = c < 2 * P ? sP[r * LDP + j] : 0.0;
+      }
+    }
+    // G = [A P[x, :] | b] into sZ, column c per thread: on wave 1 while wave 0 solves (one
+    // wave: before its solve)
+    auto g_column = [&](int c) {
+#pragma unroll
+      for (int r = 0; r < P; ++r) {
+        double v = 0.0;
+        if (c < n) {
+#pragma unroll
+          for (int k = 0; k < P; ++k) v = fma(sA[r * P + k], sP[k * LDP + c], v);
+        } else {
+          v = sA[P * P + r];
+        }
+        sZ[r * NZ1 + c] = v;
+      }
+    };
+    if constexpr (NW > 1) {
+      if (tid >= 64 && tid < 64 + n + 1) g_column(tid - 64);
+    } else {
+      if (tid < n + 1) g_column(tid);
+    }
+    EKF_TICK1(5);
+    // ---- 5. Gauss-Jordan without pivot search, in wave 0's registers -----------------
+    // step k: row k over its pivot, then a[r][k] times it off every other row (the
+    // column-k entries by readlane); at the end the right-hand block is V = (I + A C)^-1
+    if (tid < 64) {
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        const double ip = rcp_nr(read_lane_f64(a[k], k));
+        const double pr = tid > k ? a[k] * ip : a[k];
+        a[k] = pr;
+#pragma unroll
+        for (int r = 0; r < P; ++r) {
+          if (r == k) continue;
+          const double nv = fma(-read_lane_f64(a[r], k), pr, a[r]);
+          a[r] = tid > k ? nv : a[r];
+        }
+      }
+      if (tid >= P && tid < 2 * P) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) sV[k * P + tid - P] = a[k];
+      }
+    }
+    __syncthreads();
+    // [Z_G | Z_b] = V G, column c in place by thread c
+    if (tid < n + 1) {
+      const int c = tid;
+      double g[P];
+#pragma unroll
+      for (int k = 0; k < P; ++k) g[k] = sZ[k * NZ1 + c];
 #pragma unroll
       for (int r = 0; r < P; ++r) {
         double v = 0.0;
 #pragma unroll
-        for (int k = 0; k < P; ++k) v = fma(av[r][k], col[k], v);
-        if (c == r) v += 1.0;
-        a[r] = c < P + n ? v : (c == P + n ? sA[P * P + r] : 0.0);
-      }
-    }
-    EKF_TICK1(5);
-    // ---- 5. Gauss-Jordan with partial pivoting, in wave 0's registers -----------------
-    if (tid < 64) {
-      unsigned used = 0;
-      int pvk[P];
-      double pk[P];
-#pragma unroll
-      for (int k = 0; k < P; ++k) {
-        // the pivot column's lane: largest |a[r]| over the unused rows, lowest row on ties
-        double best = -1.0;
-        int bi = 0;
-#pragma unroll
-        for (int r = 0; r < P; ++r) {
-          const bool cand = !((used >> r) & 1u) && fabs(a[r]) > best;
-          best = cand ? fabs(a[r]) : best;
-          bi = cand ? r : bi;
-        }
-        const int pv = __builtin_amdgcn_readlane(bi, k);
-        double colv[P];
-#pragma unroll
-        for (int r = 0; r < P; ++r) colv[r] = read_lane_f64(a[r], k);
-        double p = 0.0, prow = 0.0;
-#pragma unroll
-        for (int r = 0; r < P; ++r) {
-          p = r == pv ? colv[r] : p;
-          prow = r == pv ? a[r] : prow;
-        }
-        // row factors a[r][k] / p by one reciprocal (the divisions were half of a step)
-        const bool upd_col = tid > k;
-        const double ip = 1.0 / p;
-#pragma unroll
-        for (int r = 0; r < P; ++r) {
-          const double nv = fma(-(colv[r] * ip), prow, a[r]);
-          a[r] = (r != pv && upd_col) ? nv : a[r];
-        }
-        used |= 1u << pv;
-        pvk[k] = pv;
-        pk[k] = p;
-      }
-      // solution row k = row pv_k over its pivot: the right-hand-side columns (lanes >= P)
-      if (tid >= P && tid < NCOL) {
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-          double v = 0.0;
-#pragma unroll
-          for (int r = 0; r < P; ++r) v = r == pvk[k] ? a[r] : v;
-          sZ[k * NZ1 + tid - P] = v * (1.0 / pk[k]);
-        }
+        for (int k = 0; k < P; ++k) v = fma(sV[r * P + k], g[k], v);
+        sZ[r * NZ1 + c] = v;
       }
     }
     __syncthreads();
