@@ -512,7 +512,7 @@ def bench_ekf(ctx, torch, n_seq, n_frames, n_cams, world, rank, mode='default', 
             'outliers_frac': float(np.mean(out['outliers'])) / max(1.0, float(np.sum(lik > 0.5)) * 2 / n_seq),
             'numerics': ('reference (float32 state rounding, FD Jacobian eps 1e-3)' if jacobian == 'fd' else
                          'float64, analytic H from the FK Jacobian (SURVEY §8(f)2)'),
-            'kernel': 'k_ekf_filter_w1 (one wave per sequence)' if P == 6 else 'k_ekf_filter (8 waves per sequence)'}
+            'kernel': 'k_ekf_filter_w1 (4 waves per sequence)' if P == 6 else 'k_ekf_filter (8 waves per sequence)'}
 
 
 def bench_pipeline(ctx, torch, stream, world, rank, n_seq=80, n_frames=250, n_cams=12, steps=3):
