@@ -41,7 +41,7 @@ fi
 if [[ $STEPS == *list* ]]; then
   run counters 120 rocprofv3 -L
 fi
-if [[ $STEPS == *pmc* ]]; then
+if [[ ",$STEPS," == *,pmc,* ]]; then
   # HBM traffic (guide: separate passes; FETCH_SIZE x2 on gfx950) and FP64 VALU counts
   export TMPDIR=/tmp
   PMC_ARGS="--no-cpu-baseline --no-fte --steps 3 --warmup 1 --ekf-seqs 0 --pipeline-seqs 0 --window-frames 0"
@@ -52,5 +52,14 @@ if [[ $STEPS == *pmc* ]]; then
     run pmc_valu 600 rocprofv3 --pmc $PMC_VALU --output-format csv -d "$OUT/pmc_${TAG}_valu" -o run -- python3 "$REPO/bench.py" $PMC_ARGS
   fi
   python tools/pmc_summary.py "$OUT/pmc_${TAG}" "$OUT/traffic_${TAG}.json" > "$OUT/pmc_summary_${TAG}.log" 2>&1 || true
+fi
+if [[ $STEPS == *ftepmc* ]]; then
+  # FTE HBM traffic at configs[3] size (FETCH_SIZE / WRITE_SIZE passes of one 10k-frame solve)
+  # and the FETCH_SIZE factor of 8-B and 16-B per lane streams (tools/probe/fetch_calib)
+  export TMPDIR=/tmp
+  run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_${TAG}_fetch" -o run -- "$REPO/tools/probe/fetch_calib"
+  run ftepmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/ftepmc_${TAG}_fetch" -o run -- python3 "$REPO/tools/prof_fte.py" --frames 10000 --reps 1
+  run ftepmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/ftepmc_${TAG}_write" -o run -- python3 "$REPO/tools/prof_fte.py" --frames 10000 --reps 1
+  python tools/pmc_summary.py "$OUT/ftepmc_${TAG}" "$OUT/traffic_fte10k_${TAG}.json" > "$OUT/ftepmc_summary_${TAG}.log" 2>&1 || true
 fi
 echo done
