@@ -224,6 +224,87 @@ __device__ void ekf_fk_batch(const SkelView& sk, const double* ss, double eps, d
   __syncthreads();
 }
 
+// Marker l's position at Jacobian pose q, from scratch in one thread: ekf_fk_batch's
+// arithmetic (the same G, M and node sums in the same order) without its shared tables and
+// barriers. For skeletons of one joint (the head model), where recomputing the joint's
+// rotation per (pose, marker) item is cheaper than the batch's four dependent workgroup
+// phases.
+template <bool F32>
+__device__ void ekf_fk_point(const SkelView& sk, const double* ss, double eps, int q, int l, double* out) {
+  const int* pk = sk.pk;
+  auto G_of = [&](int j, double* G) {
+    const int* jt = sk.joints + 8 * j;
+    const int nrot = jt[1];
+    double sn[3] = {0.0, 0.0, 0.0}, cs[3] = {1.0, 1.0, 1.0};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      if (r >= nrot) break;
+      const double v = ekf_xq<F32>(ss, q, jt[5 + r], eps);
+      if (F32) {
+        float sf, cf;
+        sincosf((float)v, &sf, &cf);
+        sn[r] = sf;
+        cs[r] = cf;
+      } else {
+        sincos(v, &sn[r], &cs[r]);
+      }
+    }
+#pragma unroll
+    for (int col = 0; col < 3; ++col) {
+      double v[3] = {col == 0 ? 1.0 : 0.0, col == 1 ? 1.0 : 0.0, col == 2 ? 1.0 : 0.0};
+      for (int r = 0; r < nrot; ++r) {
+        double w[3];
+        act_rot_vec(jt[2 + r], sn[r], cs[r], v, w);
+        v[0] = w[0];
+        v[1] = w[1];
+        v[2] = w[2];
+      }
+      G[col] = v[0];
+      G[3 + col] = v[1];
+      G[6 + col] = v[2];
+    }
+  };
+  double p0 = 0.0, p1 = 0.0, p2 = 0.0;
+  int node = sk.outn[l];
+  while (true) {
+    const int* nd = sk.nodes + 4 * node;
+    const int base = nd[0];
+    if (base == -2 || base == -1) {  // the root (or world) translation of pose q
+      const int kind = base == -2 ? PK_WORLD : PK_TRANS;
+      double t[3] = {0.0, 0.0, 0.0};
+      for (int p = 0; p < sk.P; ++p)
+        if (pk[4 * p] == kind) {
+          const int a = pk[4 * p + 1];
+          const double x = ekf_xq<F32>(ss, q, p, eps);
+          t[0] += a == 0 ? x : 0.0;
+          t[1] += a == 1 ? x : 0.0;
+          t[2] += a == 2 ? x : 0.0;
+        }
+      p0 += t[0];
+      p1 += t[1];
+      p2 += t[2];
+      break;
+    }
+    double Mm[9], G[9], T[9];  // M of the node's frame: G_root .. G_parent G_frame
+    G_of(nd[1], Mm);
+    for (int k = sk.joints[8 * nd[1]]; k >= 0; k = sk.joints[8 * k]) {
+      G_of(k, G);
+      mat3_mul(G, Mm, T);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Mm[i] = T[i];
+    }
+    double o0 = sk.off[3 * node], o1 = sk.off[3 * node + 1], o2 = sk.off[3 * node + 2];
+    if (nd[2] >= 0) o0 = ekf_xq<F32>(ss, q, nd[2], eps);
+    p0 += Mm[0] * o0 + Mm[1] * o1 + Mm[2] * o2;
+    p1 += Mm[3] * o0 + Mm[4] * o1 + Mm[5] * o2;
+    p2 += Mm[6] * o0 + Mm[7] * o1 + Mm[8] * o2;
+    node = base;
+  }
+  out[0] = p0;
+  out[1] = p1;
+  out[2] = p2;
+}
+
 // Row / column of the flat index e = tid, tid + nth, ... over rows of nc columns, stepped
 // without an integer division per element (nth / nc and nth % nc once per loop).
 struct Walk2 {
@@ -271,7 +352,8 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   const size_t u_fk = ekf_wg_fk_doubles(P, d.J, d.L, Pp);  // batched FK, or the analytic H's region
   const size_t u_la = ekf_wg_la_doubles(d.npad, Pp);
   double* ss = U + (u_fk > u_la ? u_fk : u_la);      // n: state
-  double* sRl = ss + d.npad;                          // skeleton table (reals, then ints)
+  double* sCam = ss + d.npad;                         // camera records (every projection reads them)
+  double* sRl = sCam + (size_t)d.C * ACS_CAM_STRIDE;  // skeleton table (reals, then ints)
   int* sI = reinterpret_cast<int*>(sRl + d.n_reals);
 #ifdef EKF_PROFILE  // per-phase cycle counts (tools/prof_ekf_phases.py)
   __shared__ unsigned long long s_prof[8];
@@ -292,10 +374,12 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   __shared__ unsigned long long s_out;
   for (int e = tid; e < d.n_ints; e += nth) sI[e] = I[e];  // the FK walks the table: keep it in LDS
   for (int e = tid; e < d.n_reals; e += nth) sRl[e] = Rl[e];
+  for (int e = tid; e < d.C * ACS_CAM_STRIDE; e += nth) sCam[e] = cams[e];
   __syncthreads();  // skel_view reads the header right away
   const SkelView sk = skel_view(sI, sRl);
   const double sT = d.sT, h2 = 0.5 * sT * sT;
-  // per-sequence scratch: hpose (P+1) x m; H, W H (mpad x Pp); res, w (mpad)
+  // per-sequence scratch: hpose (P+1) x m (analytic H: h, then 6 CL projection Jacobians);
+  // H, W H (mpad x Pp, forward differences); res, w (mpad)
   const int mp = d.mpad;
   double* hpose = scratch + (size_t)seq * ((size_t)(P + 1) * m + 2 * (size_t)mp * Pp + 2 * mp);
   double* H = hpose + (size_t)(P + 1) * m;
@@ -375,7 +459,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
         const int c = o / d.L, l = o - c * d.L;
         const double* x = fsh.pos[sk.outn[l]];
         ProjOut po;
-        fisheye_project<true>(cams + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
+        fisheye_project<true>(sCam + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
         hpose[2 * o] = po.u;
         hpose[2 * o + 1] = po.v;
         double* jo = hpose + m + 6 * (size_t)o;
@@ -399,7 +483,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
         const int c = o / d.L, l = o - c * d.L;
         const double* x = pos + ((size_t)q * d.L + l) * 3;
         ProjOut po;
-        fisheye_project<false>(cams + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
+        fisheye_project<false>(sCam + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
         hpose[(size_t)q * m + 2 * o] = po.u;
         hpose[(size_t)q * m + 2 * o + 1] = po.v;
       }
@@ -408,8 +492,8 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     }
     EKF_TICK(2);
     // residual and R^-1 per row (row r = 2 (c L + l) + d, the reference's ordering; rows
-    // past m are zero padding for the MFMA products), then H and W H element-parallel
-    // (coalesced stores)
+    // past m are zero padding for the MFMA products), then (forward differences) H and W H
+    // element-parallel (coalesced stores)
     for (int r = tid; r < mp; r += nth) {
       double e = 0.0, w = 0.0;
       if (r < m) {
@@ -799,7 +883,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
 __host__ __device__ inline size_t ekf_w1_lds(const EkfDims& d) {
   const size_t n = d.n, P = d.P, m = d.m;
   return n * (n + 1) + d.npad + (P + 1) * m + m * P + 3 * m + n * P + P * (n + 1) + 2 * P * P + P +
-         ekf_w1_fk_doubles(d.P, d.J, d.L) + d.n_reals + (d.n_ints + 1) / 2 + 1;
+         ekf_w1_fk_doubles(d.P, d.J, d.L) + (size_t)d.C * ACS_CAM_STRIDE + d.n_reals + (d.n_ints + 1) / 2 + 1;
 }
 
 template <bool F32, bool AH, int PM, int NW>
@@ -832,7 +916,8 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
   double* sA = sZ + (size_t)P * NZ1;                    // P x P, then b (P)
   double* sV = sA + P * P + P;                          // P x P: (I + A P_xx)^-1
   double* fkb = sV + P * P;                             // FK scratch
-  double* sRl = fkb + ekf_w1_fk_doubles(P, d.J, d.L);   // skeleton table (reals, then ints)
+  double* sCam = fkb + ekf_w1_fk_doubles(P, d.J, d.L);  // camera records (read by every projection)
+  double* sRl = sCam + (size_t)d.C * ACS_CAM_STRIDE;     // skeleton table (reals, then ints)
   int* sI = reinterpret_cast<int*>(sRl + d.n_reals);
 #ifdef EKF_PROFILE
   unsigned long long s_prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = 0;
@@ -850,6 +935,7 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
 #endif
   for (int e = tid; e < d.n_ints; e += nth) sI[e] = I[e];
   for (int e = tid; e < d.n_reals; e += nth) sRl[e] = Rl[e];
+  for (int e = tid; e < d.C * ACS_CAM_STRIDE; e += nth) sCam[e] = cams[e];
   for (int e = tid; e < n * LDP; e += nth) {
     const int r = e / LDP, c = e - r * LDP;
     sP[e] = c < n ? P0[r * n + c] : 0.0;
@@ -924,11 +1010,24 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
         const int c = o / d.L, l = o - c * d.L;
         const double* x = fsh.pos[sk.outn[l]];
         ProjOut po;
-        fisheye_project<true>(cams + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
+        fisheye_project<true>(sCam + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
         hp[2 * o] = po.u;
         hp[2 * o + 1] = po.v;
 #pragma unroll
         for (int k = 0; k < 6; ++k) hp[m + 6 * o + k] = po.J[k];
+      }
+    } else if (sk.J == 1) {
+      // one joint: every (pose, observation) item computes its marker from scratch and
+      // projects it, no workgroup phase in between
+      for (int e = tid; e < (P + 1) * CL; e += nth) {
+        const int q = e / CL, o = e - q * CL;
+        const int c = o / d.L, l = o - c * d.L;
+        double x[3];
+        ekf_fk_point<F32>(sk, ss, d.eps, q, l, x);
+        ProjOut po;
+        fisheye_project<false>(sCam + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
+        hp[(size_t)q * m + 2 * o] = po.u;
+        hp[(size_t)q * m + 2 * o + 1] = po.v;
       }
     } else {
       ekf_fk_batch<F32>(sk, ss, d.eps, fkb, tid, nth);
@@ -938,7 +1037,7 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
         const int c = o / d.L, l = o - c * d.L;
         const double* x = pos + ((size_t)q * d.L + l) * 3;
         ProjOut po;
-        fisheye_project<false>(cams + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
+        fisheye_project<false>(sCam + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
         hp[(size_t)q * m + 2 * o] = po.u;
         hp[(size_t)q * m + 2 * o + 1] = po.v;
       }
@@ -1276,6 +1375,68 @@ __global__ __launch_bounds__(256) void k_ekf_gain(EkfDims d, const double* __res
   }
 }
 
+// The same gains for small states (n = NN <= 32, the head model), one wave per (sequence,
+// frame), GW waves per workgroup. P_pred is symmetric positive definite, so
+// A_i^T = P_pred^-1 (P_est F^T)^T comes from a Gauss-Jordan on [P_pred | (P_est F^T)^T] with
+// the pivots on the diagonal (no pivot search): column c on lane c, rows in registers, the
+// column-k entries by readlane. Lane NN + c ends with column c of A_i^T, i.e. row c of A_i.
+template <int NN, int GW>
+__global__ __launch_bounds__(64 * GW) void k_ekf_gain_w(EkfDims d, const double* __restrict__ Pest, double* Ppred,
+                                                        int* __restrict__ bad) {
+  static_assert(2 * NN <= 64, "one column per lane");
+  const int N1 = d.N - 1, lane = threadIdx.x & 63;
+  const long long g = (long long)blockIdx.x * GW + (threadIdx.x >> 6);
+  if (g >= (long long)d.S * N1) return;  // whole wave
+  const int seq = (int)(g / N1), i = (int)(g - (long long)seq * N1);
+  const int P = d.P;
+  const double sT = d.sT, h2 = 0.5 * sT * sT;
+  constexpr size_t nn0 = (size_t)NN * NN;
+  const size_t base = (size_t)seq * d.N;
+  const double* Pe = Pest + (base + i) * nn0;
+  double* Pp1 = Ppred + (base + i + 1) * nn0;
+  double a[NN];
+  if (lane < NN) {
+#pragma unroll
+    for (int r = 0; r < NN; ++r) a[r] = Pp1[r * NN + lane];
+  } else if (lane < 2 * NN) {
+    const int c = lane - NN;  // row c of P_est F^T, as column c of its transpose
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+      double v = Pe[c * NN + k];
+      if (k < 2 * P) v += sT * Pe[c * NN + k + P];
+      if (k < P) v += h2 * Pe[c * NN + k + 2 * P];
+      a[k] = v;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < NN; ++r) a[r] = 0.0;
+  }
+  int nbad = 0;  // pivots that are not positive (counted as k_ekf_gain counts singular ones)
+#pragma unroll
+  for (int k = 0; k < NN; ++k) {
+    double p = read_lane_f64(a[k], k);
+    const bool ok = p > 0.0;
+    nbad += ok ? 0 : 1;
+    p = ok ? p : 1e-300;
+    const double ip = rcp_nr(p);
+    const double pr = lane > k ? a[k] * ip : a[k];
+    a[k] = pr;
+#pragma unroll
+    for (int r = 0; r < NN; ++r) {
+      if (r == k) continue;
+      const double nv = fma(-read_lane_f64(a[r], k), pr, a[r]);
+      a[r] = lane > k ? nv : a[r];
+    }
+  }
+  if (nbad && lane == 0) atomicAdd(bad, nbad);
+  if (lane >= NN && lane < 2 * NN) {  // P_pred[i+1] was read by this wave only: A_i in its place
+    const int c = lane - NN;
+#pragma unroll
+    for (int k = 0; k < NN; ++k) Pp1[c * NN + k] = a[k];
+  }
+}
+#define EKF_GAIN_W 4
+
 // Smoothed states x_s[i] = x_est[i] + A_i (x_s[i+1] - x_pred[i+1]) (src/core/ekf.py:295), one
 // workgroup per sequence: a row per aligned group of 8 lanes (3 passes cover n <= 96), the
 // gain of the next frame loaded while this frame's products are summed.
@@ -1339,6 +1500,73 @@ __global__ __launch_bounds__(256) void k_ekf_smooth_x(EkfDims d, const double* _
   }
 }
 
+// The same recursion for the models' state sizes (n = NN: 18, 78, 87): a row per group of 8 lanes,
+// QN = ceil(NN / 8) columns per lane, and the gains of the next D frames already in registers
+// (a ring of D register sets, the frame loop unrolled by D so every index is static). A step
+// is then one LDS read, QN FMAs, a 3-step DPP sum and a barrier; the gain loads of frame i
+// are issued D steps before they are used, which hides their latency (one frame ahead
+// left ~1.7 us of it per frame, profiles/r04).
+template <int NN, int D>
+__global__ __launch_bounds__(((8 * NN + 63) / 64) * 64) void k_ekf_smooth_xs(EkfDims d, const double* __restrict__ xpred,
+                                                                             const double* __restrict__ xest,
+                                                                             const double* __restrict__ Ag,
+                                                                             double* __restrict__ xs) {
+  constexpr int QN = (NN + 7) / 8;
+  constexpr size_t nn0 = (size_t)NN * NN;
+  const int seq = blockIdx.x, tid = threadIdx.x;
+  const size_t base = (size_t)seq * d.N;
+  __shared__ double sv[2][NN];
+  const int j = tid & 7, r = tid >> 3;
+  const bool live = r < NN;
+  if (tid < NN) {
+    const double v = xest[(base + d.N - 1) * NN + tid];
+    xs[(base + d.N - 1) * NN + tid] = v;
+    sv[(d.N - 1) & 1][tid] = v - xpred[(base + d.N - 1) * NN + tid];
+  }
+  double a[D][QN], xe[D], xp[D];
+  auto load = [&](int u, int i) {  // slot u <- A_i (in P_pred[i+1]'s slot), x_est[i], x_pred[i]
+    const double* A = Ag + (base + i + 1) * nn0;
+#pragma unroll
+    for (int q = 0; q < QN; ++q) {
+      const int c = j + 8 * q;
+      a[u][q] = (live && c < NN && i >= 0) ? A[r * NN + c] : 0.0;
+    }
+    xe[u] = (live && j == 0 && i >= 0) ? xest[(base + i) * NN + r] : 0.0;
+    xp[u] = (live && j == 0 && i >= 0) ? xpred[(base + i) * NN + r] : 0.0;
+  };
+#pragma unroll
+  for (int u = 0; u < D; ++u) load(u, d.N - 2 - u);
+  for (int i0 = d.N - 2; i0 >= 0; i0 -= D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int i = i0 - u;
+      if (i < 0) break;  // uniform
+      __syncthreads();
+      const double* v = sv[(i + 1) & 1];
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < QN; ++q) {
+        const int c = j + 8 * q;
+        if (c < NN) acc = fma(a[u][q], v[c], acc);
+      }
+      const double xe_i = xe[u], xp_i = xp[u];
+      load(u, i - D);
+      acc = group_sum<8>(acc);
+      if (live && j == 0) {
+        const double x = xe_i + acc;
+        xs[(base + i) * NN + r] = x;
+        sv[i & 1][r] = x - xp_i;
+      }
+    }
+  }
+}
+#define EKF_SX_D 8
+// deep register ring for small states, 2 frames ahead for the 26 / 29-parameter models (11
+// waves: the VGPR budget of 3 waves per SIMD)
+#define EKF_SMOOTH_XS(NN_, D_)                                                                                  \
+  hipLaunchKernelGGL((k_ekf_smooth_xs<NN_, D_>), dim3(n_seq), dim3(((8 * NN_ + 63) / 64) * 64), 0, s, d,      \
+                     (const double*)dxp, (const double*)dxe, (const double*)dPp, dxs)
+
 unsigned long long* g_ekf_prof = nullptr;
 
 // Filter + smoother on device buffers (common.hpp). hdr = the skeleton table header. x_pred
@@ -1389,7 +1617,7 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
   ACS_HIP(ctx, hipMemsetAsync(dbad, 0, sizeof(int), s));
   const size_t U = std::max(ekf_wg_fk_doubles(P, Jn, L, d.Ppad), ekf_wg_la_doubles(d.npad, d.Ppad));
   const size_t lds_f = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + U + d.npad +
-                                          n_reals + (n_ints + 1) / 2 + 1);
+                                          (size_t)n_cams * ACS_CAM_STRIDE + n_reals + (n_ints + 1) / 2 + 1);
   const size_t lds_w1 = sizeof(double) * ekf_w1_lds(d);
   // ACS_EKF_WG=1 keeps the 8-wave kernel for every model (A/B measurements, tools/ekf_drift.py)
   static const bool force_wg = [] {
@@ -1434,14 +1662,25 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
   } else {
     // gains in parallel over (sequence, frame), then the state recursion per sequence
     ACS_CHECK(ctx, d.npad <= 96, "ekf: n = %d", d.n);
-    if (n_frames >= 2) {
+    if (n_frames >= 2 && n == 3 * EKF_W1_P) {  // small states: one wave per gain
+      const size_t ng = (size_t)n_seq * (n_frames - 1);
+      hipLaunchKernelGGL((k_ekf_gain_w<3 * EKF_W1_P, EKF_GAIN_W>), dim3((unsigned)((ng + EKF_GAIN_W - 1) / EKF_GAIN_W)),
+                         dim3(64 * EKF_GAIN_W), 0, s, d, (const double*)dPe, dPp, dbad);
+    } else if (n_frames >= 2) {
       const size_t lds_g = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + 512);
       hipLaunchKernelGGL(k_ekf_gain, dim3((unsigned)((size_t)n_seq * (n_frames - 1))), dim3(256), lds_g, s, d,
                          (const double*)dPe, dPp, dbad);
       ACS_HIP(ctx, hipGetLastError());
     }
-    hipLaunchKernelGGL(k_ekf_smooth_x, dim3(n_seq), dim3(256), 0, s, d, (const double*)dxp, (const double*)dxe,
-                       (const double*)dPp, dxs);
+    if (n == 3 * EKF_W1_P)
+      EKF_SMOOTH_XS(3 * EKF_W1_P, EKF_SX_D);
+    else if (n == 78)  // default_nolure
+      EKF_SMOOTH_XS(78, 2);
+    else if (n == 87)  // default
+      EKF_SMOOTH_XS(87, 2);
+    else
+      hipLaunchKernelGGL(k_ekf_smooth_x, dim3(n_seq), dim3(256), 0, s, d, (const double*)dxp, (const double*)dxe,
+                         (const double*)dPp, dxs);
   }
   ACS_HIP(ctx, hipGetLastError());
   return ACS_OK;
