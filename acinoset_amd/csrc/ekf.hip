@@ -1500,7 +1500,7 @@ __global__ __launch_bounds__(256) void k_ekf_smooth_x(EkfDims d, const double* _
   }
 }
 
-// The same recursion for the models' state sizes (n = NN: 18, 78, 87): a row per group of 8 lanes,
+// The same recursion for the models' state sizes (n = NN: 18, 87): a row per group of 8 lanes,
 // QN = ceil(NN / 8) columns per lane, and the gains of the next D frames already in registers
 // (a ring of D register sets, the frame loop unrolled by D so every index is static). A step
 // is then one LDS read, QN FMAs, a 3-step DPP sum and a barrier; the gain loads of frame i
@@ -1561,7 +1561,7 @@ __global__ __launch_bounds__(((8 * NN + 63) / 64) * 64) void k_ekf_smooth_xs(Ekf
   }
 }
 #define EKF_SX_D 8
-// deep register ring for small states, 2 frames ahead for the 26 / 29-parameter models (11
+// deep register ring for small states, 2 frames ahead for the 29-parameter model (11
 // waves: the VGPR budget of 3 waves per SIMD)
 #define EKF_SMOOTH_XS(NN_, D_)                                                                                  \
   hipLaunchKernelGGL((k_ekf_smooth_xs<NN_, D_>), dim3(n_seq), dim3(((8 * NN_ + 63) / 64) * 64), 0, s, d,      \
@@ -1674,8 +1674,6 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
     }
     if (n == 3 * EKF_W1_P)
       EKF_SMOOTH_XS(3 * EKF_W1_P, EKF_SX_D);
-    else if (n == 78)  // default_nolure
-      EKF_SMOOTH_XS(78, 2);
     else if (n == 87)  // default
       EKF_SMOOTH_XS(87, 2);
     else

@@ -210,3 +210,19 @@ def test_ekf_analytic_h_rejects_reference_numerics(ctx):
     g, s0, cp = _setup('head')
     with pytest.raises(ValueError, match='float64'):
         cekf.run(g['uv'][:3], g['likelihood'][:3], cp, 'head', 90.0, s0, ctx=ctx, jacobian='analytic')
+
+
+@pytest.mark.parametrize('mode,N', [('head', 60), ('default', 12)])
+def test_ekf_parallel_gains_match_sequential_smoother(ctx, mode, N):
+    """The RTS pass without covariances (per-(sequence, frame) gains: k_ekf_gain_w for the
+    18-state head model, k_ekf_gain otherwise; the smoothed-state recursion k_ekf_smooth_xs
+    at 18 / 87 states) against the sequential smoother that also forms the smoothed
+    covariances (k_ekf_smooth), on the same filter output: the same gains
+    (src/core/ekf.py:294) by another solve, so rounding-level agreement."""
+    scene, seq, s0, cp, covs = _setup_ring(mode, N)
+    a = cekf.run(seq.uv, seq.likelihood, cp, mode, 90.0, s0, ref_numerics=False, cal_covs=covs, ctx=ctx)
+    b = cekf.run(seq.uv, seq.likelihood, cp, mode, 90.0, s0, ref_numerics=False, cal_covs=covs, covariances=True,
+                 ctx=ctx)
+    np.testing.assert_array_equal(a['x_est'], b['x_est'])
+    sc = max(1.0, float(np.abs(b['x_smooth']).max()))
+    np.testing.assert_allclose(a['x_smooth'], b['x_smooth'], atol=1e-9 * sc, rtol=0)
