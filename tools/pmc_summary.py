@@ -3,12 +3,14 @@ profiles/<round>/traffic.json: per (kernel, grid size) HBM bytes per launch and 
 flops per launch.
 
 HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
-WRITE_SIZE come from separate passes, are reported in KiB, and on gfx950 FETCH_SIZE counts
-half of the bytes of wide coalesced reads (16 B per lane); other widths are uncalibrated.
-So the x2 correction applies only to the share of a kernel's reads that are 16-B-per-lane
-streams (WIDE_SHARE below, from the kernel's own load widths); the rest is taken as
-counted (fetch_bytes = FETCH_SIZE x (1 + wide share)), and kernels without an entry are
-reported uncorrected with `fetch_calibrated: false`.
+WRITE_SIZE come from separate passes and are reported in KiB. On gfx950 FETCH_SIZE counts
+half of the bytes of coalesced streaming reads. The guide gives this for 16 B per lane;
+tools/probe/fetch_calib measured it for 8 B per lane too (profiles/r04/fetch_calib.txt: 1 GiB
+read as double or double2, FETCH_SIZE = 0.500 GiB both times). So the x2 correction applies to
+the share of a kernel's reads that are 8- or 16-B-per-lane streams (WIDE_SHARE below, from
+the kernel's own load widths); the rest is taken as counted
+(fetch_bytes = FETCH_SIZE x (1 + share)). Kernels without an entry are reported uncorrected,
+with `fetch_calibrated: false`.
 FP64 flops = 64 lanes x (2 FMA + ADD + MUL + TRANS) wave instructions (SQ_INSTS_VALU_*_F64;
 an upper bound when lanes are masked off).
 
@@ -20,10 +22,14 @@ import sys
 import pandas as pd
 
 
-# share of the algorithmic read bytes loaded 16 B per lane (double2), per kernel:
-# k_sba_lm reads per point 16 B x C of observations (double2 per lane), C mask bytes
-# (1 B per lane) and 24 B of start point (8-B loads): 96 / (96 + 6 + 24) at C = 6
-WIDE_SHARE = {'k_sba_lm': 96.0 / 126.0}
+# share of the algorithmic read bytes loaded 8 or 16 B per lane, per kernel. k_sba_lm reads,
+# per point, 16 B x C of observations (double2 per lane), C mask bytes (1 B per lane:
+# uncalibrated, taken as counted) and 24 B of start point (8-B loads): (96 + 24) / 126 at
+# C = 6. The FTE kernels read float64 rows (8-B loads; the skeleton table's ints are
+# negligible).
+WIDE_SHARE = {'k_sba_lm': 120.0 / 126.0, 'k_cr_level': 1.0, 'k_cr_assemble_build': 1.0, 'k_cr_back_all': 1.0,
+              'k_fte_linearize': 1.0, 'k_fte_cost': 1.0, 'k_cr_build': 1.0, 'k_fte_assemble': 1.0,
+              'k_cr_back': 1.0, 'k_cr_trial': 1.0, 'k_cr_tau_partial': 1.0, 'k_cr_top': 1.0}
 
 
 def load(prefix, kind):
