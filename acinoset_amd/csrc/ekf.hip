@@ -1087,8 +1087,24 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
       const int t = tid & 31, part = tid >> 5, mh = (m + 1) >> 1;
       const int r0 = part ? mh : 0, r1 = part ? m : mh;
       double v = 0.0;
-      if (t < nAb)
-        for (int r = r0; r < r1; ++r) v = fma(sw[r] * sH[r * P + ea], eb >= 0 ? sH[r * P + eb] : sr[r], v);
+      if (t < nAb) {
+        // rows 8 at a time, their loads issued before the FMAs (same summation order)
+        const double* ca = sH + ea;
+        const double* cb = eb >= 0 ? sH + eb : sr;
+        const int sb = eb >= 0 ? P : 1;
+        int r = r0;
+        for (; r + 8 <= r1; r += 8) {
+          double wa[8], bb[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            wa[u] = sw[r + u] * ca[(r + u) * P];
+            bb[u] = cb[(r + u) * sb];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v = fma(wa[u], bb[u], v);
+        }
+        for (; r < r1; ++r) v = fma(sw[r] * ca[r * P], cb[r * sb], v);
+      }
       v += __shfl_xor(v, 32);
       if (part == 0 && t < nAb) {
         if (eb >= 0) {
