@@ -645,8 +645,11 @@ def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl',
         tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    each = []
     for _ in range(steps):
-        run()
+        t1 = time.perf_counter()
+        run()                                                       # returns after the solve
+        each.append(time.perf_counter() - t1)
     torch.cuda.synchronize()
     if world > 1:
         tdist.barrier()
@@ -657,6 +660,7 @@ def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl',
         dt = float(t.item())
     return {'workload': f'fte C=6 frames={n_frames} L=20 P={table.P} sd=const intermode=vel (configs[3])',
             'ranks': world, 'scaling': 'strong', 'frames_per_s': n_frames / dt, 'ms_per_solve': dt * 1e3,
+            'ms_per_solve_each_rank0': [round(e * 1e3, 3) for e in each],
             'status': rep['status_name'], 'iters': rep['iters'], 'cost_after': rep['cost_after'],
             'pos_rms_vs_truth_m': pos_rms, 'tau_err_max_s': float(np.abs(tau - seq.tau).max()),
             'exchange': 'none' if world == 1 else (f'torch.distributed {exchange}: one all-reduce per LM step '
