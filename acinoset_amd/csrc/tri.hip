@@ -45,22 +45,28 @@ __device__ void dlt_null4(double A[16], double out[4]) {
   double V[16];
   for (int i = 0; i < 16; ++i) V[i] = (i % 5 == 0) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 30; ++sweep) {
-    double off = 0.0;
+    // a pair is rotated while |gamma| / sqrt(alpha beta) >= 1e-15, tested squared (no square
+    // root or division); the sweeps stop when no pair was. Rotation by the short-latency
+    // reciprocal / reciprocal square root (fastmath.hpp, ~1 ulp)
+    bool any = false;
+#pragma unroll
     for (int p = 0; p < 3; ++p)
+#pragma unroll
       for (int q = p + 1; q < 4; ++q) {
         double alpha = 0.0, beta = 0.0, gamma = 0.0;
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
           alpha += A[i * 4 + p] * A[i * 4 + p];
           beta += A[i * 4 + q] * A[i * 4 + q];
           gamma += A[i * 4 + p] * A[i * 4 + q];
         }
         if (gamma == 0.0) continue;
-        const double rel = fabs(gamma) / sqrt(alpha * beta);
-        off = fmax(off, rel);
-        if (rel < 1e-15) continue;
-        const double zeta = (beta - alpha) / (2.0 * gamma);
-        const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-        const double cs = 1.0 / sqrt(1.0 + t * t), sn = cs * t;
+        if (gamma * gamma < 1e-30 * (alpha * beta)) continue;
+        any = true;
+        const double zeta = (beta - alpha) * rcp_nr(2.0 * gamma);
+        const double z2 = 1.0 + zeta * zeta;
+        const double t = (zeta >= 0 ? 1.0 : -1.0) * rcp_nr(fabs(zeta) + z2 * rsq_nr(z2));
+        const double cs = rsq_nr(1.0 + t * t), sn = cs * t;
         for (int i = 0; i < 4; ++i) {
           const double ap = A[i * 4 + p], aq = A[i * 4 + q];
           A[i * 4 + p] = cs * ap - sn * aq;
@@ -70,7 +76,7 @@ __device__ void dlt_null4(double A[16], double out[4]) {
           V[i * 4 + q] = sn * vp + cs * vq;
         }
       }
-    if (off < 1e-15) break;
+    if (!any) break;
   }
   int best = 0;
   double bn = 1e300;
