@@ -86,24 +86,14 @@ __device__ __forceinline__ double ekf_xq(const double* s, int q, int p, double e
   return v;
 }
 
-// Marker positions of all P+1 poses of the forward-difference Jacobian at once, every
-// thread of the workgroup on independent (pose, joint) / (pose, marker) items. Same
-// arithmetic as fk_frame (fk.hpp), so bit-identical positions: G_j = A_{n-1}..A_0 per
-// joint, M_j = G_root .. G_parent G_j by 3x3 products walking to the root, node = sum of
-// M_frame offsets walking to the root. A pose differs from pose 0 in one parameter, so
-// only one G per pose is recomputed (that of the parameter's joint, if a rotation).
-// Output: pos (P+1) x L x 3 in LDS (after the final barrier).
+// ekf_fk_batch's phase 0: sin / cos of every parameter as given (sc rows 0, 1) and as moved by
+// eps (rows 2, 3; FK_MAXP per row), and the root / world translation of every Jacobian pose
+// (rw: 6 per pose). The caller synchronises.
 template <bool F32>
-__device__ void ekf_fk_batch(const SkelView& sk, const double* ss, double eps, double* fk, int tid, int nth) {
-  const int P = sk.P, J = sk.J, L = sk.L, NQ = P + 1;
-  double* Gb = fk;                        // FK_MAXJ x 9: G of pose 0
-  double* Gq = Gb + FK_MAXJ * 9;          // (FK_MAXP + 1) x 9: G of the moved joint of pose q
-  double* M = Gq + (FK_MAXP + 1) * 9;     // NQ x J x 9
-  double* pos = M + (size_t)NQ * J * 9;   // NQ x L x 3
-  double* rw = pos + (size_t)NQ * L * 3;  // NQ x 6: root, world translation
-  double* sc = rw + (size_t)NQ * 6;       // sin, cos of pose 0; sin, cos of the moved parameter
+__device__ void ekf_fk_trig_trans(const SkelView& sk, const double* ss, double eps, double* sc, double* rw, int tid,
+                                  int nth) {
+  const int P = sk.P, NQ = P + 1;
   const int* pk = sk.pk;
-  // 0. trig of every parameter (as given and as moved), per-pose translations
   for (int e = tid; e < 2 * P + 2 * NQ; e += nth) {
     if (e < 2 * P) {
       const int p = e % P, mv = e / P;
@@ -136,6 +126,27 @@ __device__ void ekf_fk_batch(const SkelView& sk, const double* ss, double eps, d
       dst[2] = t[2];
     }
   }
+}
+
+// Marker positions of all P+1 poses of the forward-difference Jacobian at once, every
+// thread of the workgroup on independent (pose, joint) / (pose, marker) items. Same
+// arithmetic as fk_frame (fk.hpp), so bit-identical positions: G_j = A_{n-1}..A_0 per
+// joint, M_j = G_root .. G_parent G_j by 3x3 products walking to the root, node = sum of
+// M_frame offsets walking to the root. A pose differs from pose 0 in one parameter, so
+// only one G per pose is recomputed (that of the parameter's joint, if a rotation).
+// Output: pos (P+1) x L x 3 in LDS (after the final barrier).
+template <bool F32>
+__device__ void ekf_fk_batch(const SkelView& sk, const double* ss, double eps, double* fk, int tid, int nth) {
+  const int P = sk.P, J = sk.J, L = sk.L, NQ = P + 1;
+  double* Gb = fk;                        // FK_MAXJ x 9: G of pose 0
+  double* Gq = Gb + FK_MAXJ * 9;          // (FK_MAXP + 1) x 9: G of the moved joint of pose q
+  double* M = Gq + (FK_MAXP + 1) * 9;     // NQ x J x 9
+  double* pos = M + (size_t)NQ * J * 9;   // NQ x L x 3
+  double* rw = pos + (size_t)NQ * L * 3;  // NQ x 6: root, world translation
+  double* sc = rw + (size_t)NQ * 6;       // sin, cos of pose 0; sin, cos of the moved parameter
+  const int* pk = sk.pk;
+  // 0. trig of every parameter (as given and as moved), per-pose translations
+  ekf_fk_trig_trans<F32>(sk, ss, eps, sc, rw, tid, nth);
   __syncthreads();
   // 1. G of every joint at pose 0, and of the moved joint of each pose q > 0
   for (int e = tid; e < J + P; e += nth) {
@@ -224,37 +235,26 @@ __device__ void ekf_fk_batch(const SkelView& sk, const double* ss, double eps, d
   __syncthreads();
 }
 
-// Marker l's position at Jacobian pose q, from scratch in one thread: ekf_fk_batch's
-// arithmetic (the same G, M and node sums in the same order) without its shared tables and
-// barriers. For skeletons of one joint (the head model), where recomputing the joint's
-// rotation per (pose, marker) item is cheaper than the batch's four dependent workgroup
-// phases.
+// Marker l's position at Jacobian pose q in one thread, from ekf_fk_trig_trans's tables:
+// ekf_fk_batch's phases 1-3 (the same G, M and node sums in the same order, so the same
+// bits) without their shared tables and barriers. For skeletons of one joint (the head
+// model), where recomputing a joint's rotation per (pose, marker) item is cheaper than the
+// batch's three dependent workgroup phases.
 template <bool F32>
-__device__ void ekf_fk_point(const SkelView& sk, const double* ss, double eps, int q, int l, double* out) {
-  const int* pk = sk.pk;
+__device__ void ekf_fk_point(const SkelView& sk, const double* ss, double eps, const double* sc, const double* rw, int q,
+                             int l, double* out) {
+  const int moved = q - 1;  // the parameter moved in pose q (none for q = 0)
   auto G_of = [&](int j, double* G) {
     const int* jt = sk.joints + 8 * j;
     const int nrot = jt[1];
-    double sn[3] = {0.0, 0.0, 0.0}, cs[3] = {1.0, 1.0, 1.0};
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      if (r >= nrot) break;
-      const double v = ekf_xq<F32>(ss, q, jt[5 + r], eps);
-      if (F32) {
-        float sf, cf;
-        sincosf((float)v, &sf, &cf);
-        sn[r] = sf;
-        cs[r] = cf;
-      } else {
-        sincos(v, &sn[r], &cs[r]);
-      }
-    }
 #pragma unroll
     for (int col = 0; col < 3; ++col) {
       double v[3] = {col == 0 ? 1.0 : 0.0, col == 1 ? 1.0 : 0.0, col == 2 ? 1.0 : 0.0};
       for (int r = 0; r < nrot; ++r) {
         double w[3];
-        act_rot_vec(jt[2 + r], sn[r], cs[r], v, w);
+        const int p = jt[5 + r];
+        const int mv = p == moved ? 2 : 0;
+        act_rot_vec(jt[2 + r], sc[mv * FK_MAXP + p], sc[(mv + 1) * FK_MAXP + p], v, w);
         v[0] = w[0];
         v[1] = w[1];
         v[2] = w[2];
@@ -270,16 +270,7 @@ __device__ void ekf_fk_point(const SkelView& sk, const double* ss, double eps, i
     const int* nd = sk.nodes + 4 * node;
     const int base = nd[0];
     if (base == -2 || base == -1) {  // the root (or world) translation of pose q
-      const int kind = base == -2 ? PK_WORLD : PK_TRANS;
-      double t[3] = {0.0, 0.0, 0.0};
-      for (int p = 0; p < sk.P; ++p)
-        if (pk[4 * p] == kind) {
-          const int a = pk[4 * p + 1];
-          const double x = ekf_xq<F32>(ss, q, p, eps);
-          t[0] += a == 0 ? x : 0.0;
-          t[1] += a == 1 ? x : 0.0;
-          t[2] += a == 2 ? x : 0.0;
-        }
+      const double* t = rw + q * 6 + (base == -2 ? 3 : 0);
       p0 += t[0];
       p1 += t[1];
       p2 += t[2];
@@ -1017,13 +1008,17 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
         for (int k = 0; k < 6; ++k) hp[m + 6 * o + k] = po.J[k];
       }
     } else if (sk.J == 1) {
-      // one joint: every (pose, observation) item computes its marker from scratch and
-      // projects it, no workgroup phase in between
+      // one joint: the trig and translation tables of every Jacobian pose, then every (pose,
+      // observation) item computes its marker from them and projects it
+      double* sc = fkb;                      // 4 x FK_MAXP
+      double* rw = sc + 4 * FK_MAXP;         // (P+1) x 6
+      ekf_fk_trig_trans<F32>(sk, ss, d.eps, sc, rw, tid, nth);
+      __syncthreads();
       for (int e = tid; e < (P + 1) * CL; e += nth) {
         const int q = e / CL, o = e - q * CL;
         const int c = o / d.L, l = o - c * d.L;
         double x[3];
-        ekf_fk_point<F32>(sk, ss, d.eps, q, l, x);
+        ekf_fk_point<F32>(sk, ss, d.eps, sc, rw, q, l, x);
         ProjOut po;
         fisheye_project<false>(sCam + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
         hp[(size_t)q * m + 2 * o] = po.u;
