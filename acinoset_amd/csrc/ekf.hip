@@ -604,8 +604,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
         const int r = e / Pp, q = e - r * Pp;
         double hq = 0.0;
         if (r < m && q < P) hq = (hpose[(size_t)(q + 1) * m + r] - hpose[r]) / d.eps;
-        H[e] = hq;
-        HW[e] = wr[r] * hq;
+        H[e] = hq;  // W H is formed as the MFMA operand is loaded
       }
     }
     __syncthreads();
@@ -643,10 +642,14 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
           for (int u = 0; u < UB; ++u) {
             const int k = 4 * (s0 + u * KS) + lk;
             const bool ok = s0 + u * KS < nks;
+            const double wk = (!AH && ok) ? wr[k] : 0.0;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-              av[u][h] = (ok && h < NTt) ? opW[(size_t)k * ldo + 16 * h + li] : 0.0;
               bv[u][h] = (ok && h < NTt) ? opH[(size_t)k * ldo + 16 * h + li] : 0.0;
+              if constexpr (AH)
+                av[u][h] = (ok && h < NTt) ? opW[(size_t)k * ldo + 16 * h + li] : 0.0;
+              else
+                av[u][h] = wk * bv[u][h];  // (W H)[k][q], the product the scratch copy held
             }
             rv[u] = (ok && li == 0) ? opr[k] : 0.0;
           }
