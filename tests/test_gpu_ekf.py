@@ -226,3 +226,35 @@ def test_ekf_parallel_gains_match_sequential_smoother(ctx, mode, N):
     np.testing.assert_array_equal(a['x_est'], b['x_est'])
     sc = max(1.0, float(np.abs(b['x_smooth']).max()))
     np.testing.assert_allclose(a['x_smooth'], b['x_smooth'], atol=1e-9 * sc, rtol=0)
+
+
+def test_ekf_head_8wave_kernel_matches_small_state_kernel(ctx, tmp_path):
+    """The 8-wave filter (k_ekf_filter) on the head model - the path a head model takes when
+    the small-state kernel's LDS does not fit (many cameras) - against the small-state
+    kernel (k_ekf_filter_w1) on the same 12-camera sequence, float64 numerics: the same
+    algebra in another summation order. The 8-wave kernel is forced by ACS_EKF_WG=1, read
+    once per process, so it runs in a child process (one GPU process at a time)."""
+    import os
+    import subprocess
+    import sys
+    scene, seq, s0, cp, covs = _setup_ring('head', 40)
+    a = cekf.run(seq.uv, seq.likelihood, cp, 'head', 90.0, s0, ref_numerics=False, cal_covs=covs, ctx=ctx)
+    np.savez(tmp_path / 'in.npz', uv=seq.uv, lik=seq.likelihood, s0=s0)
+    code = f"""
+import importlib, sys, numpy as np
+sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})
+sys.path.insert(0, {os.path.dirname(os.path.abspath(__file__))!r})
+from test_gpu_ekf import _setup_ring
+cekf = importlib.import_module('acinoset_amd.core.ekf')
+d = np.load({str(tmp_path / 'in.npz')!r})
+scene, seq, s0, cp, covs = _setup_ring('head', 40)
+b = cekf.run(d['uv'], d['lik'], cp, 'head', 90.0, d['s0'], ref_numerics=False, cal_covs=covs)
+np.savez({str(tmp_path / 'out.npz')!r}, x_est=b['x_est'], x_smooth=b['x_smooth'], outliers=b['outliers'])
+"""
+    env = dict(os.environ, ACS_EKF_WG='1')
+    r = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    b = np.load(tmp_path / 'out.npz')
+    P = 6
+    _check(a, P, b['x_est'][:, :P], b['x_est'][:, P:2 * P], b['x_est'][:, 2 * P:], b['x_smooth'][:, :P])
+    assert abs(int(a['outliers']) - int(b['outliers'])) <= 1
