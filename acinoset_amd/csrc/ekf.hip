@@ -70,11 +70,17 @@ __host__ __device__ inline size_t ekf_wg_la_doubles(int npad, int Ppad) {
   return (size_t)ekf_wg_px_rows(npad, Ppad) * (Ppad + 1) + (size_t)Ppad * (Ppad + npad + 1) +
          (size_t)Ppad * (Ppad + 1);
 }
+// the forward-difference A / b phase streams H through LDS in chunks of EKF_FD_RCH rows: the
+// KS = 4 partial-tile tree buffer, then the chunk (stride Ppad + 1) and its weights / residuals
+#define EKF_FD_RCH 128
+__host__ __device__ inline size_t ekf_fd_chunk_doubles(int Ppad) {
+  return 2 * 5 * 256 + (size_t)EKF_FD_RCH * (Ppad + 1) + 2 * EKF_FD_RCH;
+}
 // the 8-wave filter's measurement-model region: batched FK (forward differences) or the
 // analytic H's FK and marker-space operands, whichever is larger
 __host__ __device__ inline size_t ekf_wg_fk_doubles(int P, int J, int L, int Ppad) {
-  const size_t a = ekf_w1_fk_doubles(P, J, L), b = ekf_ah_alg_doubles(L, Ppad);
-  return a > b ? a : b;
+  const size_t a = ekf_w1_fk_doubles(P, J, L), b = ekf_ah_alg_doubles(L, Ppad), c = ekf_fd_chunk_doubles(Ppad);
+  return a > b ? (a > c ? a : c) : (b > c ? b : c);
 }
 
 // Parameter p of Jacobian pose q (q = 0: the predicted state; q > 0: parameter q-1 moved by
@@ -599,14 +605,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       opr = sg;
       nks = R3 >> 2;
       ldo = LD;
-    } else {
-      for (int e = tid; e < mp * Pp; e += nth) {
-        const int r = e / Pp, q = e - r * Pp;
-        double hq = 0.0;
-        if (r < m && q < P) hq = (hpose[(size_t)(q + 1) * m + r] - hpose[r]) / d.eps;
-        H[e] = hq;  // W H is formed as the MFMA operand is loaded
-      }
-    }
+    }  // forward differences: H is formed chunk by chunk in LDS in the products below
     __syncthreads();
     EKF_TICK(3);
     // ---- 3. information-form update -------------------------------------------------
@@ -618,7 +617,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       const int li = lane & 15, lk = lane >> 4;
       const int NTt = Pp >> 4, nAt = NTt * (NTt + 1) / 2, nt = nAt + NTt;
       const size_t avail = (size_t)d.npad * Pp + (size_t)Pp * AW;
-      int KS = EKF_WAVES;
+      int KS = AH ? EKF_WAVES : 4;  // forward differences: waves 4-7 count the outliers
       while (KS > 1 && (size_t)(KS / 2) * nt * 256 > avail) KS >>= 1;
       double* red = sPx;
       constexpr int NTMAX = 5;  // 3 upper A tiles + 2 b tiles at Ppad = 32
@@ -634,7 +633,91 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
           j0 = -1;
         }
       };
-      if (wave < KS) {
+      unsigned long long cnt_fd = 0;
+      if constexpr (!AH) {
+        // Forward differences: H (:81-96) in chunks of EKF_FD_RCH rows, formed from the pixel
+        // table into LDS with their weights and residuals (one global round trip per chunk);
+        // waves 0-3 add the chunk's k-steps to A and b on MFMA while waves 4-7 run the 3-sigma
+        // test of its rows (diag S = rows of H_x P_xx . H_x, + R, row tiles on MFMA)
+        const int LDc = Pp + 1;
+        double* sHc = sPx + 2 * 5 * 256;  // after the KS = 4 tree buffer
+        double* sWc = sHc + (size_t)EKF_FD_RCH * LDc;
+        double* sRc = sWc + EKF_FD_RCH;
+        for (int r0 = 0; r0 < mp; r0 += EKF_FD_RCH) {
+          const int rows = min(EKF_FD_RCH, mp - r0);  // a multiple of 16
+          for (int e = tid; e < rows * Pp; e += nth) {  // rows fastest: coalesced pixel loads
+            const int q = e / rows, rr = e - q * rows, r = r0 + rr;
+            double hq = 0.0;
+            if (r < m && q < P) hq = (hpose[(size_t)(q + 1) * m + r] - hpose[r]) / d.eps;
+            sHc[rr * LDc + q] = hq;
+          }
+          for (int rr = tid; rr < rows; rr += nth) {
+            sWc[rr] = wr[r0 + rr];
+            sRc[rr] = res[r0 + rr];
+          }
+          __syncthreads();
+          if (wave < KS) {
+            for (int st = wave; st < (rows >> 2); st += KS) {
+              const int kl = 4 * st + lk;
+              const double wk = sWc[kl];
+              double av[2], bv[2];
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                bv[h] = h < NTt ? sHc[kl * LDc + 16 * h + li] : 0.0;
+                av[h] = wk * bv[h];  // (W H)[k][q]
+              }
+              const double rv = li == 0 ? sRc[kl] : 0.0;
+#pragma unroll
+              for (int t = 0; t < NTMAX; ++t) {
+                if (t >= nt) break;
+                int i0, j0;
+                tile_ij(t, i0, j0);
+                const double aop = i0 ? av[1] : av[0];
+                const double bop = j0 < 0 ? rv : (j0 ? bv[1] : bv[0]);
+                acc[t] = mfma64(aop, bop, acc[t]);
+              }
+            }
+          } else {
+            for (int rt = wave - KS; rt < (rows >> 4); rt += EKF_WAVES - KS) {
+              const int i0 = rt << 4;
+              double ha[8];
+#pragma unroll
+              for (int s8 = 0; s8 < 8; ++s8) ha[s8] = (4 * s8 < Pp) ? sHc[(i0 + li) * LDc + 4 * s8 + lk] : 0.0;
+              double hr[2][4];
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) hr[h][q] = h < NTt ? sHc[(i0 + lk + 4 * q) * LDc + 16 * h + li] : 0.0;
+              double dq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                if (h >= NTt) break;
+                dbl4 g = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int s8 = 0; s8 < 8; ++s8)
+                  if (4 * s8 < Pp) g = mfma64(ha[s8], sP[(4 * s8 + lk) * LDP + 16 * h + li], g);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) dq[q] += g[q] * hr[h][q];
+              }
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                dq[q] = group_sum<16>(dq[q]);
+                const int rl = i0 + lk + 4 * q, r = r0 + rl;
+                bool outl = false;
+                if (li == 0 && r < m) {
+                  const double Srr = dq[q] + 1.0 / sWc[rl];
+                  outl = fabs(sRc[rl]) > 3.0 * sqrt(Srr);
+                }
+                // rows 2 pt (lk even) and 2 pt + 1 (lane + 16)
+                const int other = __shfl_xor((int)outl, 16);
+                if (li == 0 && !(lk & 1) && r < m && (outl || other)) ++cnt_fd;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      if (AH && wave < KS) {
         constexpr int UB = 2;  // k-steps per batch of loads
         for (int s0 = wave; s0 < nks; s0 += UB * KS) {
           double av[UB][2], bv[UB][2], rv[UB];
@@ -705,42 +788,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       // 3-sigma outlier count (:259-264): diag S = rows of H_x P_xx . H_x, + R. Row tiles of
       // H P_xx on MFMA (operands loaded first), each row's dot with its own H row summed
       // across the 16 column lanes (DPP) and the column tiles
-      unsigned long long cnt = 0;
-      for (int rt = wave; rt < (AH ? 0 : (mp >> 4)); rt += EKF_WAVES) {
-        const int i0 = rt << 4;
-        double ha[8];
-#pragma unroll
-        for (int s = 0; s < 8; ++s) ha[s] = (4 * s < Pp) ? H[(size_t)(i0 + li) * Pp + 4 * s + lk] : 0.0;
-        double hr[2][4];
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) hr[h][q] = h < NTt ? H[(size_t)(i0 + lk + 4 * q) * Pp + 16 * h + li] : 0.0;
-        double dq[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          if (h >= NTt) break;
-          dbl4 g = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int s = 0; s < 8; ++s)
-            if (4 * s < Pp) g = mfma64(ha[s], sP[(4 * s + lk) * LDP + 16 * h + li], g);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) dq[q] += g[q] * hr[h][q];
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          dq[q] = group_sum<16>(dq[q]);
-          const int r = i0 + lk + 4 * q;
-          bool outl = false;
-          if (li == 0 && r < m) {
-            const double Srr = dq[q] + 1.0 / wr[r];
-            outl = fabs(res[r]) > 3.0 * sqrt(Srr);
-          }
-          // rows 2 pt (lk even) and 2 pt + 1 (lane + 16)
-          const int other = __shfl_xor((int)outl, 16);
-          if (li == 0 && !(lk & 1) && r < m && (outl || other)) ++cnt;
-        }
-      }
+      unsigned long long cnt = cnt_fd;  // forward differences: counted in the chunks above
       if (cnt) atomicAdd(&s_out, cnt);
       __syncthreads();
     }
