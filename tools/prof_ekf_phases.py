@@ -2,14 +2,15 @@
 libprof.so as tools/prof_fte_phases.py, with ekf.hip compiled with -DEKF_PROFILE):
 python tools/prof_ekf_phases.py [mode] [n_cams] [frames] [fd|analytic]   (default: default 6 200 fd;
 'fd' = the reference numerics with the forward-difference H, 'analytic' = the analytic H in float64).
-Build: tools/build_prof.sh ekf."""
+Build: tools/build_prof.sh ekf (rebuild after every ekf.hip change; ACS_PROF_LIB=<path> picks another
+profiling build)."""
 import ctypes as C
 import importlib
 import os
 import sys
 
-os.environ['ACINOSET_HIP_LIB'] = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'acinoset_amd',
-                                              'csrc', 'build', 'libprof.so')
+os.environ['ACINOSET_HIP_LIB'] = os.environ.get('ACS_PROF_LIB') or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), '..', 'acinoset_amd', 'csrc', 'build', 'libprof.so')
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
