@@ -699,19 +699,21 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
 #pragma unroll
                 for (int q = 0; q < 4; ++q) dq[q] += g[q] * hr[h][q];
               }
+              // the 16-lane sums are all-reduced (every lane holds them, bit-identical); lane
+              // li = q < 4 tests row i0 + lk + 4 q, so the 4 rows' divisions and square roots
+              // run side by side instead of one after another
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                dq[q] = group_sum<16>(dq[q]);
-                const int rl = i0 + lk + 4 * q, r = r0 + rl;
-                bool outl = false;
-                if (li == 0 && r < m) {
-                  const double Srr = dq[q] + 1.0 / sWc[rl];
-                  outl = fabs(sRc[rl]) > 3.0 * sqrt(Srr);
-                }
-                // rows 2 pt (lk even) and 2 pt + 1 (lane + 16)
-                const int other = __shfl_xor((int)outl, 16);
-                if (li == 0 && !(lk & 1) && r < m && (outl || other)) ++cnt_fd;
+              for (int q = 0; q < 4; ++q) dq[q] = group_sum<16>(dq[q]);
+              const double dsel = li == 1 ? dq[1] : li == 2 ? dq[2] : li == 3 ? dq[3] : dq[0];
+              const int rl = i0 + lk + 4 * (li & 3), r = r0 + rl;
+              bool outl = false;
+              if (li < 4 && r < m) {
+                const double Srr = dsel + 1.0 / sWc[rl];
+                outl = fabs(sRc[rl]) > 3.0 * sqrt(Srr);
               }
+              // rows 2 pt (lk even) and 2 pt + 1 (lane + 16)
+              const int other = __shfl_xor((int)outl, 16);
+              if (li < 4 && !(lk & 1) && r < m && (outl || other)) ++cnt_fd;
             }
           }
           __syncthreads();
