@@ -112,6 +112,7 @@ struct EkfIo {
                *P0 = nullptr, *s0 = nullptr;
   double *x_pred = nullptr, *x_est = nullptr, *x_smooth = nullptr, *P_est = nullptr, *P_smooth = nullptr;
   long long* outliers = nullptr;  // set by acs_ekf_enqueue (device, one per sequence)
+  int* bad = nullptr;             // set by acs_ekf_enqueue (device): singular update / gain solves
 };
 int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n_cams, int n_seq, int n_frames,
                     double fps, double thresh, double max_pixel_err, double eps, int ref_numerics, EkfIo& io);

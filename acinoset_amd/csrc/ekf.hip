@@ -323,6 +323,105 @@ struct Walk2 {
   }
 };
 
+// k_ekf_filter's update solve for a W that is not positive definite: [I + A C | I] (A and C
+// zero outside P x P), then Gauss-Jordan with partial pivoting, register-resident like the
+// diagonal solve; pivoting is implicit (rows stay in place, a row is "used" once it has been a
+// pivot): step k takes the unused row with the largest |a[r][k]| (ties: lowest row), and at
+// the end row pv_k over its pivot is row k of V, written to sC. Called by every thread (not
+// inlined: the common path keeps its registers).
+__device__ __noinline__ void ekf_update_pivoted(double* aug, int AW, const double* sA, double* sC, int LPx,
+                                                double* colb, int P, int Pp, int* s_sing) {
+  constexpr int NCG = 4;
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int gr = tid & 31, cg = tid >> 5, half = cg & 1;
+  double av[NCG];
+  // [I + A C | I] (A and C are zero outside P x P), then Gauss-Jordan with partial
+  // pivoting, register-resident as above; pivoting is implicit (rows stay in place, a
+  // row is "used" once it has been a pivot): step k takes the unused row with the
+  // largest |a[r][k]| (ties: lowest row), and at the end row pv_k over its pivot is row k
+  // of V
+  for (int e = tid; e < Pp * Pp; e += nth) {
+    const int r = e / Pp, c = e - r * Pp;
+    aug[r * AW + c] = r == c ? 1.0 : 0.0;
+    aug[r * AW + Pp + c] = r == c ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  wg_mgemm<false, false>(aug, AW, sA, LPx, sC, LPx, Pp, Pp, Pp, 1.0, 1.0);  // I + A C
+#pragma unroll
+  for (int j = 0; j < NCG; ++j) {
+    const int c = cg + 16 * j;
+    av[j] = (c < 2 * Pp && gr < Pp) ? aug[gr * AW + c] : 0.0;
+  }
+  int* pvb = reinterpret_cast<int*>(colb + 64);  // 2 ints
+  bool used = gr >= P;
+  int myk = -1;
+  double myp = 1.0;
+  int nsing = 0;
+  for (int k = 0; k < P; ++k) {
+    const int buf = k & 1;
+    if (cg == (k & 15)) {
+      const double colv = (k >> 4) ? av[1] : av[0];
+      // arg max over the 32 lanes: DPP inside each 16-lane row, then the row pair
+      double best = used ? -1.0 : fabs(colv);
+      int bi = gr;
+      auto take = [&](double ob, int oi) {
+        const bool t = (ob > best) | ((ob == best) & (oi < bi));
+        best = t ? ob : best;
+        bi = t ? oi : bi;
+      };
+      take(dpp_f64<0xB1>(best), __builtin_amdgcn_mov_dpp(bi, 0xB1, 0xF, 0xF, false));
+      take(dpp_f64<0x4E>(best), __builtin_amdgcn_mov_dpp(bi, 0x4E, 0xF, 0xF, false));
+      take(dpp_f64<0x141>(best), __builtin_amdgcn_mov_dpp(bi, 0x141, 0xF, 0xF, false));
+      take(dpp_f64<0x140>(best), __builtin_amdgcn_mov_dpp(bi, 0x140, 0xF, 0xF, false));
+      {
+        const auto bh = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(best),
+                                                         (unsigned)__double2hiint(best), false, false);
+        const auto bl = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(best),
+                                                         (unsigned)__double2loint(best), false, false);
+        const auto bx = __builtin_amdgcn_permlane16_swap((unsigned)bi, (unsigned)bi, false, false);
+        const double b0 = __hiloint2double((int)bh[0], (int)bl[0]), b1 = __hiloint2double((int)bh[1], (int)bl[1]);
+        best = b0;
+        bi = (int)bx[0];
+        take(b1, (int)bx[1]);
+      }
+      const double p = read_lane_f64(colv, bi + 32 * half);
+      colb[buf * 32 + gr] = gr == bi ? p : colv * (1.0 / p);
+      if (gr == 0) pvb[buf] = bi;
+    }
+    __syncthreads();
+    const int pv = pvb[buf];
+    const double f = colb[buf * 32 + gr];
+    const bool piv = gr == pv;
+    if (piv) {
+      used = true;
+      myk = k;
+      myp = f;
+      nsing += f == 0.0 ? 1 : 0;
+    }
+    const bool upd = !piv && gr < P;
+    const int src = (pv + 32 * half) << 2;  // the pivot row's lane of this half-wave
+    double prow[NCG];
+#pragma unroll
+    for (int j = 0; j < NCG; ++j)
+      prow[j] = __hiloint2double(__builtin_amdgcn_ds_bpermute(src, __double2hiint(av[j])),
+                                 __builtin_amdgcn_ds_bpermute(src, __double2loint(av[j])));
+#pragma unroll
+    for (int j = 0; j < NCG; ++j) {
+      const double nv = fma(-f, prow[j], av[j]);
+      av[j] = (upd && (cg + 16 * j > k)) ? nv : av[j];
+    }
+  }
+  if (myk >= 0) {  // sC was last read by the product above
+    const double ip = 1.0 / myp;
+#pragma unroll
+    for (int j = 0; j < NCG; ++j) {
+      const int c = cg + 16 * j;
+      if (c >= Pp && c < Pp + P) sC[myk * LPx + c - Pp] = av[j] * ip;
+    }
+  }
+  if (nsing && cg == 0) atomicAdd(s_sing, nsing);  // singular I + A C (counted, not hidden)
+}
+
 template <bool F32, bool AH>
 __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __restrict__ I,
                                                     const double* __restrict__ Rl, const double* __restrict__ cams,
@@ -332,7 +431,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
                                                     double* __restrict__ xpred, double* __restrict__ xest,
                                                     double* __restrict__ Ppred, double* __restrict__ Pest,
                                                     double* __restrict__ scratch, long long* __restrict__ outliers,
-                                                    unsigned long long* ekf_prof) {
+                                                    int* __restrict__ bad, unsigned long long* ekf_prof) {
   const int seq = blockIdx.x;
   const int tid = threadIdx.x, nth = blockDim.x, lane = tid & 63, wave = tid >> 6;
   const int n = d.n, P = d.P, m = d.m, LDP = d.npad + 1, Pp = d.Ppad;
@@ -369,6 +468,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   } while (0)
 #endif
   __shared__ unsigned long long s_out;
+  __shared__ int s_piv, s_sing;  // pivoted update solve from now on (sticky); singular solves
   for (int e = tid; e < d.n_ints; e += nth) sI[e] = I[e];  // the FK walks the table: keep it in LDS
   for (int e = tid; e < d.n_reals; e += nth) sRl[e] = Rl[e];
   for (int e = tid; e < d.C * ACS_CAM_STRIDE; e += nth) sCam[e] = cams[e];
@@ -389,7 +489,11 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
     sP[e] = (r < n && c < n) ? P0[r * n + c] : 0.0;
   }
   for (int r = tid; r < d.npad; r += nth) ss[r] = r < n ? s0[(size_t)seq * n + r] : 0.0;
-  if (tid == 0) s_out = 0;
+  if (tid == 0) {
+    s_out = 0;
+    s_piv = 0;
+    s_sing = 0;
+  }
   __syncthreads();
 
   for (int i = 0; i < d.N; ++i) {
@@ -795,10 +899,15 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       __syncthreads();
     }
     EKF_TICK(4);
-    // The update needs (I + A C)^-1 [A P[x, :] | b], C = P_xx. With W = C + C A C = C (I + A C),
-    // symmetric positive definite, (I + A C)^-1 = W^-1 C: a Gauss-Jordan on [W | C] with the
-    // pivots on the diagonal (no pivot search; the pivot row of step k is row k) gives
-    // V = (I + A C)^-1, then Z_G = (V A) P[x, :] and Z_b = V b on MFMA / per thread.
+    // The update needs (I + A C)^-1 [A P[x, :] | b], C = P_xx. With W = C + C A C = C (I + A C)
+    // (symmetric), (I + A C)^-1 = W^-1 C: a Gauss-Jordan on [W | C] with the pivots on the
+    // diagonal (no pivot search; the pivot row of step k is row k) gives V = (I + A C)^-1, then
+    // Z_G = (V A) P[x, :] and Z_b = V b on MFMA / per thread.
+    // W is positive definite exactly when C is (A is PSD), and then diagonal pivots are stable.
+    // The reference's default P0 is not (src/core/ekf.py:155, neck length -0.28), so every
+    // pivot is checked: all positive certifies W > 0 (Sylvester); the first that is not ends
+    // the diagonal solve, and V comes from a partially pivoted Gauss-Jordan on [I + A C | I]
+    // instead, for this frame and (sticky, s_piv) every later frame of the sequence.
     // Scratch: C, then V, in sPx's first Ppad x LPx; A C, then V A, in the next; [W | C] in
     // aug's first 2 Ppad columns (P[:, x] is copied into sPx once they are consumed).
     double* sC = sPx;
@@ -824,44 +933,56 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
       constexpr int NCG = 4;  // 2 Ppad <= 64 columns
       const int gr = tid & 31, cg = tid >> 5, half = cg & 1;
       double av[NCG];
-#pragma unroll
-      for (int j = 0; j < NCG; ++j) {
-        const int c = cg + 16 * j;
-        av[j] = (c < 2 * Pp && gr < Pp) ? aug[gr * AW + c] : 0.0;
-      }
       double* colb = sAC;                           // 2 x 32 doubles (A C is consumed)
-      double myp = 1.0;
-      __syncthreads();  // sAC free
-      for (int k = 0; k < P; ++k) {
-        const int buf = k & 1;
-        if (cg == (k & 15)) {
-          const double colv = (k >> 4) ? av[1] : av[0];  // k < P <= FK_MAXP = 32 (checked on entry)
-          const double p = read_lane_f64(colv, k + 32 * half);
-          colb[buf * 32 + gr] = gr == k ? p : colv * rcp_nr(p);  // one reciprocal (rcp + Newton), uniform
-        }
-        __syncthreads();
-        const double f = colb[buf * 32 + gr];
-        if (gr == k) myp = f;
-        const bool upd = gr != k && gr < P;
-        const int src = (k + 32 * half) << 2;  // row k's lane of this half-wave
-        double prow[NCG];
-#pragma unroll
-        for (int j = 0; j < NCG; ++j)
-          prow[j] = __hiloint2double(__builtin_amdgcn_ds_bpermute(src, __double2hiint(av[j])),
-                                     __builtin_amdgcn_ds_bpermute(src, __double2loint(av[j])));
-#pragma unroll
-        for (int j = 0; j < NCG; ++j) {
-          const double nv = fma(-f, prow[j], av[j]);
-          av[j] = (upd && (cg + 16 * j > k)) ? nv : av[j];
-        }
-      }
-      if (gr < P) {  // V rows into sC (every thread read sC into aug above)
-        const double ip = rcp_nr(myp);
+      bool diag = s_piv == 0;                       // uniform
+      if (diag) {
 #pragma unroll
         for (int j = 0; j < NCG; ++j) {
           const int c = cg + 16 * j;
-          if (c >= Pp && c < Pp + P) sC[gr * LPx + c - Pp] = av[j] * ip;
+          av[j] = (c < 2 * Pp && gr < Pp) ? aug[gr * AW + c] : 0.0;
         }
+        double myp = 1.0;
+        __syncthreads();  // sAC free
+        for (int k = 0; k < P; ++k) {
+          const int buf = k & 1;
+          if (cg == (k & 15)) {
+            const double colv = (k >> 4) ? av[1] : av[0];  // k < P <= FK_MAXP = 32 (checked on entry)
+            const double p = read_lane_f64(colv, k + 32 * half);
+            colb[buf * 32 + gr] = gr == k ? p : colv * rcp_nr(p);  // one reciprocal (rcp + Newton), uniform
+          }
+          __syncthreads();
+          const double f = colb[buf * 32 + gr];
+          if (!(colb[buf * 32 + k] > 0.0)) {  // W not positive definite: the pivoted solve below
+            diag = false;
+            break;
+          }
+          if (gr == k) myp = f;
+          const bool upd = gr != k && gr < P;
+          const int src = (k + 32 * half) << 2;  // row k's lane of this half-wave
+          double prow[NCG];
+#pragma unroll
+          for (int j = 0; j < NCG; ++j)
+            prow[j] = __hiloint2double(__builtin_amdgcn_ds_bpermute(src, __double2hiint(av[j])),
+                                       __builtin_amdgcn_ds_bpermute(src, __double2loint(av[j])));
+#pragma unroll
+          for (int j = 0; j < NCG; ++j) {
+            const double nv = fma(-f, prow[j], av[j]);
+            av[j] = (upd && (cg + 16 * j > k)) ? nv : av[j];
+          }
+        }
+        if (diag && gr < P) {  // V rows into sC (every thread read sC into aug above)
+          const double ip = rcp_nr(myp);
+#pragma unroll
+          for (int j = 0; j < NCG; ++j) {
+            const int c = cg + 16 * j;
+            if (c >= Pp && c < Pp + P) sC[gr * LPx + c - Pp] = av[j] * ip;
+          }
+        }
+      }
+      if (!diag) {
+        __syncthreads();  // every thread past the diagonal solve's LDS reads
+        if (tid == 0) s_piv = 1;
+        ekf_update_pivoted(aug, AW, sA, sC, LPx, colb, P, Pp, &s_sing);
       }
       __syncthreads();
     }
@@ -898,7 +1019,10 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
   if (tid == 0 && ekf_prof)
     for (int k = 0; k < 8; ++k) ekf_prof[seq * 8 + k] = s_prof[k];
 #endif
-  if (tid == 0) outliers[seq] = (long long)s_out;
+  if (tid == 0) {
+    outliers[seq] = (long long)s_out;
+    if (s_sing) atomicAdd(bad, s_sing);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -930,6 +1054,80 @@ __host__ __device__ inline size_t ekf_w1_lds(const EkfDims& d) {
          ekf_w1_fk_doubles(d.P, d.J, d.L) + (size_t)d.C * ACS_CAM_STRIDE + d.n_reals + (d.n_ints + 1) / 2 + 1;
 }
 
+// k_ekf_filter_w1's update solve for a W that is not positive definite: column c of
+// [I + A C | I] on lane c of wave 0, Gauss-Jordan with partial pivoting in its registers (the
+// pivot column's lane finds the pivot row in its own registers: largest |a|, lowest row on
+// ties); row pv_k over its pivot ends as row k of V (not inlined: the common path keeps its
+// registers).
+template <int P>
+__device__ __noinline__ void ekf_w1_pivoted(const double* sA, const double* sP, int LDP, double* sV, int tid,
+                                            int* __restrict__ bad) {
+  double a[P];
+  const int c = tid;
+  if (c < P) {  // column c of I + A C
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      double v = r == c ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < P; ++k) v = fma(sA[r * P + k], sP[k * LDP + c], v);
+      a[r] = v;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < P; ++r) a[r] = r == c - P ? 1.0 : 0.0;
+  }
+  // the pivot column's lane finds the pivot row in its own registers (largest |a|,
+  // lowest row on ties); row pv_k over its pivot ends as row k of V
+  unsigned used = 0;
+  int pvk[P];
+  double pk[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    double best = -1.0;
+    int bi = 0;
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      const bool cand = !((used >> r) & 1u) && fabs(a[r]) > best;
+      best = cand ? fabs(a[r]) : best;
+      bi = cand ? r : bi;
+    }
+    const int pv = __builtin_amdgcn_readlane(bi, k);
+    double colv[P];
+#pragma unroll
+    for (int r = 0; r < P; ++r) colv[r] = read_lane_f64(a[r], k);
+    double pp = 0.0, prow = 0.0;
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      pp = r == pv ? colv[r] : pp;
+      prow = r == pv ? a[r] : prow;
+    }
+    const double ip = 1.0 / pp;
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      const double nv = fma(-(colv[r] * ip), prow, a[r]);
+      a[r] = (r != pv && tid > k) ? nv : a[r];
+    }
+    used |= 1u << pv;
+    pvk[k] = pv;
+    pk[k] = pp;
+  }
+  if (tid >= P && tid < 2 * P) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      double v = 0.0;
+#pragma unroll
+      for (int r = 0; r < P; ++r) v = r == pvk[k] ? a[r] : v;
+      sV[k * P + tid - P] = v / pk[k];
+    }
+  }
+  if (tid == 0) {
+    int ns = 0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) ns += pk[k] == 0.0 ? 1 : 0;
+    if (ns) atomicAdd(bad, ns);  // singular I + A C (counted, not hidden)
+  }
+}
+
 template <bool F32, bool AH, int PM, int NW>
 __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int* __restrict__ I,
                                                       const double* __restrict__ Rl, const double* __restrict__ cams,
@@ -938,7 +1136,7 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
                                                       const double* __restrict__ P0, const double* __restrict__ s0,
                                                       double* __restrict__ xpred, double* __restrict__ xest,
                                                       double* __restrict__ Ppred, double* __restrict__ Pest,
-                                                      long long* __restrict__ outliers,
+                                                      long long* __restrict__ outliers, int* __restrict__ bad,
                                                       unsigned long long* ekf_prof) {
   constexpr int P = PM, n = 3 * PM, LDP = n + 1, NZ1 = n + 1;
   static_assert(n + 1 <= 64 && 2 * P <= 64, "one column per lane");
@@ -1253,11 +1451,17 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
     EKF_TICK1(5);
     // ---- 5. Gauss-Jordan without pivot search, in wave 0's registers -----------------
     // step k: row k over its pivot, then a[r][k] times it off every other row (the
-    // column-k entries by readlane); at the end the right-hand block is V = (I + A C)^-1
+    // column-k entries by readlane); at the end the right-hand block is V = (I + A C)^-1.
+    // Every pivot positive certifies W > 0 (Sylvester), where diagonal pivots are stable; a
+    // P0 that is not positive definite makes W indefinite, and then V comes from a partially
+    // pivoted Gauss-Jordan on [I + A C | I] in the same registers.
     if (tid < 64) {
+      bool spd = true;  // uniform (the pivots come by readlane)
 #pragma unroll
       for (int k = 0; k < P; ++k) {
-        const double ip = rcp_nr(read_lane_f64(a[k], k));
+        const double p = read_lane_f64(a[k], k);
+        spd = spd && p > 0.0;
+        const double ip = rcp_nr(p);
         const double pr = tid > k ? a[k] * ip : a[k];
         a[k] = pr;
 #pragma unroll
@@ -1267,9 +1471,13 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
           a[r] = tid > k ? nv : a[r];
         }
       }
-      if (tid >= P && tid < 2 * P) {
+      if (spd) {
+        if (tid >= P && tid < 2 * P) {
 #pragma unroll
-        for (int k = 0; k < P; ++k) sV[k * P + tid - P] = a[k];
+          for (int k = 0; k < P; ++k) sV[k * P + tid - P] = a[k];
+        }
+      } else {
+        ekf_w1_pivoted<P>(sA, sP, LDP, sV, tid, bad);
       }
     }
     __syncthreads();
@@ -1439,11 +1647,75 @@ __global__ __launch_bounds__(256) void k_ekf_gain(EkfDims d, const double* __res
   }
 }
 
+// k_ekf_gain_w's path for a P_pred that is not positive definite (not inlined: the kernel's
+// common path keeps its registers)
+template <int NN>
+__device__ __noinline__ void ekf_gain_pivoted(const double* __restrict__ Pe, double* Pp1, int P, double sT, double h2,
+                                              int lane, int* __restrict__ bad) {
+  double a[NN];
+  // P_pred is not positive definite (a P0 that is not, or rounding): Gauss-Jordan with partial
+  // pivoting on the same columns, reloaded. Step k: the pivot column's lane picks the unused
+  // row with the largest |a| (lowest on ties; the index is uniform, so it stays scalar), the
+  // pivot row is normalised and column k eliminated from every other row; row pv_k ends as
+  // row k of the solution.
+  if (lane < NN) {
+#pragma unroll
+    for (int r = 0; r < NN; ++r) a[r] = Pp1[r * NN + lane];
+  } else if (lane < 2 * NN) {
+    const int c = lane - NN;
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+      double v = Pe[c * NN + k];
+      if (k < 2 * P) v += sT * Pe[c * NN + k + P];
+      if (k < P) v += h2 * Pe[c * NN + k + 2 * P];
+      a[k] = v;
+    }
+  }
+  // (a rare path: rolled loops, pv_k kept in lane k, so it adds few registers to the kernel)
+  unsigned used = 0;
+  int mypv = 0, nsing = 0;
+#pragma unroll 1
+  for (int k = 0; k < NN; ++k) {
+    double best = -1.0;
+    int bi = 0;
+#pragma unroll
+    for (int r = 0; r < NN; ++r) {
+      const bool cand = !((used >> r) & 1u) && fabs(a[r]) > best;
+      best = cand ? fabs(a[r]) : best;
+      bi = cand ? r : bi;
+    }
+    const int pv = __builtin_amdgcn_readlane(bi, k);
+    double prow = 0.0;
+#pragma unroll
+    for (int r = 0; r < NN; ++r) prow = r == pv ? a[r] : prow;
+    const double pp = read_lane_f64(prow, k);
+    nsing += pp == 0.0 ? 1 : 0;
+    const double pn = lane > k ? prow * (1.0 / pp) : prow;
+#pragma unroll
+    for (int r = 0; r < NN; ++r) {
+      const double nv = fma(-read_lane_f64(a[r], k), pn, a[r]);
+      a[r] = lane > k ? (r == pv ? pn : nv) : a[r];
+    }
+    used |= 1u << pv;
+    mypv = lane == k ? pv : mypv;
+  }
+  if (nsing && lane == 0) atomicAdd(bad, nsing);  // singular P_pred (counted, reported by the host)
+#pragma unroll 1
+  for (int k = 0; k < NN; ++k) {
+    const int pv = __builtin_amdgcn_readlane(mypv, k);
+    double v = 0.0;
+#pragma unroll
+    for (int r = 0; r < NN; ++r) v = r == pv ? a[r] : v;
+    if (lane >= NN && lane < 2 * NN) Pp1[(lane - NN) * NN + k] = v;
+  }
+}
+
 // The same gains for small states (n = NN <= 32, the head model), one wave per (sequence,
-// frame), GW waves per workgroup. P_pred is symmetric positive definite, so
-// A_i^T = P_pred^-1 (P_est F^T)^T comes from a Gauss-Jordan on [P_pred | (P_est F^T)^T] with
-// the pivots on the diagonal (no pivot search): column c on lane c, rows in registers, the
-// column-k entries by readlane. Lane NN + c ends with column c of A_i^T, i.e. row c of A_i.
+// frame), GW waves per workgroup. A_i^T = P_pred^-1 (P_est F^T)^T comes from a Gauss-Jordan
+// on [P_pred | (P_est F^T)^T] with the pivots on the diagonal (no pivot search) when P_pred is
+// positive definite (every pivot positive), else with partial pivoting: column c on lane c,
+// rows in registers, the column-k entries by readlane. Lane NN + c ends with column c of
+// A_i^T, i.e. row c of A_i.
 template <int NN, int GW>
 __global__ __launch_bounds__(64 * GW) void k_ekf_gain_w(EkfDims d, const double* __restrict__ Pest, double* Ppred,
                                                         int* __restrict__ bad) {
@@ -1475,13 +1747,11 @@ __global__ __launch_bounds__(64 * GW) void k_ekf_gain_w(EkfDims d, const double*
 #pragma unroll
     for (int r = 0; r < NN; ++r) a[r] = 0.0;
   }
-  int nbad = 0;  // pivots that are not positive (counted as k_ekf_gain counts singular ones)
+  bool spd = true;  // every pivot positive certifies P_pred > 0 (uniform: pivots by readlane)
 #pragma unroll
   for (int k = 0; k < NN; ++k) {
-    double p = read_lane_f64(a[k], k);
-    const bool ok = p > 0.0;
-    nbad += ok ? 0 : 1;
-    p = ok ? p : 1e-300;
+    const double p = read_lane_f64(a[k], k);
+    spd = spd && p > 0.0;
     const double ip = rcp_nr(p);
     const double pr = lane > k ? a[k] * ip : a[k];
     a[k] = pr;
@@ -1492,13 +1762,17 @@ __global__ __launch_bounds__(64 * GW) void k_ekf_gain_w(EkfDims d, const double*
       a[r] = lane > k ? nv : a[r];
     }
   }
-  if (nbad && lane == 0) atomicAdd(bad, nbad);
-  if (lane >= NN && lane < 2 * NN) {  // P_pred[i+1] was read by this wave only: A_i in its place
-    const int c = lane - NN;
+  if (spd) {
+    if (lane >= NN && lane < 2 * NN) {  // P_pred[i+1] was read by this wave only: A_i in its place
+      const int c = lane - NN;
 #pragma unroll
-    for (int k = 0; k < NN; ++k) Pp1[c * NN + k] = a[k];
+      for (int k = 0; k < NN; ++k) Pp1[c * NN + k] = a[k];
+    }
+    return;
   }
+  ekf_gain_pivoted<NN>(Pe, Pp1, P, sT, h2, lane, bad);
 }
+
 #define EKF_GAIN_W 4
 
 // Smoothed states x_s[i] = x_est[i] + A_i (x_s[i+1] - x_pred[i+1]) (src/core/ekf.py:295), one
@@ -1678,6 +1952,7 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
   long long* dout = (long long*)(scr + std::max(scr_f, scr_s));
   io.outliers = dout;
   int* dbad = (int*)(dout + n_seq);
+  io.bad = dbad;
   ACS_HIP(ctx, hipMemsetAsync(dbad, 0, sizeof(int), s));
   const size_t U = std::max(ekf_wg_fk_doubles(P, Jn, L, d.Ppad), ekf_wg_la_doubles(d.npad, d.Ppad));
   const size_t lds_f = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + U + d.npad +
@@ -1700,7 +1975,8 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
   // small states (the head model): k_ekf_filter_w1
 #define EKF_W1_NW(f32, ah, nw)                                                                                     \
   hipLaunchKernelGGL((k_ekf_filter_w1<f32, ah, EKF_W1_P, nw>), dim3(n_seq), dim3(64 * nw), lds_w1, s, d, io.I, \
-                     io.R, io.cams, io.meas, io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, dout, g_ekf_prof)
+                     io.R, io.cams, io.meas, io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, dout, dbad,         \
+                     g_ekf_prof)
 #define EKF_W1(f32, ah)          \
   if (w1_waves == 4)             \
     EKF_W1_NW(f32, ah, 4);       \
@@ -1711,7 +1987,7 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
     EKF_W1(f32, ah);                                                                                                \
   else                                                                                                              \
     hipLaunchKernelGGL((k_ekf_filter<f32, ah>), dim3(n_seq), dim3(512), lds_f, s, d, io.I, io.R, io.cams, io.meas, \
-                       io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, scr, dout, g_ekf_prof)
+                       io.lik, io.rstd, io.Q, io.P0, io.s0, dxp, dxe, dPp, dPe, scr, dout, dbad, g_ekf_prof)
   if (ref_numerics == ACS_EKF_ANALYTIC_H)
     EKF_FILTER(false, true);
   else if (ref_numerics)
@@ -1810,13 +2086,18 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
   if (P_smooth && !(flags & ACS_DEVICE_PTRS) &&
       (rc = acs_stage_out(ctx, P_smooth, io.P_smooth, sizeof(double) * NF * n * n, flags)))
     return rc;
-  if (outliers) {
+  if (outliers || !(flags & ACS_DEVICE_PTRS)) {
+    // a call that synchronises anyway also reports singular solves (numpy's inv raises on
+    // them, src/core/ekf.py:267,294); a device-pointer call without outliers stays asynchronous
     std::vector<long long> ho(n_seq);
-    ACS_HIP(ctx, hipMemcpyAsync(ho.data(), io.outliers, sizeof(long long) * n_seq, hipMemcpyDeviceToHost, s));
+    int hbad = 0;
+    if (outliers)
+      ACS_HIP(ctx, hipMemcpyAsync(ho.data(), io.outliers, sizeof(long long) * n_seq, hipMemcpyDeviceToHost, s));
+    ACS_HIP(ctx, hipMemcpyAsync(&hbad, io.bad, sizeof(int), hipMemcpyDeviceToHost, s));
     ACS_HIP(ctx, hipStreamSynchronize(s));
-    for (int q = 0; q < n_seq; ++q) outliers[q] = ho[q];
-  } else if (!(flags & ACS_DEVICE_PTRS)) {
-    ACS_HIP(ctx, hipStreamSynchronize(s));
+    if (outliers)
+      for (int q = 0; q < n_seq; ++q) outliers[q] = ho[q];
+    ACS_CHECK(ctx, hbad == 0, "ekf: %d singular solve(s) (I + A P_xx in the update or P_pred in a gain)", hbad);
   }
   return ACS_OK;
 }

@@ -253,14 +253,16 @@ int acs_sba_ekf_pipeline(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints,
   if ((rc = acs_stage_out(ctx, x_smooth, io.x_smooth, sizeof(double) * SN * n, flags))) return rc;
   if (outliers || !(flags & ACS_DEVICE_PTRS)) {
     std::vector<long long> ho(n_seq);
-    int hbad = 0;
+    int hbad = 0, hsing = 0;
     ACS_HIP(ctx, hipMemcpyAsync(ho.data(), io.outliers, sizeof(long long) * n_seq, hipMemcpyDeviceToHost, s));
     ACS_HIP(ctx, hipMemcpyAsync(&hbad, dbad, sizeof(int), hipMemcpyDeviceToHost, s));
+    ACS_HIP(ctx, hipMemcpyAsync(&hsing, io.bad, sizeof(int), hipMemcpyDeviceToHost, s));
     ACS_HIP(ctx, hipStreamSynchronize(s));
     if (outliers)
       for (int q = 0; q < n_seq; ++q) outliers[q] = ho[q];
     ACS_CHECK(ctx, hbad == 0, "pipeline: %d sequence(s) with the nose in fewer than two frames (no initial state, "
                               "src/core/ekf.py:144-152)", hbad);
+    ACS_CHECK(ctx, hsing == 0, "pipeline: %d singular EKF solve(s) (I + A P_xx or P_pred)", hsing);
   }
   return ACS_OK;
 }

@@ -163,20 +163,25 @@ def main():
         torch.cuda.synchronize()
 
     def timed_graph():
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # the host bracket holds the replay and the synchronisation only; the GPU clock (for
+        # roofline.achieved) comes from a second replay bracketed by events. (Round 4 recorded
+        # the start event outside the bracket and the end event inside it: asymmetric, ADVICE
+        # r04; since round 5 neither is inside.)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        # the GPU clock's start mark is recorded just ahead of the host bracket: its first
-        # record after a synchronisation costs ~15 us of host time (measured), which is not a step
-        e0.record(stream)
         t0 = time.perf_counter()
+        graph.replay()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
         graph.replay()
         e1.record(stream)
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        return time.perf_counter() - t0, e0.elapsed_time(e1) / args.steps
+        return dt, e0.elapsed_time(e1) / args.steps
 
     def max_over_ranks(dt):
         if world > 1:
@@ -249,19 +254,16 @@ def main():
                          'note': 'against the reference\'s scipy TRF solution of the same problem '
                                  '(it stops on xtol; SURVEY.md §8(a) a4)'},
     }
-    if pmc and pmc.get('fp64_flops') and pmc.get('valu_insts') and pmc.get('waves'):
-        # the same kernel against the FP64 VALU peak, and the issue rate of one wave: VALU
-        # instructions per wave (PMC) over the kernel's time in 2.4 GHz clocks
-        tfs = pmc['fp64_flops'] / (kern_ms * 1e-3) / 1e12
+    out['roofline_fp64'] = sba_fp64_roofline(int(mask.sum()), n_pts, iters_mean, kern_ms, pmc)
+    if pmc and pmc.get('valu_insts') and pmc.get('waves'):
+        # the issue rate of one wave: VALU instructions per wave (PMC) over the kernel's time
+        # in 2.4 GHz clocks
         ipw = pmc['valu_insts'] / pmc['waves']
-        out['roofline_fp64'] = {'bound': 'fp64-valu', 'achieved': tfs, 'peak': FP64_VALU_PEAK_TFS,
-                                'unit': 'TFLOP/s', 'frac': tfs / FP64_VALU_PEAK_TFS,
-                                'flops_per_launch': pmc['fp64_flops'], 'valu_insts_per_wave': ipw,
-                                'clocks_per_valu_inst': kern_ms * 1e-3 * 2.4e9 / ipw,
-                                'source': pmc['source'],
-                                'note': 'one wave per busy SIMD: each wave issues its VALU stream serially, '
-                                        'so time ~ instructions per wave x issue interval (f64 FMA: 8 clocks '
-                                        'dependent latency, profiles/r01d/probes)'}
+        out['roofline_fp64'].update({
+            'valu_insts_per_wave': ipw, 'clocks_per_valu_inst': kern_ms * 1e-3 * 2.4e9 / ipw,
+            'note': 'one wave per busy SIMD: each wave issues its VALU stream serially, so time ~ '
+                    'instructions per wave x issue interval (f64 FMA: 8 clocks dependent latency, '
+                    'profiles/r01d/probes)'})
 
     def leg(name, fn):
         # a side leg reports its failure in the line instead of costing the headline
@@ -399,6 +401,26 @@ def cpu_baseline(wl, seconds):
             res[0][2])
 
 
+def sba_fp64_roofline(n_obs, n_pts, gn_steps_mean, kern_ms, pmc):
+    """k_sba_lm against the FP64 vector peak with ALGORITHMIC flops (150 flop
+    per observation + 40 per point for one residual + Jacobian + GN evaluation), times the
+    evaluations of a solve (the GN steps + the initial one), over the kernel's time. The PMC
+    lane-flop count (64 x the f64 VALU instructions, FMA twice: what the kernel issues,
+    including the null-camera lanes and the transcendental expansions) is kept beside it as
+    issued_flops."""
+    evals = gn_steps_mean + 1.0
+    alg = (150.0 * n_obs + 40.0 * n_pts) * evals
+    tfs = alg / (kern_ms * 1e-3) / 1e12
+    r = {'bound': 'fp64-valu', 'achieved': tfs, 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
+         'frac': tfs / FP64_VALU_PEAK_TFS, 'flops_per_launch': alg, 'evaluations_per_solve': evals,
+         'flop_model': '150/obs + 40/pt per evaluation (SURVEY.md 8(d))'}
+    if pmc and pmc.get('fp64_flops'):
+        itf = pmc['fp64_flops'] / (kern_ms * 1e-3) / 1e12
+        r.update({'issued_flops_per_launch': pmc['fp64_flops'], 'issued_achieved': itf,
+                  'issued_frac': itf / FP64_VALU_PEAK_TFS, 'issued_source': pmc['source']})
+    return r
+
+
 def bench_sba_scale(ctx, torch, stream, n_frames=20000, n_cams=12, steps=10):
     """configs[4] shape on one GPU (report the roofline fraction where the
     observation tensor is ~100 MB): 12-camera ring, 20,000 frames x 20 keypoints."""
@@ -437,11 +459,7 @@ def bench_sba_scale(ctx, torch, stream, n_frames=20000, n_cams=12, steps=10):
     bytes_launch = n_frames * (C * L * 17 + 6 * L * 8)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic, pmc = pmc_per_launch('k_sba_lm', n_pts * _group(C))
-    fp64 = None
-    if pmc and pmc.get('fp64_flops'):
-        tfs = pmc['fp64_flops'] / (kern_ms * 1e-3) / 1e12
-        fp64 = {'bound': 'fp64-valu', 'achieved': tfs, 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
-                'frac': tfs / FP64_VALU_PEAK_TFS, 'flops_per_launch': pmc['fp64_flops'], 'source': pmc['source']}
+    fp64 = sba_fp64_roofline(int(mask.sum()), n_pts, rep['iters_sum'] / max(1, rep['n_problems']), kern_ms, pmc)
     return {'workload': f'sba_points C={C} frames={n_frames} L={L} (configs[4] shape, 1 GPU)',
             'frames_per_s': n_frames / dt, 'ms_per_step': dt * 1e3, 'n_points': int(n_pts),
             'obs': int(mask.sum()),

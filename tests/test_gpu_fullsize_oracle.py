@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 
 from oracle import fte as ofte, kinematics as okin
-from acinoset_amd import _native, kinematics as pkin, synth, workloads
+from acinoset_amd import _native, dist, kinematics as pkin, synth, workloads
 
 from test_gpu_pipeline import TOL, _oracle
 
@@ -28,14 +28,18 @@ pytestmark = pytest.mark.gpu
 cekf = importlib.import_module('acinoset_amd.core.ekf')
 
 
-@pytest.mark.timeout(600)
-def test_cfg3_fte_10k_frames_matches_oracle(ctx):
+@pytest.fixture(scope='module')
+def cfg3(ctx):
+    """The bench's configs[3] problem and ONE oracle solve of it (about a minute of a host
+    core), shared by the single-GPU and the 8-window tests."""
     wl = workloads.fte_workload(ctx, 10000)
     sc = wl.scene
-    X, tau, rep = ctx.fte_solve(wl.table, wl.cams, wl.meas, wl.w, wl.Ts, wl.qinv, wl.X0, shutter_delay=True,
-                                intermode=1)
     prob = ofte.Problem('default_nolure', wl.meas, wl.w, sc.K, sc.D, sc.R, sc.t, wl.Ts, sd=True, intermode='vel')
     Xo, to, info = ofte.solve(prob, wl.X0)
+    return wl, Xo, to, info
+
+
+def _check_cfg3(ctx, wl, X, tau, rep, Xo, to, info):
     assert rep['status_name'] == info['status'], (rep, info)
     assert rep['iters'] == info['iters'] and rep['n_accepted'] == info['n_accepted'], (rep, info)
     pg = okin.marker_positions('default_nolure', X[2:])
@@ -48,6 +52,26 @@ def test_cfg3_fte_10k_frames_matches_oracle(ctx):
     np.testing.assert_allclose(tau, to, rtol=0, atol=1e-6)
     np.testing.assert_allclose(rep['cost_after'], info['cost_after'], rtol=1e-9)
     assert float(np.sqrt(np.mean(np.sum((pg - wl.seq.pos3d[:, 0]) ** 2, -1)))) < 0.01
+
+
+@pytest.mark.timeout(600)
+def test_cfg3_fte_10k_frames_matches_oracle(ctx, cfg3):
+    wl, Xo, to, info = cfg3
+    X, tau, rep = ctx.fte_solve(wl.table, wl.cams, wl.meas, wl.w, wl.Ts, wl.qinv, wl.X0, shutter_delay=True,
+                                intermode=1)
+    _check_cfg3(ctx, wl, X, tau, rep, Xo, to, info)
+
+
+@pytest.mark.timeout(600)
+def test_cfg3_fte_10k_8_window_split_matches_oracle(ctx, cfg3):
+    """configs[3]'s own partitioning: the 10,000 frames as 8 frame-window ranks
+    (dist.fte_solve_virtual: the ranks' kernels and payloads of the torchrun path, the
+    all-reduce summed in-process) against the oracle's monolithic LM from the same start,
+    at the single-GPU tolerances. (The split against the single-GPU solve, 1e-9, is
+    tests/test_gpu_fullsize.py.)"""
+    wl, Xo, to, info = cfg3
+    X, tau, rep = dist.fte_solve_virtual(ctx, wl.table, wl.cams, wl.meas, wl.w, wl.Ts, wl.qinv, wl.X0, world=8)
+    _check_cfg3(ctx, wl, X, tau, rep, Xo, to, info)
 
 
 @pytest.mark.timeout(600)
