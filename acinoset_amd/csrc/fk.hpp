@@ -69,6 +69,15 @@ __device__ __forceinline__ SkelView skel_stage(const int* __restrict__ I, const 
   return skel_view(sI, sR);
 }
 
+// The copy of skel_stage with the table's sizes known to the caller (no dependent header load
+// first, and the caller's other loads in flight with it); the caller synchronises, then takes
+// skel_view of the LDS copy.
+__device__ __forceinline__ void skel_copy(const int* __restrict__ I, const double* __restrict__ R, int* sI,
+                                          double* sR, int ni, int nr, int tid, int nth) {
+  for (int e = tid; e < ni; e += nth) sI[e] = I[e];
+  for (int e = tid; e < nr; e += nth) sR[e] = R[e];
+}
+
 struct FkShared {
   double sn[FK_MAXP], cs[FK_MAXP], xp[FK_MAXP];
   double root[3], world[3];  // head-root translation (x_0, y_0, z_0) and world (lure) position

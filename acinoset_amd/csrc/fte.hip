@@ -49,7 +49,7 @@ __device__ unsigned long long g_fte_prof[64];  // wall-clock ticks (100 MHz) of 
 // (Ct = C tau columns in the local blocks, no border: Cg = 0).
 struct FteDims {
   int N, M, P, L, C, Cg, NZ, im, nblk, BP, GR, nlev;
-  int var, Ct, NT, pad_;
+  int var, Ct, NT, nint, nreal, pad_;  // nint / nreal: the skeleton table's sizes
   double Ts, la, lb, lc;
 };
 
@@ -247,10 +247,11 @@ __device__ double block_max(double v, double* s_red) {
 __host__ __device__ __forceinline__ int tc_stride(int Cg) { return Cg * Cg + Cg; }
 
 struct LinLds {
-  int cam, am, qt, ac, cf, uni, total;
+  int cam, am, qt, ac, cf, uni, tabR, tabI, total;
 };
-// dynamic LDS of k_fte_linearize (doubles)
-__host__ __device__ __forceinline__ LinLds lin_lds(int C, int L, int NZP) {
+// dynamic LDS of k_fte_linearize (doubles): QW = the compact width of the Q rows (the
+// shift / delay columns 0..2 and P..NZ-1), nint / nreal the skeleton table's sizes
+__host__ __device__ __forceinline__ LinLds lin_lds(int C, int L, int NZP, int QW, int nint, int nreal) {
   LinLds o;
   int p = 0;
   o.cam = p;
@@ -263,9 +264,14 @@ __host__ __device__ __forceinline__ LinLds lin_lds(int C, int L, int NZP) {
   p += 9 * C;
   o.cf = p;  // per camera: own, prev, prev2, v_c (3), tau_c
   p += 7 * C;
-  o.uni = p;  // observation chunk (9 per obs) | operand rows (3 x 3 LIN_MC x (NZP + 1))
-  const int a = 9 * LIN_OCH, b = 9 * LIN_MC * (NZP + 1);
-  p += a > b ? a : b;
+  o.uni = p;  // observation chunk (9 per obs) | operand rows D, B (3 LIN_MC x (NZP + 1)) and
+              // Q (3 LIN_MC x QW) | the block sums' scratch (256)
+  const int a = 9 * LIN_OCH, b = 3 * LIN_MC * (2 * (NZP + 1) + QW);
+  p += a > b ? (a > 256 ? a : 256) : (b > 256 ? b : 256);
+  o.tabR = p;  // skeleton table: reals, then ints
+  p += nreal;
+  o.tabI = p;
+  p += (nint + 1) / 2;
   o.total = p;
   return o;
 }
@@ -293,7 +299,14 @@ __device__ __forceinline__ int lin_tcol(int x, int P, int NZ, int* i) {
   return -1;
 }
 
-__global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* __restrict__ I,
+// WPC: the workgroups per CU the register budget is set for (256 threads each). The kernel is
+// bound by its dependent LDS chains, so with more frames than fit the chip at once the frames
+// in flight per CU set its throughput: 5 per CU (the LDS, ~30 KB per workgroup at 6 cameras,
+// allows it; 96 VGPRs with a few spilled) took 10,000 frames 357 -> 326 us, while a grid that
+// fits in one wave of workgroups at 4 per CU is latency-bound and the spills cost it (1,000
+// frames 42.3 -> 45.8 us; profiles/r05/seq*_lin4.log). lin_kernel picks the instance.
+template <int WPC>
+__global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int* __restrict__ I,
                                                        const double* __restrict__ Rl,
                                                        const double* __restrict__ cams,
                                                        const double* __restrict__ meas,
@@ -324,18 +337,20 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   const double* X = Xbuf + (size_t)cur * d.M * P;
   const double* tau = taubuf + (size_t)cur * d.NT + (d.var ? (size_t)k * C : 0);
   extern __shared__ double lds[];
-  const LinLds lo = lin_lds(C, L, NZP);
+  const int QW = 3 + NZ - P;  // compact Q rows: columns 0..2 and P..NZ-1
+  const LinLds lo = lin_lds(C, L, NZP, QW, d.nint, d.nreal);
   double *s_cam = lds + lo.cam, *s_am = lds + lo.am, *s_qt = lds + lo.qt, *s_ac = lds + lo.ac, *s_cf = lds + lo.cf,
          *s_u = lds + lo.uni;
+  double* s_red = s_u;  // the block sums at the end (the operand rows are dead by then)
+  int* s_tabI = reinterpret_cast<int*>(lds + lo.tabI);
+  double* s_tabR = lds + lo.tabR;
   __shared__ FkShared fk;
   __shared__ FkDeriv fkd;
   __shared__ double s_dx[3], s_ddx[3];
-  __shared__ double s_red[256];
-  __shared__ int s_tabI[FK_MAX_INTS];
-  __shared__ double s_tabR[3 * FK_MAXN];
   LPROF_T0
-  const SkelView s = skel_stage(I, Rl, s_tabI, s_tabR, tid, blockDim.x);
-  LPROF(61);
+  // every input load in flight before the one barrier: the skeleton table (sizes from the
+  // host: no dependent header load), the cameras, the frame's position rows
+  skel_copy(I, Rl, s_tabI, s_tabR, d.nint, d.nreal, tid, blockDim.x);
   const int f = k + 2;
   for (int i = tid; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
   for (int i = lo.am + tid; i < lo.cf; i += blockDim.x) lds[i] = 0.0;
@@ -344,6 +359,9 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
     s_dx[tid] = (x0 - x1) / d.Ts;
     s_ddx[tid] = (x0 - 2.0 * x1 + x2) / (d.Ts * d.Ts);
   }
+  __syncthreads();
+  const SkelView s = skel_view(s_tabI, s_tabR);
+  LPROF(61);
   LPROF(62);
   fk_frame(s, X + f * P, fk, tid, blockDim.x);
   __syncthreads();
@@ -473,7 +491,8 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
   constexpr int RC = 3 * LIN_MC;
   double* sD = s_u;            // D_l rows
   double* sB = s_u + RC * LD;  // Z_l D_l + Q_l rows
-  double* sQ = sB + RC * LD;   // Q_l rows
+  double* sQ = sB + RC * LD;   // Q_l rows, compact (RC x QW): zero outside the shift / delay columns
+  auto qcol = [&](int x) { return x < 3 ? x : (x >= P && x < NZ ? 3 + x - P : -1); };
   for (int l0 = 0; l0 < L; l0 += LIN_MC) {
 #ifdef FTE_PROFILE
     unsigned long long tb = wall_clock64();
@@ -492,11 +511,12 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
           for (int i = 0; i < 3; ++i) qv[i] = s_qt[(l * C + i0) * 3 + i];
         }
       }
+      const int cq = qcol(q);
       for (int i = 0; i < 3; ++i) {
         const int r = (3 * m + i) * LD + q;
         sD[r] = dp[i];
         sB[r] = (l < L) ? am[sym3(i, 0)] * dp[0] + am[sym3(i, 1)] * dp[1] + am[sym3(i, 2)] * dp[2] + qv[i] : 0.0;
-        sQ[r] = qv[i];
+        if (cq >= 0) sQ[(3 * m + i) * QW + cq] = qv[i];
       }
     }
     __syncthreads();
@@ -532,10 +552,12 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
         }
       }
       if (tb * 16 < P && (ta == 0 || (ta * 16 + 15 >= P && ta * 16 < NZ))) {
+        const int cq = qcol(ci);
 #pragma unroll
         for (int r0 = 0; r0 < RC; r0 += 4) {
           const int r = (r0 + lk) * LD;
-          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(sQ[r + ci], sD[r + cj], acc[q], 0, 0, 0);
+          const double qa = cq >= 0 ? sQ[(r0 + lk) * QW + (cq >= 0 ? cq : 0)] : 0.0;
+          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(qa, sD[r + cj], acc[q], 0, 0, 0);
         }
       }
     }
@@ -626,8 +648,13 @@ __global__ __launch_bounds__(256, 4) void k_fte_linearize(FteDims d, const int* 
 #endif
 }
 
+typedef void (*LinKernel)(FteDims, const int*, const double*, const double*, const double*, const double*,
+                          const double*, const double*, const FteState*, int, int, double*, double*, double*, int,
+                          double*, const double*, double*);
+static LinKernel lin_kernel(int nwg) { return nwg > 4 * 256 ? k_fte_linearize<5> : k_fte_linearize<4>; }
+
 static size_t lin_lds_bytes(const FteDims& d) {
-  return sizeof(double) * (size_t)lin_lds(d.C, d.L, (d.NZ + 15) & ~15).total;
+  return sizeof(double) * (size_t)lin_lds(d.C, d.L, (d.NZ + 15) & ~15, 3 + d.NZ - d.P, d.nint, d.nreal).total;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -850,8 +877,18 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
 #define CR_MAXBP 96
 
 #ifdef FTE_PROFILE  // per-phase wall-clock ticks (100 MHz) of block 0 (tools/prof_fte_phases.py)
+// the timeline (PROFA) of the deep levels, or with -DFTE_PROF_WIDE=n of the levels with at
+// least n elimination workgroups (tools/prof_cr_timeline.py)
+#ifdef FTE_PROF_WIDE
+#ifndef FTE_PROF_WIDE_MAX
+#define FTE_PROF_WIDE_MAX 1000000
+#endif
+#define PROF_ON_LEVEL(nwg) ((nwg) >= FTE_PROF_WIDE && (nwg) <= FTE_PROF_WIDE_MAX)
+#else
+#define PROF_ON_LEVEL(nwg) ((nwg) <= 12)
+#endif
 #define PROF_T0 unsigned long long t_prof = wall_clock64(); const unsigned long long t_start = t_prof; \
-  const bool prof_on = ne * nsplit + (int)gridDim.x * 0 <= 12 && ne > 0;
+  const bool prof_on = ne > 0 && PROF_ON_LEVEL(ne * nsplit);
 // timeline event: wave w of block 0 at time since the kernel start (deep levels only)
 #define PROFA(slot, w)                                                      \
   do {                                                                      \
@@ -1080,8 +1117,13 @@ static void cr_launch_build(const FteDims& d, hipStream_t s, int nblk, const Fte
 }
 
 // One reduction level: workgroups [0, ne * nsplit) eliminate the blocks i = a0 + s(2m+1)
-// (< iend), workgroups after them apply the pending Schur terms of level s/2 to the survivors
-// j = a0 + astep m (<= top). 1024 threads = 16 waves, register-tiled (16x16 f64 MFMA tiles):
+// (< iend), workgroups after them apply the pending Schur terms to the survivors
+// j = a0 + astep m (<= top). Pending terms are applied lazily, and at the wide levels not at
+// every level: the terms of the levels with steps lo_s, 2 lo_s, .., s/2 have not reached the
+// blocks yet (no survivor workgroups were launched for them: they would have cost whole
+// extra rounds of 1024-thread workgroups), so an eliminated block or a survivor subtracts
+// them all, level by level in ascending order (symmask bit l: the level of step 2^l stored its
+// D parts as upper tiles). 1024 threads = 16 waves, register-tiled (16x16 f64 MFMA tiles):
 //   waves 0 .. NB-1  hold the row-blocks of D_i,
 //   waves NB ..      hold one column-block each of [E_i | E_r^T | GB_i] (r = i + s);
 // Gauss-Jordan elimination on that augmented matrix leaves W_i = D_i^-1 [E_i | E_r^T | GB_i]
@@ -1100,7 +1142,7 @@ static void cr_launch_build(const FteDims& d, hipStream_t s, int nblk, const Fte
 // loaded at the next level (or by an apply workgroup), so a level is one launch.
 template <int NB>
 __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int iend, int top, int ne, int astep,
-                                                   int nsplit, int sym_in, int top_mode,
+                                                   int nsplit, unsigned symmask, int lo_s, int top_mode,
                                                    const FteState* __restrict__ st,
                                                    double* __restrict__ Dc, const double* __restrict__ Ein,
                                                    double* __restrict__ Eout, double* __restrict__ GBc,
@@ -1116,42 +1158,51 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   const int hs = s >> 1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
   if ((int)blockIdx.x >= ne * nsplit) {
-    // survivor: D_j -= dR_{j-hs} + dL_{j+hs},  GB_j likewise
+    // survivor: D_j -= sum over the pending levels sp of dR_{j-sp} + dL_{j+sp},  GB_j likewise
     if (!hs) return;
     const int j = a0 + astep * ((int)blockIdx.x - ne * nsplit);
-    const double* pr = (j - hs >= a0) ? dR + (size_t)(j - hs) * BP * LDD : nullptr;
-    const double* pl = (j + hs < iend) ? dL + (size_t)(j + hs) * BP * LDD : nullptr;
     double* D = Dc + (size_t)j * BP * BP;
     double* G = GBc + (size_t)j * BP * GR;
-    // every load of the block in flight before the first store (blockDim = 1024; the loop
-    // form waited for each round of loads: ~15 us per survivor, which at 10,000 frames
-    // occupied whole CUs for rounds of the level)
+    // every load of a level in flight before it is summed, the block's own loads first
+    // (blockDim = 1024; the loop form waited for each round of loads: ~15 us per survivor)
     constexpr int NQ = (BP * (BP + 32) + 1023) / 1024;  // GR <= 32
     const int n = BP * LDD;
-    double vr[NQ], vl[NQ], vd[NQ];
+    double vd[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int e = tid + 1024 * q;
       const int r = e / LDD, c = e - r * LDD;
-      // D parts of the pending terms hold their upper tiles only (symmetric)
-      const int es = (sym_in && c < BP && (r >> 4) > (c >> 4)) ? c * LDD + r : e;
-      const bool ok = e < n;
-      vr[q] = (ok && pr) ? pr[es] : 0.0;
-      vl[q] = (ok && pl) ? pl[es] : 0.0;
-      vd[q] = ok ? (c < BP ? D[r * BP + c] : G[r * GR + c - BP]) : 0.0;
+      vd[q] = e < n ? (c < BP ? D[r * BP + c] : G[r * GR + c - BP]) : 0.0;
+    }
+    // one pending term per trip (dR then dL of each level, ascending)
+#pragma unroll 1
+    for (int k = 0; (lo_s << (k >> 1)) <= hs; ++k) {
+      const int sp = lo_s << (k >> 1);
+      const bool sy = (symmask >> (__ffs(sp) - 1)) & 1u;
+      const double* pq = (k & 1) ? ((j + sp < iend) ? dL + (size_t)(j + sp) * BP * LDD : nullptr)
+                                 : ((j - sp >= a0) ? dR + (size_t)(j - sp) * BP * LDD : nullptr);
+      if (!pq) continue;
+      double v[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int e = tid + 1024 * q;
+        const int r = e / LDD, c = e - r * LDD;
+        // D parts of the pending terms hold their upper tiles only (symmetric)
+        const int es = (sy && c < BP && (r >> 4) > (c >> 4)) ? c * LDD + r : e;
+        v[q] = e < n ? pq[es] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) vd[q] -= v[q];
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int e = tid + 1024 * q;
       if (e >= n) continue;
       const int r = e / LDD, c = e - r * LDD;
-      double v = 0.0;
-      if (pr) v += vr[q];
-      if (pl) v += vl[q];
       if (c < BP)
-        D[r * BP + c] = vd[q] - v;
+        D[r * BP + c] = vd[q];
       else
-        G[r * GR + c - BP] = vd[q] - v;
+        G[r * GR + c - BP] = vd[q];
     }
     return;
   }
@@ -1160,8 +1211,10 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   // W_gb = D^-1 GB and Tau = GB^T W_gb for k_cr_top), after its pending terms
   const int i = top_mode ? a0 : a0 + s * (2 * ((int)blockIdx.x / nsplit) + 1);
   const int r = (!top_mode && i + s <= top) ? i + s : -1;
-  const double* qR = (hs && !top_mode) ? dR + (size_t)(i - hs) * BP * LDD : nullptr;  // pending of level hs
-  const double* qL = (hs && i + hs < iend) ? dL + (size_t)(i + hs) * BP * LDD : nullptr;
+  // pending terms of the levels lo_s .. hs: dR of the left neighbour i - sp (none for the top
+  // block) and dL of the right one i + sp (when it was eliminated, < iend)
+  auto qR_at = [&](int sp) { return !top_mode ? dR + (size_t)(i - sp) * BP * LDD : (const double*)nullptr; };
+  auto qL_at = [&](int sp) { return i + sp < iend ? dL + (size_t)(i + sp) * BP * LDD : (const double*)nullptr; };
   const double* Ei = top_mode ? nullptr : Ein + (size_t)i * BP * BP;
   const double* Er = r >= 0 ? Ein + (size_t)r * BP * BP : nullptr;
   extern __shared__ double lds[];
@@ -1194,7 +1247,12 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     }
   }
   PROF_T0
-  if (!dwave) {
+  // one workgroup holding every column block (the wide levels): the column waves' own E_i and
+  // E_r^T blocks ARE the LDS copies, stored from their registers below; otherwise the column
+  // waves copy the two coupling blocks from global memory first (HBM-bound when every CU
+  // starts a level at once: 265 KB per block with the copies, 163 KB without)
+  const bool own_all = nsplit == 1 && 16 - NB >= NBB && !top_mode;
+  if (!dwave && !own_all) {
     // the column waves copy the coupling blocks (read only in the Schur phase, after the
     // pivot steps' barriers); the row waves go straight to their loads: wave 0's first
     // pivot tile no longer waits behind this copy's round trip. Every load in flight
@@ -1225,17 +1283,17 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
       for (int q = 0; q < 4; ++q) t[K][q] = src[(r0 + lk + 4 * q) * ld + K * 16 + li];
   };
-  // pending D terms of a level that took the one-wave-per-column-block path (sym_in) are
+  // pending D terms of a level that took the one-wave-per-column-block path (its symmask bit) are
   // stored as upper tiles: tile (r0/16, K) with K < r0/16 is the transpose of tile (K, r0/16);
   // the deep path writes full tiles (rows read contiguously)
-  auto sub_rows = [&](const double* src, int ld, int r0) {
+  auto sub_rows = [&](const double* src, int ld, int r0, bool sy) {
     double v[NB][4];
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        v[K][q] = (sym_in && K * 16 < r0) ? src[(K * 16 + li) * ld + r0 + lk + 4 * q]
-                                          : src[(r0 + lk + 4 * q) * ld + K * 16 + li];
+        v[K][q] = (sy && K * 16 < r0) ? src[(K * 16 + li) * ld + r0 + lk + 4 * q]
+                                      : src[(r0 + lk + 4 * q) * ld + K * 16 + li];
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
@@ -1261,10 +1319,28 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   };
   if (dwave) {
     load_rows(Dc + (size_t)i * BP * BP, BP, wave * 16);
-    if (qR) sub_rows(qR, LDD, wave * 16);
-    if (qL) sub_rows(qL, LDD, wave * 16);
+    // dR then dL of each level; both terms' loads in flight at once where the registers allow
+    // (NB <= 5), one at a time at NB = 6
+#pragma unroll 1
+    for (int sp = lo_s; sp <= hs; sp <<= 1) {
+      const bool sy = (symmask >> (__ffs(sp) - 1)) & 1u;
+      const double *qR = qR_at(sp), *qL = qL_at(sp);
+      if constexpr (NB <= 5) {
+        if (qR) sub_rows(qR, LDD, wave * 16, sy);
+        if (qL) sub_rows(qL, LDD, wave * 16, sy);
+      } else {
+        if (qR) sub_rows(qR, LDD, wave * 16, sy);
+        __builtin_amdgcn_sched_barrier(0);
+        if (qL) sub_rows(qL, LDD, wave * 16, sy);
+      }
+    }
   } else if (J >= 0 && J < NB) {
     load_cols(Ei, BP, J * 16);
+    if (own_all)
+#pragma unroll
+      for (int K = 0; K < NB; ++K)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sEi[(K * 16 + lk + 4 * q) * BP + J * 16 + li] = t[K][q];
   } else if (J >= NB && J < 2 * NB) {
     if (Er) {
       // E_r^T: element (K*16 + lk + 4q, li) = E_r[(J-NB)*16 + li][K*16 + lk + 4q]
@@ -1273,6 +1349,11 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
       for (int K = 0; K < NB; ++K)
 #pragma unroll
         for (int q = 0; q < 4; ++q) t[K][q] = src[K * 16 + lk + 4 * q];
+      if (own_all && sEr)
+#pragma unroll
+        for (int K = 0; K < NB; ++K)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sEr[((J - NB) * 16 + li) * (BP + 1) + K * 16 + lk + 4 * q] = t[K][q];
     } else {
 #pragma unroll
       for (int K = 0; K < NB; ++K) t[K] = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -1280,8 +1361,12 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   } else if (J >= 2 * NB) {
     const int c0 = (J - 2 * NB) * 16;
     load_cols(GBc + (size_t)i * BP * GR, GR, c0);
-    if (qR) sub_cols(qR + BP, LDD, c0);
-    if (qL) sub_cols(qL + BP, LDD, c0);
+#pragma unroll 1
+    for (int k = 0; (lo_s << (k >> 1)) <= hs; ++k) {
+      const int sp = lo_s << (k >> 1);
+      const double* q = (k & 1) ? qL_at(sp) : qR_at(sp);
+      if (q) sub_cols(q + BP, LDD, c0);
+    }
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
@@ -1378,6 +1463,8 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     }
   }
   PROFA(40, NB);
+  PROFA(29, 15);
+  PROFA(31, 0);
   PROF(1);
   if (nsplit >= 3 && ((NBB + nsplit - 1) / nsplit) * BP * 16 <= 2 * BUF) {
     // Deep levels (few column-blocks per workgroup): the Schur terms are dealt out to all 16
@@ -1538,6 +1625,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   }
   PROFW(5 + 8, 15);
   PROFA(43, NB);
+  PROFA(30, 15);
 }
 
 // Fixed-order partial sums feeding the tau border (parallel over chunks, summed in chunk
@@ -2332,6 +2420,8 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   d.Ct = sd ? n_cams : 0;
   d.Cg = sd && !d.var ? n_cams : 0;
   d.NT = d.var ? N * n_cams : n_cams;
+  d.nint = (int)n_ints;
+  d.nreal = (int)n_reals;
   d.pad_ = 0;
   d.NZ = P + 6 + d.Ct;
   ACS_CHECK(ctx, d.NZ <= FTE_NZP, "fte: P + 6 + C = %d exceeds %d", d.NZ, FTE_NZP);
@@ -2462,34 +2552,46 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   return ACS_OK;
 }
 
-// one k_cr_level launch (template on the tile count NB = BP/16)
-// Returns whether this level's pending Schur terms are stored as upper tiles (the
-// one-wave-per-column-block path; the deep path of k_cr_level writes full tiles). `sym_in`:
-// the same for the level whose terms this launch applies.
-static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int iend, int top, int ne, int ns,
-                           int astep, const FteState* st, FteBuffers& b, const double* Ein, double* Eout, int* bad,
-                           int sym_in) {
-  if (ne + ns == 0) return 0;
+// workgroups per eliminated block of a k_cr_level launch: enough column waves (16 - NB per
+// workgroup), and more of them when few blocks are left (the deep levels are latency-bound):
+// the widest split whose grid still fits the 256 CUs in one wave of workgroups (one
+// 1024-thread workgroup per CU: the LDS is full), one column-block per workgroup when
+// possible, else 6 / 4 / 3 / 2 column-blocks' worth of workgroups per block
+static int cr_nsplit(const FteDims& d, int ne, int ns) {
   const int NB = d.BP >> 4, NBB = 2 * NB + d.GR / 16;
-  // workgroups per eliminated block: enough column waves (16 - NB per workgroup), and more
-  // of them when few blocks are left (the deep levels are latency-bound)
   const int need = (NBB + 16 - NB - 1) / (16 - NB);
-  // the widest split whose grid still fits the 256 CUs in one wave of workgroups (one
-  // 1024-thread workgroup per CU: the LDS is full): one column-block per workgroup when
-  // possible, else 6 / 4 / 3 / 2 column-blocks' worth of workgroups per block
   int want = 1;
   for (int c : {NBB, 6, 4, 3, 2})
     if (c <= NBB && ne * c + ns <= 256) {
       want = c;
       break;
     }
-  const int nsplit = std::min(std::max(need, want), NBB);
+  return std::min(std::max(need, want), NBB);
+}
+
+// Pending-term bookkeeping of one cyclic reduction (k_cr_level): the terms of the levels with
+// steps lo_s .. (current step)/2 have not been applied to the surviving blocks; bit l of
+// symmask: the level of step 2^l stored its D parts as upper tiles.
+struct CrPending {
+  int lo_s = 1;
+  unsigned symmask = 0;
+};
+
+// one k_cr_level launch (template on the tile count NB = BP/16). Returns whether this level's
+// pending Schur terms are stored as upper tiles (the one-wave-per-column-block path; the deep
+// path of k_cr_level writes full tiles).
+static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int iend, int top, int ne, int ns,
+                           int astep, const FteState* st, FteBuffers& b, const double* Ein, double* Eout, int* bad,
+                           const CrPending& pend) {
+  if (ne + ns == 0) return 0;
+  const int NB = d.BP >> 4, NBB = 2 * NB + d.GR / 16;
+  const int nsplit = cr_nsplit(d, ne, ns);
   const int nwg = ne * nsplit + ns;
   const size_t lds = sizeof(double) * (2 * (16 * 17 + 16 * (size_t)d.BP + 17 * (size_t)d.BP) + (size_t)d.BP * d.GR +
                                        (NB <= 5 ? 2 * (size_t)d.BP + 1 : (size_t)d.BP) * d.BP);
 #define CR_LEVEL(nb)                                                                                               \
   hipLaunchKernelGGL((k_cr_level<nb>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, top, ne, astep, nsplit, \
-                     sym_in, 0, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
+                     pend.symmask, pend.lo_s, 0, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
   switch (NB) {
     case 1: CR_LEVEL(1); break;
     case 2: CR_LEVEL(2); break;
@@ -2506,19 +2608,33 @@ static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int 
 }
 
 // Block cyclic reduction of super-blocks [a0, top] (blocks < iend may be eliminated; a
-// chain end at iend survives), nlev levels, then the last level's pending Schur terms are
-// applied to the survivors. Returns the buffer holding the final couplings E.
+// chain end at iend survives), nlev levels, then (final_apply) every pending Schur term is
+// applied to the survivors. Survivor workgroups apply the previous level's terms at every
+// level. ACS_CR_DEFER=1 launches them only at a level whose grid then still fits the chip in
+// one wave of workgroups, and the blocks subtract the deferred terms when they are next loaded:
+// at 10,000 frames that saved 26 us at level 1 and cost 30 us at levels 2-4 (each deferred
+// term is one more dependent round of loads, profiles/r05/seq10k_*.log), so it is off.
+// Returns the buffer holding the final couplings E; *pend_out: what is still pending (for the
+// top block).
 static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* st, FteBuffers& b, int a0, int iend,
-                               int top, int nlev, int* bad, bool final_apply = true, int* sym_out = nullptr) {
+                               int top, int nlev, int* bad, bool final_apply = true, CrPending* pend_out = nullptr) {
+  static const bool defer = [] {
+    const char* e = std::getenv("ACS_CR_DEFER");
+    return e && e[0] == '1';
+  }();
   const double* Ein = b.Ec;
   double* Eout = b.Ec2;
-  int sl = 1, sym = 0;
+  CrPending pend;
+  int sl = 1;
   for (int lv = 0; lv < nlev; ++lv, sl <<= 1) {
     int ne = 0, ns = 0;
     for (int i = a0 + sl; i < iend; i += 2 * sl) ++ne;
     if (sl > 1)
       for (int j = a0; j <= top; j += 2 * sl) ++ns;
-    sym = cr_launch_level(d, s, sl, a0, iend, top, ne, ns, 2 * sl, st, b, Ein, Eout, bad, sym);
+    if (ns && defer && ne * cr_nsplit(d, ne, ns) + ns > 256) ns = 0;  // defer
+    const int sym = cr_launch_level(d, s, sl, a0, iend, top, ne, ns, 2 * sl, st, b, Ein, Eout, bad, pend);
+    if (ns) pend.lo_s = sl;  // the survivors now hold every term of the levels below sl
+    pend.symmask |= (unsigned)sym << lv;
     double* t = const_cast<double*>(Ein);
     Ein = Eout;
     Eout = t;
@@ -2526,9 +2642,10 @@ static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* 
   if (nlev > 0 && final_apply) {
     int ns = 0;
     for (int j = a0; j <= top; j += sl) ++ns;
-    cr_launch_level(d, s, sl, a0, iend, top, 0, ns, sl, st, b, Ein, Eout, bad, sym);
+    cr_launch_level(d, s, sl, a0, iend, top, 0, ns, sl, st, b, Ein, Eout, bad, pend);
+    pend.lo_s = sl;
   }
-  if (sym_out) *sym_out = sym;
+  if (pend_out) *pend_out = pend;
   return Ein;
 }
 
@@ -2536,13 +2653,13 @@ static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* 
 // then W_gb = D^-1 GB and Tau = GB^T W_gb on the register-tiled Gauss-Jordan of k_cr_level
 // (top_mode); k_cr_top finishes with the tau border.
 static void cr_launch_top(const FteDims& d, hipStream_t s, int nlev, int a0, int iend, const FteState* st,
-                          FteBuffers& b, int* bad, int sym_in) {
+                          FteBuffers& b, int* bad, const CrPending& pend) {
   const int sl = 1 << nlev, NB = d.BP >> 4;
   const size_t lds = sizeof(double) * (2 * (16 * 17 + 16 * (size_t)d.BP + 17 * (size_t)d.BP) + (size_t)d.BP * d.GR +
                                        (NB <= 5 ? 2 * (size_t)d.BP + 1 : (size_t)d.BP) * d.BP);
 #define CR_TOP(nb)                                                                                                \
-  hipLaunchKernelGGL((k_cr_level<nb>), dim3(1), dim3(1024), lds, s, d, sl, a0, iend, a0, 1, sl, 1, sym_in, 1, st, \
-                     b.Dc, b.Ec, b.Ec2, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
+  hipLaunchKernelGGL((k_cr_level<nb>), dim3(1), dim3(1024), lds, s, d, sl, a0, iend, a0, 1, sl, 1, pend.symmask, \
+                     pend.lo_s, 1, st, b.Dc, b.Ec, b.Ec2, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
   switch (NB) {
     case 1: CR_TOP(1); break;
     case 2: CR_TOP(2); break;
@@ -2576,7 +2693,7 @@ static void cr_launch_assemble_build(const FteDims& d, hipStream_t s, const FteB
 static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
-  hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
+  hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
                      b.st, force, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr, b.Tc);
   hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, force, 0, 0, INT_MAX,
                      b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1);
@@ -2598,9 +2715,9 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
     cr_launch_assemble_build(d, s, b);
   }
   const int bend = d.nblk - 1;
-  int sym = 0;
-  cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad, false, &sym);
-  cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, sym);
+  CrPending pend;
+  cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad, false, &pend);
+  cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, pend);
   // tau partials, the top block and every back-substitution level in one launch, chained by
   // per-launch stamps (running the top levels' few blocks one after the other inside one
   // workgroup was tried in r03 and took 30 us: one workgroup streams a block's W at ~2 us, so
@@ -2615,7 +2732,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
                        b.normp, 1, 0, 1);
   // speculative linearisation at the trial state: its measurement terms and the model terms
   // are the trial cost (no separate cost pass)
-  hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
+  hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
                      b.X, b.tau, b.st, 0, 0, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv, b.Tc);
   hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 0, b.Floc, b.Fq, b.normp, 1, S.snap);
 }
@@ -3053,7 +3170,7 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 1, b.Fm, b.Fq, b.normp, 0);
   // the linearisation of the initial state (buffer cur = 0); later ones are speculative
   if (op.max_iters > 0)
-    hipLaunchKernelGGL(k_fte_linearize, dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
+    hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
                        b.X, b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr, b.Tc);
   ACS_HIP(ctx, hipGetLastError());
   // enqueue the iterations one ahead of the host: the host reads iteration n's status
@@ -3370,7 +3487,7 @@ int acs_fte_dist_init(acs_fte_dist* h, double* payload) {
                      (const double*)b.Fm, (const double*)b.Fq, 0, 0, (const double*)nullptr, p3);
   // the linearisation of the starting state (copy 0); later ones are speculative (phase 3)
   if (h->a0 < d.nblk && h->k_hi > h->k_lo)
-    hipLaunchKernelGGL(k_fte_linearize, dim3(h->k_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
+    hipLaunchKernelGGL(lin_kernel(h->k_hi - h->k_lo), dim3(h->k_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
                        b.meas, b.w, b.X, b.tau, b.st, 1, h->k_lo, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr,
                        (const double*)nullptr, b.Tc);
   ACS_HIP(ctx, hipGetLastError());
@@ -3425,9 +3542,9 @@ static int dist_phase2_body(acs_fte_dist* h, const double* p1) {
   hipLaunchKernelGGL(k_red_build, dim3(dr.nblk), dim3(256), 0, s, d, b.st, h->Lo, h->R, h->span, p1, r.Dc, r.Ec,
                      r.GBc, r.gmaxp);
   const int rb = dr.nblk - 1;
-  int sym = 0;
-  cr_reduce(dr, s, b.st, r, 0, dr.nblk, rb, dr.nlev, b.bad, false, &sym);
-  cr_launch_top(dr, s, dr.nlev, 0, dr.nblk, b.st, r, b.bad, sym);
+  CrPending pend;
+  cr_reduce(dr, s, b.st, r, 0, dr.nblk, rb, dr.nlev, b.bad, false, &pend);
+  cr_launch_top(dr, s, dr.nlev, 0, dr.nblk, b.st, r, b.bad, pend);
   hipLaunchKernelGGL(k_cr_tau_partial, dim3(CR_NCHUNK), dim3(512), 0, s, dr, b.st, r.Hloc, r.gloc, r.Tau, r.part, 0,
                      0, 0, dr.nblk, 0, (const double*)nullptr);
   const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
@@ -3477,7 +3594,7 @@ static int dist_phase3_body(acs_fte_dist* h, double* p3) {
   // accepted step needs no new linearisation in phase 1
   const int l_hi = std::min(h->k_hi + 1, d.N);
   if (h->a0 < d.nblk && l_hi > h->k_lo)
-    hipLaunchKernelGGL(k_fte_linearize, dim3(l_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
+    hipLaunchKernelGGL(lin_kernel(l_hi - h->k_lo), dim3(l_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
                        b.meas, b.w, b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv, b.Tc);
   const int q0 = std::max(h->k_lo + 1, 1), q1 = l_hi;
   const int t_hi = std::min(h->bend, d.nblk - 1) + 1;

@@ -11,8 +11,8 @@
   12-camera ring, rank 0's seeds) through `acs_sba_ekf_pipeline`; four clips drawn at random
   (seeded) are re-run through the oracle pieces chained (pairwise triangulation ->
   points-only SBA -> EKF initial state -> EKF + RTS, src/core/sba.py:27-70 then
-  src/core/ekf.py:26-298) at `test_gpu_pipeline.py`'s tolerances (reference numerics: the first 40
-  frames, see the test).
+  src/core/ekf.py:26-298) over all 250 frames: float64 at `test_gpu_pipeline.py`'s
+  tolerances, reference numerics at the whole-clip bounds TOL_REF_CLIP (below).
 """
 import importlib
 
@@ -74,18 +74,24 @@ def test_cfg3_fte_10k_8_window_split_matches_oracle(ctx, cfg3):
     _check_cfg3(ctx, wl, X, tau, rep, Xo, to, info)
 
 
+# Reference numerics (float32 state rounding, src/core/ekf.py:79) over whole clips: a float32
+# rounding that falls the other way after a rounding-level difference (a different summation
+# order) moves the state by ~1e-7 relative and the filter carries it, so the two trajectories
+# wander apart and back within bounds. tools/ekf_drift_survey.py (profiles/r05/drift_r05b.log,
+# 8 clips x 250 frames) measured at most x 2.2e-5, dx 5.7e-4, ddx 6.2e-3, smoothed x 9.1e-6
+# and 1.2e-6 m in the marker positions; the bounds below are those with a 2.3-2.7x margin, and
+# the positions are held to 1e-5 m (north_star: 1e-4 m).
+TOL_REF_CLIP = {'x': 5e-5, 'dx': 1.5e-3, 'ddx': 1.5e-2, 'smoothed_x': 2e-5, 'pos': 1e-5}
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize('ref_numerics', [False, True])
 def test_cfg4_benched_pipeline_clips_match_oracle(ctx, ref_numerics):
     """The bench's configs[4] step (80 clips x 250 frames, 12 cameras) and four random clips
-    through the chained oracle. float64 numerics: every frame at test_gpu_pipeline.py's
-    tolerances. Reference numerics (float32 state rounding, src/core/ekf.py:79): the first
-    40 frames at those tolerances (as the 40-frame reference fixture); past them a float32
-    rounding that falls the other way after a rounding-level difference moves the state by
-    ~1e-7 relative and the filter carries it, so the two trajectories separate slowly
-    (tools/ekf_drift.py, clip 0 over 250 frames: x within 1.9e-5, dx 3.7e-4, ddx 4.4e-3,
-    the same for the 8-wave and the small-state kernel) - the SBA points, the first
-    state and the outlier counts are still compared over the whole clip."""
+    through the chained oracle, every frame of every clip. float64 numerics at
+    test_gpu_pipeline.py's tolerances; reference numerics at TOL_REF_CLIP (above). Both: the
+    head markers' positions (FK of x_est and x_smooth) against the oracle's, the SBA points,
+    the first state and the outlier counts."""
     n_seq, n_frames, n_cams = 80, 250, 12          # bench.py bench_pipeline defaults, rank 0
     scene = synth.ring_scene(n_cams)
     seqs = [synth.make_sequence(n_frames, scene, mode='default_nolure', seed=3000 + k) for k in range(n_seq)]
@@ -99,7 +105,7 @@ def test_cfg4_benched_pipeline_clips_match_oracle(ctx, ref_numerics):
                                cekf.measurement_std(n_cams, covs), cekf.process_covariance(P, 1 / 90.0),
                                cekf.initial_covariance('head'), ref_numerics=ref_numerics)
     assert out['sba']['n_problems'] == n_seq * n_frames * 20
-    nf = n_frames if not ref_numerics else 40
+    tol = TOL_REF_CLIP if ref_numerics else dict(TOL, pos=1e-6)  # float64: measured 3.4e-7 m
     for k in np.random.default_rng(2024).choice(n_seq, 4, replace=False):
         pts, s0, o = _oracle(scene, uv[k], lik[k], seqs[k].markers, 'head', 0.5, False, ref_numerics, covs)
         g = out['pts'][k]
@@ -107,10 +113,13 @@ def test_cfg4_benched_pipeline_clips_match_oracle(ctx, ref_numerics):
         m = ~np.isnan(pts)
         np.testing.assert_allclose(g[m], pts[m], rtol=0, atol=1e-7)
         xe, xs = out['x_est'][k], out['x_smooth'][k]
+        assert xe.shape[0] == n_frames
         np.testing.assert_allclose(xe[0], o['x_est'][0], rtol=0, atol=1e-9)
-        np.testing.assert_allclose(xe[:nf, :P], o['x_est'][:nf, :P], rtol=0, atol=TOL['x'])
-        np.testing.assert_allclose(xe[:nf, P:2 * P], o['x_est'][:nf, P:2 * P], rtol=0, atol=TOL['dx'])
-        np.testing.assert_allclose(xe[:nf, 2 * P:], o['x_est'][:nf, 2 * P:], rtol=0, atol=TOL['ddx'])
-        if not ref_numerics:
-            np.testing.assert_allclose(xs[:, :P], o['x_smooth'][:, :P], rtol=0, atol=TOL['smoothed_x'])
+        np.testing.assert_allclose(xe[:, :P], o['x_est'][:, :P], rtol=0, atol=tol['x'])
+        np.testing.assert_allclose(xe[:, P:2 * P], o['x_est'][:, P:2 * P], rtol=0, atol=tol['dx'])
+        np.testing.assert_allclose(xe[:, 2 * P:], o['x_est'][:, 2 * P:], rtol=0, atol=tol['ddx'])
+        np.testing.assert_allclose(xs[:, :P], o['x_smooth'][:, :P], rtol=0, atol=tol['smoothed_x'])
+        for a, b in ((xe, o['x_est']), (xs, o['x_smooth'])):
+            dp = np.abs(okin.marker_positions('head', a[:, :P]) - okin.marker_positions('head', b[:, :P])).max()
+            assert dp < tol['pos'], (k, dp)
         assert abs(int(out['outliers'][k]) - o['outliers']) <= 1
