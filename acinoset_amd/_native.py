@@ -414,6 +414,19 @@ class Context:
             out = {k: v[0] for k, v in out.items()}
         return out
 
+    def ekf_run_dev(self, ints_p, n_ints, reals_p, n_reals, cams_p, n_cams, meas_p, lik_p, S, N, fps, thresh,
+                    max_pixel_err, r_std_p, Q_p, P0_p, s0_p, x_est_p, x_smooth_p, x_pred_p=None, ref_numerics=True,
+                    eps=1e-3, jacobian='fd'):
+        """acs_ekf_run on device pointers (ACS_DEVICE_PTRS: inputs resident in HBM, outputs
+        written there; asynchronous on the context stream, no outliers report): the layouts of
+        ekf_run, every pointer an int (torch data_ptr())."""
+        v = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+        self.check(self.lib.acs_ekf_run(self.h, v(ints_p), n_ints, v(reals_p), n_reals, v(cams_p), n_cams, v(meas_p),
+                                        v(lik_p), S, N, float(fps), float(thresh), float(max_pixel_err), v(r_std_p),
+                                        v(Q_p), v(P0_p), v(s0_p), ekf_numerics_mode(ref_numerics, jacobian),
+                                        float(eps), v(x_pred_p), v(x_est_p), v(x_smooth_p), None, None, None,
+                                        ACS_DEVICE_PTRS), 'acs_ekf_run')
+
     # ---- configs[4]: SBA + EKF fused ------------------------------------------------
     def sba_ekf_pipeline(self, table, cams, meas, likelihood, obs_markers, fps, thresh, max_pixel_err, r_std_base, Q,
                          P0, sba_opts=None, from_sba=False, ref_numerics=True, eps=1e-3, jacobian='fd'):

@@ -443,6 +443,16 @@ static int run_lm(acs_ctx* ctx, const double* dcams, int C, int K, const double2
   if (G > 64) {
     G = 64;
     S = 4;
+  } else if (G > K && (int64_t)((n_pts * G + 63) / 64) > 16 * (int64_t)ctx->n_cu) {
+    // a throughput-bound grid (more than 4 waves per SIMD) whose slot count is not a power of
+    // two: three slots per lane in groups of G / 4 lanes wherever that wastes fewer lanes
+    // (K = 12: 4 lanes x 3 slots, where 16-lane groups ran 4 lanes per point through the null
+    // camera record; the per-point LM arithmetic is also repeated by 4 lanes instead of 16)
+    const int g3 = next_pow2((K + 2) / 3);
+    if (3 * g3 < G) {
+      G = g3 < 2 ? 2 : g3;
+      S = 3;
+    }
   }
   const int64_t threads = n_pts * G;
   int block = 256;
@@ -452,13 +462,17 @@ static int run_lm(acs_ctx* ctx, const double* dcams, int C, int K, const double2
   if (dcamid) {
     rc = (S == 1) ? launch_lm_g<1, true>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in, dpts, prm,
                                          c0, c1, st)
-                  : launch_lm_g<4, true>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in, dpts, prm,
-                                         c0, c1, st);
+         : (S == 3) ? launch_lm_g<3, true>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in, dpts,
+                                           prm, c0, c1, st)
+                    : launch_lm_g<4, true>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in, dpts,
+                                           prm, c0, c1, st);
   } else {
     rc = (S == 1) ? launch_lm_g<1, false>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in, dpts,
                                           prm, c0, c1, st)
-                  : launch_lm_g<4, false>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in, dpts,
-                                          prm, c0, c1, st);
+         : (S == 3) ? launch_lm_g<3, false>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in,
+                                            dpts, prm, c0, c1, st)
+                    : launch_lm_g<4, false>(ctx, G, blocks, block, dcams, C, K, duv, dmask, dcamid, n_pts, dpts_in,
+                                            dpts, prm, c0, c1, st);
   }
   if (rc) return rc;
   ACS_HIP(ctx, hipGetLastError());
