@@ -28,6 +28,9 @@
 
 #ifdef FTE_PROFILE
 __device__ unsigned long long g_fte_prof[64];  // wall-clock ticks (100 MHz) of block 0 phases
+// k_cr_back_all per ticket: {entry, inputs ready, done, level} (tools/prof_back_all.py)
+#define FTE_BACK_TRACE 8192
+__device__ unsigned long long g_back_trace[4 * FTE_BACK_TRACE];
 // fk_frame phase marks (slots 24..28): thread 0 of block 0, time since fk_frame started
 #define FK_MARK_T0 const unsigned long long fk_t0 = wall_clock64();
 #define FK_MARK(slot)                                                                  \
@@ -197,12 +200,16 @@ __device__ __forceinline__ double strided_max(const double* __restrict__ x, int 
   return m;
 }
 
+// any blockDim (max is exact: the fold order does not change the value)
 __device__ double block_max(double v, double* s_red) {
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, n = blockDim.x;
   s_red[t] = v;
   __syncthreads();
-  for (int h = blockDim.x / 2; h > 0; h >>= 1) {
-    if (t < h) s_red[t] = fmax(s_red[t], s_red[t + h]);
+  int w = n;
+  while (w > 1) {
+    const int h = (w + 1) >> 1;
+    if (t < w - h) s_red[t] = fmax(s_red[t], s_red[t + h]);
+    w = h;
     __syncthreads();
   }
   const double r = s_red[0];
@@ -1078,7 +1085,10 @@ __global__ __launch_bounds__(1024) void k_cr_assemble_build(FteDims d, const dou
       if (dist <= 3) ev = rowA(ar)[dist * PP + pr * P + pc];
     }
     D[e] = dv;
-    E[e] = ev;
+    // E_i is upper triangular (frame distance 3 + ar - ac <= 3, and the distance-3 blocks are
+    // the model term's diagonal): its strictly lower 16 x 16 tiles are not stored; level 0 of
+    // k_cr_level, their only reader, takes them as zeros (cr_reduce's e_upper)
+    if ((r >> 4) <= (c >> 4)) E[e] = ev;
   }
   for (int e = tid; e < BP * GR; e += blockDim.x) {
     const int r = e / GR, c = e - (e / GR) * GR;
@@ -1263,8 +1273,10 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
     for (int q = 0; q < NCP; ++q) {
       const int e = ct + CN * q;
-      ve[q] = (Ei && e < BP * BP) ? Ei[e] : 0.0;
-      vr[q] = (sEr && e < BP * BP) ? Er[e] : 0.0;
+      // level 0: the strictly lower tiles of E are zero and not stored (k_cr_assemble_build)
+      const bool ez = l0 && ((e / BP) >> 4) > ((e % BP) >> 4);
+      ve[q] = (Ei && e < BP * BP && !ez) ? Ei[e] : 0.0;
+      vr[q] = (sEr && e < BP * BP && !ez) ? Er[e] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < NCP; ++q) {
@@ -1335,7 +1347,14 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
       }
     }
   } else if (J >= 0 && J < NB) {
-    load_cols(Ei, BP, J * 16);
+    if (l0) {  // level 0: tiles (K > J) of E_i are zero and not stored (k_cr_assemble_build)
+#pragma unroll
+      for (int K = 0; K < NB; ++K)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[K][q] = K > J ? 0.0 : Ei[(K * 16 + lk + 4 * q) * BP + J * 16 + li];
+    } else {
+      load_cols(Ei, BP, J * 16);
+    }
     if (own_all)
 #pragma unroll
       for (int K = 0; K < NB; ++K)
@@ -1348,7 +1367,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
       for (int K = 0; K < NB; ++K)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) t[K][q] = src[K * 16 + lk + 4 * q];
+        for (int q = 0; q < 4; ++q) t[K][q] = (l0 && K < J - NB) ? 0.0 : src[K * 16 + lk + 4 * q];
       if (own_all && sEr)
 #pragma unroll
         for (int K = 0; K < NB; ++K)
@@ -1517,7 +1536,9 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
         if (!Er) continue;
         const int I = rr - NB;
         const dbl4 acc = sEr ? chain([&](int I_, int K, int ks) { return sEr[(I_ * 16 + li) * (BP + 1) + K * 16 + 4 * ks + lk]; }, I)
-                             : chain([&](int I_, int K, int ks) { return Er[(I_ * 16 + li) * BP + K * 16 + 4 * ks + lk]; }, I);
+                             : chain([&](int I_, int K, int ks) {
+                                 return (l0 && K < I_) ? 0.0 : Er[(I_ * 16 + li) * BP + K * 16 + 4 * ks + lk];
+                               }, I);
         if (Jt < NB) {
           double* o = Eout + (size_t)r * BP * BP;
 #pragma unroll
@@ -1659,16 +1680,17 @@ __device__ __forceinline__ void cr_tau_partial_chunk(const FteDims& d, const Fte
   const int fc = (nf + CR_NCHUNK - 1) / CR_NCHUNK, bc = (nb + CR_NCHUNK - 1) / CR_NCHUNK;
   const int k0 = k_lo + ch * fc, k1 = min(k_hi, k0 + fc);
   const int b0 = b_lo + ch * bc, b1 = min(b_hi, b0 + bc);
-  // 8 loads in flight per thread (the frame / block loops are strided gathers), summed in
-  // index order
+  // 16 loads in flight per thread (the frame / block loops are strided gathers: at 10,000
+  // frames a chunk's 157 frames took 20 rounds of 8, ~22 us), summed in index order (the
+  // same bits as any batch size)
   auto sum8 = [](const double* base, size_t stride, int lo, int hi) {
     double v = 0.0;
-    for (int k = lo; k < hi; k += 8) {
-      double t[8];
+    for (int k = lo; k < hi; k += 16) {
+      double t[16];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) t[q] = k + q < hi ? base[(size_t)(k + q) * stride] : 0.0;
+      for (int q = 0; q < 16; ++q) t[q] = k + q < hi ? base[(size_t)(k + q) * stride] : 0.0;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v += t[q];
+      for (int q = 0; q < 16; ++q) v += t[q];
     }
     return v;
   };
@@ -1769,7 +1791,7 @@ __device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* 
   }
 }
 
-// k_cr_top's work (blockDim 1024, every thread): `loadp(i)` reads element i of the chunk
+// k_cr_top's work (blockDim 1024, or k_cr_back_all's 8 BP; every thread): `loadp(i)` reads element i of the chunk
 // partials, `pub_tau(c, v)` (c < 32) and `pub_row(r, v)` (r < BP) hand dtau and block 0's
 // step on to the back substitution (besides the plain dtau / dcv stores)
 template <typename LoadPart, typename PubTau, typename PubRow>
@@ -1842,7 +1864,7 @@ __device__ __forceinline__ void cr_top_body(const FteDims& d, FteState* __restri
       if (r >= Cg || c >= Cg || s_held[r] || s_held[c]) sS[e] = (r == c) ? 1.0 : 0.0;
     }
     __syncthreads();
-    wg_spd_inverse(sS, GR, GR >> 4, tmp, bad);
+    wg_gj_inverse_body<true>(sS, GR, GR >> 4, tmp, bad);  // inlined: k_cr_back_all's VGPR budget
     if (tid < GR) {
       double v = 0.0;
       for (int c = 0; c < GR; ++c) v += sS[tid * GR + c] * sr[c];
@@ -1852,7 +1874,7 @@ __device__ __forceinline__ void cr_top_body(const FteDims& d, FteState* __restri
     __syncthreads();
   }
   if (tid < 32 && (!Cg || tid >= GR)) pub_tau(tid, 0.0);
-  double v0 = 0.0;  // row tid of block 0's step (nth = 1024 > BP)
+  double v0 = 0.0;  // row tid of block 0's step (nth >= 8 BP > BP)
   if (tid < BP) {
     const double* w = W0 + (size_t)tid * WL + 2 * BP;
     double v = w[Cg];
@@ -1877,25 +1899,29 @@ __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict
       [](int, double) {}, [](int, double) {});
 }
 
-// back substitution of eliminated block i at level s (blockDim 1024; every thread calls it).
+// back substitution of eliminated block i at level s (blockDim >= 8 BP; every thread calls it).
 // `fetch(l, r)` runs after the W loads are issued and fills sl / sr_ (threads < BP) with the
 // survivors' rows and st_ (threads < 32) with dtau (zero past Cg); `publish(row, value)`
 // stores one row of the block's step.
-template <typename Fetch, typename Publish>
+// NQ = BP / 8 and NTQ = GR / 8 columns per lane (the kernels' template sizes; CR_MAXBP / 8
+// and 4 cover every size)
+template <int NQ = CR_MAXBP / 8, int NTQ = 4, typename Fetch, typename Publish>
 __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, int bend, const double* __restrict__ Wc,
                                               double* sl, double* sr_, double* st_,
-                                              Fetch fetch, Publish publish) {
+                                              Fetch fetch, Publish publish, bool late = false) {
   const int l = i - s, r = (i + s <= bend && i + s < d.nblk) ? i + s : -1;
   const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
   const double* W = Wc + (size_t)i * BP * WL;
   const int tid = threadIdx.x;
   // one row per aligned group of 8 lanes (BP <= 96 < 128 groups): the W loads of every
   // row are issued together, then an FMA chain per lane and a 3-step DPP sum
-  constexpr int NQ = CR_MAXBP / 8;
   const int row = tid >> 3, j = tid & 7;
   const bool live = row < BP;
   const double* w = W + (size_t)(live ? row : 0) * WL;
-  double a[NQ], b[NQ], t[4];
+  // late: the inputs first, then the W loads (they then stay out of the memory queues while
+  // the blocks the inputs come from are still being formed)
+  if (late) fetch(l, r);
+  double a[NQ], b[NQ], t[NTQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int c = j + 8 * q;
@@ -1903,12 +1929,12 @@ __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, in
     b[q] = (live && r >= 0 && c < BP) ? w[BP + c] : 0.0;
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < NTQ; ++q) {
     const int c = j + 8 * q;
     t[q] = (live && c < Cg) ? w[2 * BP + c] : 0.0;
   }
   const double rhs = live ? w[2 * BP + Cg] : 0.0;
-  fetch(l, r);
+  if (!late) fetch(l, r);
   __syncthreads();
   double v = 0.0;
 #pragma unroll
@@ -1917,7 +1943,7 @@ __device__ __forceinline__ void cr_back_block(const FteDims& d, int i, int s, in
     if (c < BP) v = fma(a[q], sl[c], fma(b[q], sr_[c], v));
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < NTQ; ++q) {
     const int c = j + 8 * q;
     if (c < 32) v = fma(t[q], st_[c], v);
   }
@@ -1950,7 +1976,7 @@ __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int 
 // block). A workgroup takes a ticket at entry; tickets are dealt partials first, then the
 // top, then the back blocks coarse level first, so a workgroup only ever waits for
 // workgroups of lower tickets, which have already started: the grid drains whatever the
-// residency (one 1024-thread workgroup per CU). Hand-offs (MI355X_MICROARCH.md, inter-
+// residency (two 8 BP-thread workgroups per CU). Hand-offs (MI355X_MICROARCH.md, inter-
 // workgroup visibility, first table row / handoff-1to1):
 //  - partials -> top: every element stored with a relaxed agent-scope store (sc1, written
 //    through), every wave's vmcnt(0), a barrier, then one agent-scope add to the counter
@@ -1971,7 +1997,8 @@ __device__ __forceinline__ void cr_publish_granules(unsigned long long* g, unsig
   __hip_atomic_store(g + 1, (stamp << 32) | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, FteState* __restrict__ st,
+template <int NB, int GRB>
+__global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(5))) void k_cr_back_all(FteDims d, int bend, FteState* __restrict__ st,
                                                       const double* __restrict__ Wc, const double* __restrict__ Hloc,
                                                       const double* __restrict__ gloc, const double* __restrict__ Tau,
                                                       const double* __restrict__ Tc, double* __restrict__ part,
@@ -1979,10 +2006,25 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, FteSt
                                                       double* __restrict__ dtau, double* __restrict__ dcv,
                                                       int* __restrict__ bk, unsigned long long* __restrict__ gdcv,
                                                       int* __restrict__ bad, double* __restrict__ Xbuf,
-                                                      double* __restrict__ normp) {
+                                                      double* __restrict__ normp, int late_lv) {
   __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32], sdv[CR_MAXBP], s_red[1024];
   __shared__ int s_tk;
   const int nwork = CR_NCHUNK + d.nblk;  // partials, top, nblk - 1 back blocks
+#ifdef FTE_PROFILE
+  const unsigned long long tb_entry = wall_clock64();
+  unsigned long long tb_ready = 0;
+#define BACK_TRACE(w_, lv_)                                                      \
+  do {                                                                           \
+    if (threadIdx.x == 0 && (w_) < FTE_BACK_TRACE) {                              \
+      g_back_trace[4 * (w_)] = tb_entry;                                         \
+      g_back_trace[4 * (w_) + 1] = tb_ready;                                     \
+      g_back_trace[4 * (w_) + 2] = wall_clock64();                               \
+      g_back_trace[4 * (w_) + 3] = (unsigned long long)(lv_);                    \
+    }                                                                            \
+  } while (0)
+#else
+#define BACK_TRACE(w_, lv_)
+#endif
   if (threadIdx.x == 0) s_tk = atomicAdd(bk, 1);
   __syncthreads();
   const unsigned tk = (unsigned)s_tk;
@@ -2001,6 +2043,7 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, FteSt
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(bk + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    BACK_TRACE(w, 100);
     return;
   }
   if (w == CR_NCHUNK) {
@@ -2024,8 +2067,13 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, FteSt
         },
         [&](int c, double v) { cr_publish_granules(gtau + 2 * c, stamp, v); },
         [&](int r, double v) { cr_publish_granules(gdcv + 2 * r, stamp, v); });
+    BACK_TRACE(w, 101);
     return;
   }
+#ifdef FTE_PROFILE
+  const int w_tr = w;
+  int lv_tr = -1;
+#endif
   w -= CR_NCHUNK + 1;
   int s = 1, i = 1;
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
@@ -2033,12 +2081,15 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, FteSt
     if (w < ne) {
       s = sv;
       i = sv * (2 * w + 1);
+#ifdef FTE_PROFILE
+      lv_tr = lv;
+#endif
       break;
     }
     w -= ne;
   }
   const double xpre = cr_trial_x(d, st, i, Xbuf);
-  cr_back_block(
+  cr_back_block<2 * NB, 2 * GRB>(
       d, i, s, bend, Wc, sl, sr_, st_,
       [&](int l, int r) {
         const int t = threadIdx.x;
@@ -2075,18 +2126,24 @@ __global__ __launch_bounds__(1024) void k_cr_back_all(FteDims d, int bend, FteSt
         if (wl) sl[t] = __hiloint2double((int)(unsigned)a0, (int)(unsigned)a1);
         if (wl) sr_[t] = wr ? __hiloint2double((int)(unsigned)b0, (int)(unsigned)b1) : 0.0;
         if (wt) st_[t] = __hiloint2double((int)(unsigned)c0, (int)(unsigned)c1);
+#ifdef FTE_PROFILE
+        tb_ready = wall_clock64();
+#endif
       },
       [&](int row, double v) {
         const size_t e = (size_t)i * BP + row;
         cr_publish_granules(gdcv + 2 * e, stamp, v);
         dcv[e] = v;
         sdv[row] = v;
-      });
+      },
+      s >= (1 << late_lv));
   __syncthreads();
   // constant / no delays: this block's trial state and norms (k_cr_trial's work)
   if (Xbuf) cr_trial_rows(d, st, i, threadIdx.x < BP ? sdv[threadIdx.x] : 0.0, xpre, dtau, Xbuf, nullptr, normp, false,
                           s_red);
+  BACK_TRACE(w_tr, lv_tr);
 }
+#undef BACK_TRACE
 
 // trial state X + delta, tau + dtau (clipped), norm partials per super-block. Variable
 // shutter delay: block i back-substitutes the delays of frames 3i-2..3i (X rows 3i..3i+2),
@@ -2734,9 +2791,35 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   // the W loads of every block have to be in flight at once). Constant / no delays: the
   // trial state is stepped there too; variable delays need the neighbours' rows: k_cr_trial
   double* Xt = d.var ? nullptr : b.X;
-  hipLaunchKernelGGL(k_cr_back_all, dim3(CR_NCHUNK + d.nblk), dim3(1024), 0, s, d, bend, b.st, (const double*)b.Wc,
-                     (const double*)b.Hloc, (const double*)b.gloc, (const double*)b.Tau, (const double*)b.Tc, b.part,
-                     (const double*)b.gmaxp, b.tau, b.dtau, b.dcv, b.bk, b.gdcv, b.bad, Xt, b.normp);
+  // 8 lanes per row of a block (cr_back_block): 640 threads at BP = 80, so two workgroups
+  // share a CU (91 VGPRs, 5 waves per SIMD) and one's W loads overlap the other's wait
+  // (template sizes: the columns each lane of a row holds, BP / 8 and GR / 8, no padding)
+  const int nth_back = (8 * d.BP + 63) / 64 * 64;
+  // blocks of levels >= late_lv wait for their inputs before loading W (ACS_BACK_LATE_LV; 30: never)
+  static const int late_lv = [] {
+    const char* e = std::getenv("ACS_BACK_LATE_LV");
+    return e ? std::atoi(e) : 30;
+  }();
+#define CR_BACK_ALL(nb, grb)                                                                                   \
+  hipLaunchKernelGGL((k_cr_back_all<nb, grb>), dim3(CR_NCHUNK + d.nblk), dim3(nth_back), 0, s, d, bend, b.st,  \
+                     (const double*)b.Wc, (const double*)b.Hloc, (const double*)b.gloc, (const double*)b.Tau,   \
+                     (const double*)b.Tc, b.part, (const double*)b.gmaxp, b.tau, b.dtau, b.dcv, b.bk, b.gdcv,    \
+                     b.bad, Xt, b.normp, late_lv)
+#define CR_BACK_ALL_G(nb) \
+  if (d.GR <= 16)         \
+    CR_BACK_ALL(nb, 1);   \
+  else                    \
+    CR_BACK_ALL(nb, 2)
+  switch (d.BP >> 4) {
+    case 1: CR_BACK_ALL_G(1); break;
+    case 2: CR_BACK_ALL_G(2); break;
+    case 3: CR_BACK_ALL_G(3); break;
+    case 4: CR_BACK_ALL_G(4); break;
+    case 5: CR_BACK_ALL_G(5); break;
+    default: CR_BACK_ALL_G(6); break;
+  }
+#undef CR_BACK_ALL_G
+#undef CR_BACK_ALL
   if (d.var)
     hipLaunchKernelGGL(k_cr_trial, dim3(d.nblk), dim3(256), 0, s, d, b.st, b.dcv, b.dtau, b.Hloc, b.gloc, b.X, b.tau,
                        b.normp, 1, 0, 1);
@@ -3347,6 +3430,9 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
 #ifdef FTE_PROFILE
 void acs_fte_prof_read(unsigned long long* out) {
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fte_prof), sizeof(g_fte_prof));
+}
+void acs_fte_back_trace_read(unsigned long long* out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_back_trace), sizeof(g_back_trace));
 }
 #endif
 }  // extern "C"

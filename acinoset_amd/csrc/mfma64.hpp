@@ -283,8 +283,16 @@ __device__ void wg_spd_inverse(double* A, int lda, int nb, double* tmp, int* bad
 
 // Blocked Gauss-Jordan inverse without pivoting. SPD: pivots must be positive; otherwise
 // (symmetric indefinite, e.g. the reference EKF's covariances) any pivot with |p| > 1e-300.
+// wg_gj_inverse_body: the same, inlined into the caller (whose register budget then holds
+// for it: a called function's VGPRs count against the kernel's occupancy unconstrained)
+template <bool SPD>
+__device__ __forceinline__ void wg_gj_inverse_body(double* A, int lda, int nb, double* tmp, int* bad);
 template <bool SPD>
 __device__ void wg_gj_inverse(double* A, int lda, int nb, double* tmp, int* bad) {
+  wg_gj_inverse_body<SPD>(A, lda, nb, tmp, bad);
+}
+template <bool SPD>
+__device__ __forceinline__ void wg_gj_inverse_body(double* A, int lda, int nb, double* tmp, int* bad) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
   for (int k = 0; k < nb; ++k) {
