@@ -1775,6 +1775,300 @@ __global__ __launch_bounds__(64 * GW) void k_ekf_gain_w(EkfDims d, const double*
 
 #define EKF_GAIN_W 4
 
+// The gains of the larger states (n = 33..96: the default model's 87), one workgroup of NB
+// waves per (sequence, frame), NB = n padded to 16 / 16: A_i = (P_est F^T) P_pred^-1 with the
+// explicit inverse, as the reference (src/core/ekf.py:294; on these covariances, cond ~1e12,
+// a solve instead of the inverse moves the smoothed states by 1e-5 relative, while any
+// explicit inverse then product agrees with numpy's to 1e-9). k_ekf_gain's arithmetic (the
+// blocked Gauss-Jordan of wg_gj_inverse, then the product in the same k order), so the same
+// bits, organised for throughput:
+//  * P_pred's 16 x 16 tiles in LDS (72 KB, two workgroups per CU; k_ekf_gain's padded copy
+//    plus scratch held one), in a swizzled layout: element (r, c) of a tile at
+//    r * 16 + (c ^ 4 ((r >> 1) & 3)), so every fragment read is 2-way, the minimum;
+//  * wave I owns row block I. Step k: wave k inverts the diagonal tile in registers
+//    (tile16_gj_inverse) and forms its row panel W A_kJ; after one barrier every other wave
+//    updates its whole row, A_IJ -= A_Ik A_kJ, then A_Ik <- -A_Ik W (it is the only reader of
+//    its A_Ik): two barriers per step instead of four;
+//  * the product's A operand, row block I of P_est F^T, is loaded into registers at entry
+//    (its loads in flight during the inverse); k_ekf_gain read it from global memory inside
+//    the MFMA loop.
+// Every scalar pivot positive certifies P_pred > 0 (Sylvester); otherwise the workgroup writes
+// nothing and flags the gain for k_ekf_gain_piv (partial pivoting). k_ekf_gain took 9.6 ms for
+// the bench's 64 x 499 gains of the default model.
+__device__ __forceinline__ int gt_idx(int r, int c) { return r * 16 + (c ^ (((r >> 1) & 3) << 2)); }
+
+#ifdef EKF_PROFILE
+// k_ekf_gain_t per-workgroup phase times (wall clock, 100 MHz): load, Gauss-Jordan, product,
+// count, first entry, last exit (tools/prof_ekf_gain.py)
+__device__ unsigned long long g_gain_prof[8];
+__device__ unsigned long long g_gain_trace[2 * 32768];  // per workgroup: entry, exit (last launch)
+#define GAIN_TICK(slot, t_prev)                                                   \
+  do {                                                                          \
+    __syncthreads();                                                            \
+    const unsigned long long t_now_ = wall_clock64();                           \
+    if (threadIdx.x == 0) atomicAdd(&g_gain_prof[slot], t_now_ - t_prev);       \
+    t_prev = t_now_;                                                            \
+  } while (0)
+#else
+#define GAIN_TICK(slot, t_prev)
+#endif
+
+// __launch_bounds__(1024), not 64 NB GP: a 384-thread bound made workgroups of >= 54 KB of LDS
+// run one per CU (tools/probe/lds_occ_probe.hip, profiles/r05/lds_occ_probe_c.log)
+template <int NB, int GP>
+__global__ __launch_bounds__(1024) void k_ekf_gain_t(EkfDims d, const double* __restrict__ Pest,
+                                                             double* Ppred, int* __restrict__ flag, int ng) {
+#ifdef EKF_PROFILE
+  unsigned long long t_g = wall_clock64();
+  if (threadIdx.x == 0) atomicMin(&g_gain_prof[4], t_g);
+  if (threadIdx.x == 0 && blockIdx.x < 32768) g_gain_trace[2 * blockIdx.x] = t_g;
+#endif
+  // GP gains per workgroup, NB waves each (their own LDS matrices; the barriers are shared)
+  __shared__ double sAll[GP * NB * NB * 256];
+  __shared__ int s_bads[GP];
+  const int sub = (int)threadIdx.x / (64 * NB);
+  const int g = (int)blockIdx.x * GP + sub;
+  const bool live = g < ng;  // a missing last gain's waves only keep the barriers
+  double* sA = sAll + sub * NB * NB * 256;
+  int& s_bad = s_bads[sub];
+  const int N1 = d.N - 1;
+  const int seq = (live ? g : 0) / N1, i = (live ? g : 0) - seq * N1;
+  const int tid = (int)threadIdx.x - sub * 64 * NB, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const int n = d.n, P = d.P;
+  const double sT = d.sT, h2 = 0.5 * sT * sT;
+  const size_t nn0 = (size_t)n * n, base = (size_t)seq * d.N;
+  const double* Pe = Pest + (base + i) * nn0;
+  double* Pp1 = Ppred + (base + i + 1) * nn0;
+  auto tile = [&](int I, int J) { return sA + (I * NB + J) * 256; };
+  if (tid == 0) s_bad = 0;
+  // P_pred (identity on the padding): every load in flight before the first LDS store (a
+  // loop waiting for each round of loads made the kernel 5x slower)
+  {
+    constexpr int NL = NB * 4;  // NB * NB * 256 elements / (64 NB threads)
+    double pv[NL];
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      const int e = tid + 64 * NB * q;
+      const int t = e >> 8, r = (e >> 4) & 15, c = e & 15, I = t / NB, J = t - I * NB;
+      const int R = 16 * I + r, C = 16 * J + c;
+      pv[q] = (live && R < n && C < n) ? Pp1[(size_t)R * n + C] : (R == C ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      const int e = tid + 64 * NB * q;
+      sA[(e >> 8) * 256 + gt_idx((e >> 4) & 15, e & 15)] = pv[q];
+    }
+  }
+  __syncthreads();
+  GAIN_TICK(0, t_g);
+  int nbad = 0;
+  auto inv_tile = [&](double* T, double* v) {  // the pivot tile, inverted in registers
+    tile16_gj_steps<true>(v, lane, nbad, std::make_integer_sequence<int, 16>{});
+#pragma unroll
+    for (int q = 0; q < 4; ++q) T[gt_idx(lk + 4 * q, li)] = v[q];
+  };
+  if (wave == 0) {
+    double v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = sA[gt_idx(lk + 4 * q, li)];
+    inv_tile(sA, v);
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int k = 0; k < NB; ++k) {
+    double* W = tile(k, k);
+    // row panel A_kJ <- W_k A_kJ, tile J by wave J (J != k)
+    if (wave != k) {
+      double* AkJ = tile(k, wave);
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = mfma64(W[gt_idx(li, 4 * q + lk)], AkJ[gt_idx(4 * q + lk, li)], acc);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) AkJ[gt_idx(lk + 4 * q, li)] = acc[q];
+    }
+    __syncthreads();
+    if (wave != k) {
+      // row block I = wave: A_IJ -= A_Ik A_kJ (J != k), then A_Ik <- -A_Ik W_k. Wave k + 1
+      // updates its diagonal tile first and inverts it at once: the next step's pivot
+      double* AIk = tile(wave, k);
+      double aik[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) aik[q] = AIk[gt_idx(li, 4 * q + lk)];
+      const int J0 = wave == k + 1 ? wave : 0;
+#pragma unroll 1
+      for (int jj = 0; jj < NB; ++jj) {
+        const int J = jj == 0 ? J0 : (jj <= J0 ? jj - 1 : jj);  // J0 first, then the others in order
+        if (J == k) continue;
+        double* AIJ = tile(wave, J);
+        const double* AkJ = tile(k, J);
+        dbl4 acc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = AIJ[gt_idx(lk + 4 * q, li)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = mfma64(-aik[q], AkJ[gt_idx(4 * q + lk, li)], acc);
+        if (J == k + 1 && wave == k + 1) {
+          double v[4] = {acc[0], acc[1], acc[2], acc[3]};
+          inv_tile(AIJ, v);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) AIJ[gt_idx(lk + 4 * q, li)] = acc[q];
+        }
+      }
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = mfma64(-aik[q], W[gt_idx(4 * q + lk, li)], acc);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) AIk[gt_idx(lk + 4 * q, li)] = acc[q];
+    }
+    __syncthreads();
+  }
+  // A operand of the product, row block `wave` of P_est F^T: ba[K][s] = (P_est F^T)[r][16K + 4s + lk],
+  // loaded after the inverse: held through it, its 48 VGPRs made the kernel 129 VGPRs, 3 waves
+  // per SIMD, and the two workgroups per CU the LDS allows never shared one (253 in flight)
+  double ba[NB][4];
+  {
+    const int r = 16 * wave + li;
+    const double* pr = Pe + (size_t)(r < n ? r : 0) * n;
+#pragma unroll
+    for (int K = 0; K < NB; ++K)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = 16 * K + 4 * q + lk;
+        double a = 0.0;
+        if (live && r < n && k < n) {
+          a = pr[k];
+          if (k < 2 * P) a += sT * pr[k + P];
+          if (k < P) a += h2 * pr[k + 2 * P];
+        }
+        ba[K][q] = a;
+      }
+  }
+  if (nbad && lane == 0) s_bad = 1;
+  __syncthreads();
+  GAIN_TICK(1, t_g);
+  if (!live) return;
+  if (s_bad) {  // not positive definite: P_pred left as it is, k_ekf_gain_piv takes the gain
+    if (tid == 0) flag[g] = 1;
+    return;
+  }
+  if (tid == 0) flag[g] = 0;
+  // A_i row block `wave` = (P_est F^T) P_pred^-1, k in order (k_ekf_gain's sums); P_pred[i+1]
+  // was read by this workgroup only
+#pragma unroll 1
+  for (int J = 0; J < NB; ++J) {
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int K = 0; K < NB; ++K) {
+      const double* X = tile(K, J);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = mfma64(ba[K][q], X[gt_idx(4 * q + lk, li)], acc);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = 16 * wave + lk + 4 * q, cc = 16 * J + li;
+      if (rr < n && cc < n) Pp1[(size_t)rr * n + cc] = acc[q];
+    }
+  }
+#ifdef EKF_PROFILE
+  GAIN_TICK(2, t_g);
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_gain_prof[3], 1ull);
+    const unsigned long long t_e = wall_clock64();
+    atomicMax(&g_gain_prof[5], t_e);
+    if (blockIdx.x < 32768) g_gain_trace[2 * blockIdx.x + 1] = t_e;
+  }
+#endif
+}
+
+// The gains k_ekf_gain_t flagged (P_pred not positive definite): the inverse by Gauss-Jordan
+// with partial pivoting on [P_pred | I] in LDS (the reference inverts by LAPACK's pivoted LU,
+// src/core/ekf.py:294), then (P_est F^T) P_pred^-1. Step k: wave 0 picks the unused row with
+// the largest |a_rk| (lowest on ties), the pivot row is normalised and column k eliminated
+// from every other row; row pv_k of the right half ends as row k of the inverse. A rare path
+// (an indefinite P_pred), one workgroup per gain, every other workgroup returns at once.
+__global__ __launch_bounds__(256) void k_ekf_gain_piv(EkfDims d, const double* __restrict__ Pest, double* Ppred,
+                                                      const int* __restrict__ flag, int* __restrict__ bad) {
+  if (!flag[blockIdx.x]) return;
+  const int N1 = d.N - 1;
+  const int seq = blockIdx.x / N1, i = blockIdx.x - seq * N1;
+  const int tid = threadIdx.x, nth = blockDim.x, n = d.n, P = d.P, LDM = 2 * n + 1;
+  const double sT = d.sT, h2 = 0.5 * sT * sT;
+  const size_t nn0 = (size_t)n * n, base = (size_t)seq * d.N;
+  const double* Pe = Pest + (base + i) * nn0;
+  double* Pp1 = Ppred + (base + i + 1) * nn0;
+  extern __shared__ double lds[];
+  double* M = lds;                         // n x LDM
+  double* fcol = M + (size_t)n * LDM;      // n: column k before the step
+  int* s_pv = (int*)(fcol + n);            // n: pivot row of step k
+  __shared__ unsigned long long s_used[2];
+  __shared__ int s_sing;
+  for (int e = tid; e < n * 2 * n; e += nth) {
+    const int r = e / (2 * n), c = e - r * 2 * n;
+    M[(size_t)r * LDM + c] = c < n ? Pp1[(size_t)r * n + c] : (c - n == r ? 1.0 : 0.0);
+  }
+  if (tid == 0) {
+    s_used[0] = s_used[1] = 0ull;
+    s_sing = 0;
+  }
+  __syncthreads();
+  for (int k = 0; k < n; ++k) {
+    if (tid < 64) {
+      double best = -1.0;
+      int bi = n;
+      for (int r = tid; r < n; r += 64) {
+        const bool used = (s_used[r >> 6] >> (r & 63)) & 1ull;
+        const double a = fabs(M[(size_t)r * LDM + k]);
+        if (!used && a > best) {
+          best = a;
+          bi = r;
+        }
+      }
+#pragma unroll
+      for (int h = 32; h > 0; h >>= 1) {
+        const double ob = __shfl_xor(best, h, 64);
+        const int oi = __shfl_xor(bi, h, 64);
+        if (ob > best || (ob == best && oi < bi)) {
+          best = ob;
+          bi = oi;
+        }
+      }
+      if (tid == 0) {
+        s_pv[k] = bi;
+        s_used[bi >> 6] |= 1ull << (bi & 63);
+        if (!(best > 0.0)) s_sing += 1;
+      }
+    }
+    __syncthreads();
+    const int pv = s_pv[k];
+    const double p = M[(size_t)pv * LDM + k];
+    const double ip = p != 0.0 ? 1.0 / p : 0.0;
+    for (int r = tid; r < n; r += nth) fcol[r] = M[(size_t)r * LDM + k];
+    __syncthreads();
+    for (int c = tid; c < 2 * n; c += nth) M[(size_t)pv * LDM + c] *= ip;
+    __syncthreads();
+    for (int e = tid; e < n * 2 * n; e += nth) {
+      const int r = e / (2 * n), c = e - r * 2 * n;
+      if (r != pv) M[(size_t)r * LDM + c] = fma(-fcol[r], M[(size_t)pv * LDM + c], M[(size_t)r * LDM + c]);
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && s_sing) atomicAdd(bad, s_sing);
+  // A_i[r][c] = sum_k (P_est F^T)[r][k] inv[k][c], inv[k] = row pv_k of the right half
+  for (int e = tid; e < n * n; e += nth) {
+    const int r = e / n, c = e - r * n;
+    const double* pr = Pe + (size_t)r * n;
+    double v = 0.0;
+    for (int k = 0; k < n; ++k) {
+      double a = pr[k];
+      if (k < 2 * P) a += sT * pr[k + P];
+      if (k < P) a += h2 * pr[k + 2 * P];
+      v = fma(a, M[(size_t)s_pv[k] * LDM + n + c], v);
+    }
+    Pp1[(size_t)r * n + c] = v;
+  }
+}
+
 // Smoothed states x_s[i] = x_est[i] + A_i (x_s[i+1] - x_pred[i+1]) (src/core/ekf.py:295), one
 // workgroup per sequence: a row per aligned group of 8 lanes (3 passes cover n <= 96), the
 // gain of the next frame loaded while this frame's products are summed.
@@ -1946,7 +2240,9 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
   double* dPp = (double*)acs_ws(ctx, WS_FTE14, sizeof(double) * NF * n * n);
   const size_t scr_f = (size_t)n_seq * ((size_t)(P + 1) * d.m + 2 * (size_t)d.mpad * d.Ppad + 2 * d.mpad);
   const size_t scr_s = (size_t)n_seq * 5 * d.npad * d.npad;
-  double* scr = (double*)acs_ws(ctx, WS_FTE6, sizeof(double) * std::max(scr_f, scr_s) + 64 * (size_t)n_seq * 8);
+  // tail: outlier counts (n_seq), the singular-solve counter, then k_ekf_gain_t's per-gain flags
+  double* scr = (double*)acs_ws(ctx, WS_FTE6, sizeof(double) * std::max(scr_f, scr_s) + 64 * (size_t)n_seq * 8 +
+                                                  sizeof(int) * (size_t)n_seq * n_frames + 64);
   if (!io.x_pred || !io.P_est || !dPp || !scr) return ACS_E_NOMEM;
   double *dxp = io.x_pred, *dxe = io.x_est, *dxs = io.x_smooth, *dPe = io.P_est, *dPs = io.P_smooth;
   long long* dout = (long long*)(scr + std::max(scr_f, scr_s));
@@ -2006,6 +2302,36 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
       const size_t ng = (size_t)n_seq * (n_frames - 1);
       hipLaunchKernelGGL((k_ekf_gain_w<3 * EKF_W1_P, EKF_GAIN_W>), dim3((unsigned)((ng + EKF_GAIN_W - 1) / EKF_GAIN_W)),
                          dim3(64 * EKF_GAIN_W), 0, s, d, (const double*)dPe, dPp, dbad);
+    } else if (n_frames >= 2 && d.npad >= 48) {
+      // tiled gains, then the pivoted path for any P_pred that is not positive definite
+      const unsigned ng = (unsigned)((size_t)n_seq * (n_frames - 1));
+      int* dflag = (int*)(scr + std::max(scr_f, scr_s)) + 16 * (size_t)n_seq + 16;
+  // two gains per workgroup: one 144 KB workgroup per CU (a workgroup of >= 54 KB of LDS never
+  // shares a CU, tools/probe/lds_occ_probe.hip: the 72 KB one-gain form ran one gain per CU)
+  // one gain per workgroup, two workgroups per CU: 4.09 ms for the bench's 64 x 499 gains;
+  // two gains per 768-thread workgroup (lockstep barriers) 4.31 ms (ACS_EKF_GAIN_GP=2, A/B)
+  static const int gp = [] {
+    const char* e = std::getenv("ACS_EKF_GAIN_GP");
+    return e && std::atoi(e) == 2 ? 2 : 1;
+  }();
+#define EKF_GAIN_T(NB)                                                                                          \
+  if (gp == 1)                                                                                                  \
+    hipLaunchKernelGGL((k_ekf_gain_t<NB, 1>), dim3(ng), dim3(64 * NB), 0, s, d, (const double*)dPe, dPp, dflag, \
+                       (int)ng);                                                                                \
+  else                                                                                                          \
+    hipLaunchKernelGGL((k_ekf_gain_t<NB, 2>), dim3((ng + 1) / 2), dim3(128 * NB), 0, s, d, (const double*)dPe,  \
+                       dPp, dflag, (int)ng)
+      switch (d.npad >> 4) {
+        case 3: EKF_GAIN_T(3); break;
+        case 4: EKF_GAIN_T(4); break;
+        case 5: EKF_GAIN_T(5); break;
+        default: EKF_GAIN_T(6); break;
+      }
+#undef EKF_GAIN_T
+      const size_t lds_p = sizeof(double) * ((size_t)n * (2 * n + 1) + n) + sizeof(int) * n;
+      hipLaunchKernelGGL(k_ekf_gain_piv, dim3(ng), dim3(256), lds_p, s, d, (const double*)dPe, dPp,
+                         (const int*)dflag, dbad);
+      ACS_HIP(ctx, hipGetLastError());
     } else if (n_frames >= 2) {
       const size_t lds_g = sizeof(double) * ((size_t)d.npad * (d.npad + 1) + 512);
       hipLaunchKernelGGL(k_ekf_gain, dim3((unsigned)((size_t)n_seq * (n_frames - 1))), dim3(256), lds_g, s, d,
@@ -2026,6 +2352,19 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
 
 extern "C" {
 void acs_ekf_prof(unsigned long long* p) { g_ekf_prof = p; }
+#ifdef EKF_PROFILE
+void acs_ekf_gain_prof(unsigned long long* out, int reset) {
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, ~0ull, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gain_prof), z, sizeof(z));
+  } else {
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gain_prof), sizeof(g_gain_prof));
+  }
+}
+void acs_ekf_gain_trace(unsigned long long* out) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gain_trace), sizeof(g_gain_trace));
+}
+#endif
 
 int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals, int64_t n_reals,
                 const double* cams, int32_t n_cams, const double* meas, const double* likelihood, int32_t n_seq,

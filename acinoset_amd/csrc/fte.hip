@@ -1126,6 +1126,89 @@ static void cr_launch_build(const FteDims& d, hipStream_t s, int nblk, const Fte
 #undef CR_BUILD
 }
 
+// Fixed-order partial sums feeding the tau border (parallel over chunks, summed in chunk
+// order by k_cr_top): per-frame tau blocks of the normal matrix / gradient, and the tau
+// Schur contributions of every eliminated super-block.
+#define CR_NCHUNK 64
+// chunk `ch` of the partial sums; `store(e, v)` writes element e of the chunk's row of `part`
+template <typename Store>
+__device__ __forceinline__ void cr_tau_partial_chunk(const FteDims& d, const FteState* __restrict__ st,
+                                                     const double* __restrict__ Hloc, const double* __restrict__ gloc,
+                                                     const double* __restrict__ Tau, int k_lo, int k_hi, int b_lo,
+                                                     int b_hi, int hsel, const double* __restrict__ Tc, int ch,
+                                                     Store store) {
+  // frames [k_lo, k_hi) (tau blocks of their normal matrices / gradients) and eliminated
+  // super-blocks [b_lo, b_hi) (tau Schur terms), each range cut into CR_NCHUNK chunks
+  if (hsel) {
+    Hloc += (size_t)st->cur * d.N * FTE_NZP * FTE_NZP;
+    gloc += (size_t)st->cur * d.N * FTE_NZP;
+    if (Tc) Tc += (size_t)st->cur * d.N * tc_stride(d.Cg);
+  }
+  const int P = d.P, Cg = d.Cg, GR = d.GR;
+  const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
+  const int nf = max(0, k_hi - k_lo), nb = max(0, b_hi - b_lo);
+  const int fc = (nf + CR_NCHUNK - 1) / CR_NCHUNK, bc = (nb + CR_NCHUNK - 1) / CR_NCHUNK;
+  const int k0 = k_lo + ch * fc, k1 = min(k_hi, k0 + fc);
+  const int b0 = b_lo + ch * bc, b1 = min(b_hi, b0 + bc);
+  // 16 loads in flight per thread (the frame / block loops are strided gathers: at 10,000
+  // frames a chunk's 157 frames took 20 rounds of 8, ~22 us), summed in index order (the
+  // same bits as any batch size)
+  auto sum8 = [](const double* base, size_t stride, int lo, int hi) {
+    double v = 0.0;
+    for (int k = lo; k < hi; k += 16) {
+      double t[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t[q] = k + q < hi ? base[(size_t)(k + q) * stride] : 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v += t[q];
+    }
+    return v;
+  };
+  for (int e = threadIdx.x; e < nE; e += blockDim.x) {
+    double v;
+    if (Tc && e < nH + Cg) {
+      v = sum8(Tc + e, (size_t)tc_stride(Cg), k0, k1);  // compact copy from k_fte_linearize
+    } else if (e < nH) {
+      const int r = e / Cg, c = e % Cg;
+      v = sum8(Hloc + (P + 6 + r) * FTE_NZP + P + 6 + c, (size_t)FTE_NZP * FTE_NZP, k0, k1);
+    } else if (e < nH + Cg) {
+      v = sum8(gloc + P + 6 + (e - nH), FTE_NZP, k0, k1);
+    } else {
+      v = sum8(Tau + (e - nH - Cg), (size_t)GR * GR, b0, b1);
+    }
+    store(e, v);
+  }
+}
+
+// the top level's extra workgroups (cr_launch_top with partials): the tau partial sums of the
+// single-GPU solve, computed while the top block is eliminated (k_cr_back_all's top then
+// adds the top block's own Tau last)
+struct CrTauSrc {
+  const double* Tc;
+  const double* gmaxp;
+  double* part;
+};
+
+// the top level's extra workgroups (k_cr_level, top_mode, blockIdx.x = 1 + chunk): chunk
+// `ch` of the tau partial sums (every frame, every eliminated block but the top one, a0 = 0;
+// consecutive threads read consecutive elements) and of the frames' |g| max, as row ch of
+// part (nE + 1 wide). (One wave per element, lanes over the frames, took 130 us at 10,000
+// frames: every load instruction touched 64 lines.)
+__device__ __forceinline__ void cr_top_border_sums(const FteDims& d, const FteState* __restrict__ st,
+                                                   const double* __restrict__ Tau, const CrTauSrc& tsrc) {
+  const int ch = (int)blockIdx.x - 1, nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
+  double* row = tsrc.part + (size_t)ch * (nE + 1);
+  cr_tau_partial_chunk(d, st, nullptr, nullptr, Tau, 0, d.N, 1, d.nblk, 1, tsrc.Tc, ch,
+                       [&](int e, double v) { row[e] = v; });
+  if (threadIdx.x < 64) {
+    const int fm = (d.M + CR_NCHUNK - 1) / CR_NCHUNK, f0 = ch * fm, f1 = min(d.M, f0 + fm);
+    double mx = strided_max(tsrc.gmaxp, f0 + (int)threadIdx.x, f1, 64, 0.0);
+#pragma unroll
+    for (int h = 32; h > 0; h >>= 1) mx = fmax(mx, __shfl_xor(mx, h, 64));
+    if (threadIdx.x == 0) row[nE] = mx;
+  }
+}
+
 // One reduction level: workgroups [0, ne * nsplit) eliminate the blocks i = a0 + s(2m+1)
 // (< iend), workgroups after them apply the pending Schur terms to the survivors
 // j = a0 + astep m (<= top). Pending terms are applied lazily, and at the wide levels not at
@@ -1158,8 +1241,12 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
                                                    double* __restrict__ Eout, double* __restrict__ GBc,
                                                    double* __restrict__ Wc, double* __restrict__ Tau,
                                                    double* __restrict__ dL, double* __restrict__ dR,
-                                                   int* __restrict__ bad) {
+                                                   int* __restrict__ bad, CrTauSrc tsrc) {
   if (st->status != 0) return;
+  if (top_mode && blockIdx.x >= 1) {
+    cr_top_border_sums(d, st, Tau, tsrc);
+    return;
+  }
   // pivot tiles in LDS with row stride 17 doubles: the 16 rows an A fragment reads land on
   // distinct banks
   constexpr int BP = 16 * NB, TS = 17, BUF = 16 * TS + 16 * BP + BP * TS;
@@ -1656,60 +1743,6 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   PROFA(30, 15);
 }
 
-// Fixed-order partial sums feeding the tau border (parallel over chunks, summed in chunk
-// order by k_cr_top): per-frame tau blocks of the normal matrix / gradient, and the tau
-// Schur contributions of every eliminated super-block.
-#define CR_NCHUNK 64
-// chunk `ch` of the partial sums; `store(e, v)` writes element e of the chunk's row of `part`
-template <typename Store>
-__device__ __forceinline__ void cr_tau_partial_chunk(const FteDims& d, const FteState* __restrict__ st,
-                                                     const double* __restrict__ Hloc, const double* __restrict__ gloc,
-                                                     const double* __restrict__ Tau, int k_lo, int k_hi, int b_lo,
-                                                     int b_hi, int hsel, const double* __restrict__ Tc, int ch,
-                                                     Store store) {
-  // frames [k_lo, k_hi) (tau blocks of their normal matrices / gradients) and eliminated
-  // super-blocks [b_lo, b_hi) (tau Schur terms), each range cut into CR_NCHUNK chunks
-  if (hsel) {
-    Hloc += (size_t)st->cur * d.N * FTE_NZP * FTE_NZP;
-    gloc += (size_t)st->cur * d.N * FTE_NZP;
-    if (Tc) Tc += (size_t)st->cur * d.N * tc_stride(d.Cg);
-  }
-  const int P = d.P, Cg = d.Cg, GR = d.GR;
-  const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
-  const int nf = max(0, k_hi - k_lo), nb = max(0, b_hi - b_lo);
-  const int fc = (nf + CR_NCHUNK - 1) / CR_NCHUNK, bc = (nb + CR_NCHUNK - 1) / CR_NCHUNK;
-  const int k0 = k_lo + ch * fc, k1 = min(k_hi, k0 + fc);
-  const int b0 = b_lo + ch * bc, b1 = min(b_hi, b0 + bc);
-  // 16 loads in flight per thread (the frame / block loops are strided gathers: at 10,000
-  // frames a chunk's 157 frames took 20 rounds of 8, ~22 us), summed in index order (the
-  // same bits as any batch size)
-  auto sum8 = [](const double* base, size_t stride, int lo, int hi) {
-    double v = 0.0;
-    for (int k = lo; k < hi; k += 16) {
-      double t[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) t[q] = k + q < hi ? base[(size_t)(k + q) * stride] : 0.0;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) v += t[q];
-    }
-    return v;
-  };
-  for (int e = threadIdx.x; e < nE; e += blockDim.x) {
-    double v;
-    if (Tc && e < nH + Cg) {
-      v = sum8(Tc + e, (size_t)tc_stride(Cg), k0, k1);  // compact copy from k_fte_linearize
-    } else if (e < nH) {
-      const int r = e / Cg, c = e % Cg;
-      v = sum8(Hloc + (P + 6 + r) * FTE_NZP + P + 6 + c, (size_t)FTE_NZP * FTE_NZP, k0, k1);
-    } else if (e < nH + Cg) {
-      v = sum8(gloc + P + 6 + (e - nH), FTE_NZP, k0, k1);
-    } else {
-      v = sum8(Tau + (e - nH - Cg), (size_t)GR * GR, b0, b1);
-    }
-    store(e, v);
-  }
-}
-
 __global__ __launch_bounds__(512) void k_cr_tau_partial(FteDims d, const FteState* __restrict__ st,
                                                         const double* __restrict__ Hloc,
                                                         const double* __restrict__ gloc,
@@ -1791,47 +1824,77 @@ __device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* 
   }
 }
 
-// k_cr_top's work (blockDim 1024, or k_cr_back_all's 8 BP; every thread): `loadp(i)` reads element i of the chunk
-// partials, `pub_tau(c, v)` (c < 32) and `pub_row(r, v)` (r < BP) hand dtau and block 0's
-// step on to the back substitution (besides the plain dtau / dcv stores)
+// k_cr_top's work (blockDim 1024, or k_cr_back_all's 8 BP; every thread, nth >= 8 BP):
+// `loadp(i)` reads element i of the CR_NCHUNK chunk partials, rows nE wide; fused (the rows
+// of cr_launch_top with_partials): rows nE + 1 wide, the chunk's frame |g| max last;
+// `pub_tau(c, v)` (c < 32) and `pub_row(r, v)` (r < BP) hand dtau and block 0's step on to
+// the back substitution (besides the plain dtau / dcv stores); tau0: the top block's own Tau
+// term when the sums leave it out
 template <typename LoadPart, typename PubTau, typename PubRow>
 __device__ __forceinline__ void cr_top_body(const FteDims& d, FteState* __restrict__ st, const double* __restrict__ W0,
                                             const double* __restrict__ gmaxp, double* __restrict__ taubuf,
                                             double* __restrict__ dcv, double* __restrict__ dtau, int* __restrict__ bad,
                                             double* __restrict__ Xbuf, double* __restrict__ normp, LoadPart loadp,
-                                            PubTau pub_tau, PubRow pub_row) {
+                                            PubTau pub_tau, PubRow pub_row, bool fused = false,
+                                            const double* __restrict__ tau0 = nullptr) {
   // block 0 has been eliminated by k_cr_level (top_mode): W0 = its W (BP x WL), its tau Schur
-  // term is in the Tau sums like every other block's
+  // term is in the Tau sums like every other block's (or in tau0)
   const int tid = threadIdx.x, nth = blockDim.x;
   const int BP = d.BP, GR = d.GR, Cg = d.Cg, WL = 2 * BP + GR;
   const double lam = st->lam;
   const double xpre = cr_trial_x(d, st, 0, Xbuf);
+  // block 0's step rows = rhs - W_tau dtau, 8 lanes per row: this lane's W_tau entries and the
+  // rhs loaded first (they were dependent loads after the tau solve)
+  const int wrow = tid >> 3, wj = tid & 7;
+  const bool wlive = wrow < BP;
+  double wq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = wj + 8 * q;
+    wq[q] = (wlive && c < Cg) ? W0[(size_t)wrow * WL + 2 * BP + c] : 0.0;
+  }
+  const double wrhs = (wlive && wj == 0) ? W0[(size_t)wrow * WL + 2 * BP + Cg] : 0.0;
   __shared__ double sS[32 * 32];
   __shared__ double sr[32];
   __shared__ double tmp[512];
   __shared__ double s_red[1024];
+  __shared__ double s_dt[32];
   // chunk partials -> sums (fixed order)
   const int nH = Cg * Cg, nE = nH + Cg + GR * GR;
   __shared__ double s_sum[16 * 16 + 16 + 32 * 32];
   __shared__ int s_held[32];
-  for (int e = tid; e < nE; e += nth) {
+  const int pw = fused ? nE + 1 : nE;
+  __shared__ double s_gm;
+  for (int e = tid; e < (fused ? nE + 1 : nE); e += nth) {
     // 16 loads in flight at a time, summed in chunk order (one CU streams the 64 x nE
     // partials from L2: splitting the chunks over more threads did not help, r03j)
     double v = 0.0;
     for (int c0 = 0; c0 < CR_NCHUNK; c0 += 16) {
       double pv[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) pv[q] = loadp((size_t)(c0 + q) * nE + e);
+      for (int q = 0; q < 16; ++q) pv[q] = loadp((size_t)(c0 + q) * pw + e);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) v += pv[q];
+      for (int q = 0; q < 16; ++q) v = e < nE ? v + pv[q] : fmax(v, pv[q]);
     }
+    if (e == nE) {
+      s_gm = v;  // fused: the frames' |g| max
+      continue;
+    }
+    if (tau0 && e >= nH + Cg) v += tau0[e - nH - Cg];
     s_sum[e] = v;
   }
   __syncthreads();
   if (tid < 32) s_held[tid] = tid >= Cg || tau_held(taubuf[(size_t)st->cur * d.NT + tid], s_sum[nH + tid], d.Ts, tid);
   __syncthreads();
   // gradient max (frames + free tau border)
-  {
+  if (fused) {
+    if (tid == 0) {
+      double mx = s_gm;
+      for (int c = 0; c < Cg; ++c)
+        if (!s_held[c]) mx = fmax(mx, fabs(s_sum[nH + c]));
+      st->gmax = mx;
+    }
+  } else {
     double mx = 0.0;
     mx = strided_max(gmaxp, tid, d.M, nth, mx);
     for (int c = tid; c < Cg; c += nth)
@@ -1839,6 +1902,7 @@ __device__ __forceinline__ void cr_top_body(const FteDims& d, FteState* __restri
     mx = block_max(mx, s_red);
     if (tid == 0) st->gmax = mx;
   }
+  if (tid < 32) s_dt[tid] = 0.0;
   if (Cg) {
     // S = D_tau - sum_i Tau_i ;  rhs = b_tau - sum_i Tau_i[:, Cg]   (GR x GR, padded)
     for (int e = tid; e < GR * GR; e += nth) {
@@ -1868,23 +1932,33 @@ __device__ __forceinline__ void cr_top_body(const FteDims& d, FteState* __restri
     if (tid < GR) {
       double v = 0.0;
       for (int c = 0; c < GR; ++c) v += sS[tid * GR + c] * sr[c];
-      dtau[tid] = (tid < Cg && !s_held[tid]) ? v : 0.0;
-      if (tid < 32) pub_tau(tid, (tid < Cg && !s_held[tid]) ? v : 0.0);
+      const double dt = (tid < Cg && !s_held[tid]) ? v : 0.0;
+      dtau[tid] = dt;
+      if (tid < 32) {
+        pub_tau(tid, dt);
+        s_dt[tid] = dt;
+      }
     }
-    __syncthreads();
   }
   if (tid < 32 && (!Cg || tid >= GR)) pub_tau(tid, 0.0);
-  double v0 = 0.0;  // row tid of block 0's step (nth >= 8 BP > BP)
-  if (tid < BP) {
-    const double* w = W0 + (size_t)tid * WL + 2 * BP;
-    double v = w[Cg];
-    for (int c = 0; c < Cg; ++c) v -= w[c] * dtau[c];
-    dcv[tid] = v;
-    pub_row(tid, v);
-    v0 = v;
+  __syncthreads();
+  // block 0's step: row wrow = rhs - sum_c W[wrow][2 BP + c] dtau_c (a 3-step DPP sum)
+  double vp = 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = wj + 8 * q;
+    if (c < 32) vp = fma(wq[q], s_dt[c], vp);
   }
+  vp = group_sum<8>(vp);
+  if (wlive && wj == 0) {
+    const double v = wrhs - vp;
+    dcv[wrow] = v;
+    pub_row(wrow, v);
+    tmp[wrow] = v;
+  }
+  __syncthreads();
   // the single-GPU solve steps block 0 (and the constant delays) here: no k_cr_trial launch
-  if (Xbuf) cr_trial_rows(d, st, 0, v0, xpre, dtau, Xbuf, taubuf, normp, d.Cg != 0, s_red);
+  if (Xbuf) cr_trial_rows(d, st, 0, tid < BP ? tmp[tid] : 0.0, xpre, dtau, Xbuf, taubuf, normp, d.Cg != 0, s_red);
 }
 
 __global__ __launch_bounds__(1024) void k_cr_top(FteDims d, FteState* __restrict__ st, const double* __restrict__ W0,
@@ -1970,27 +2044,25 @@ __global__ __launch_bounds__(1024) void k_cr_back(FteDims d, int s, int a0, int 
       [&](int row, double v) { dcv[(size_t)i * BP + row] = v; });
 }
 
-// The end of the single-GPU solve's reduction in one launch: the tau partial sums
-// (k_cr_tau_partial, CR_NCHUNK workgroups), the top block with the tau border (k_cr_top, one
-// workgroup) and every back-substitution level (nblk - 1 workgroups, one per eliminated
-// block). A workgroup takes a ticket at entry; tickets are dealt partials first, then the
-// top, then the back blocks coarse level first, so a workgroup only ever waits for
-// workgroups of lower tickets, which have already started: the grid drains whatever the
-// residency (two 8 BP-thread workgroups per CU). Hand-offs (MI355X_MICROARCH.md, inter-
-// workgroup visibility, first table row / handoff-1to1):
-//  - partials -> top: every element stored with a relaxed agent-scope store (sc1, written
-//    through), every wave's vmcnt(0), a barrier, then one agent-scope add to the counter
-//    bk[1]; the top polls the counter with sc1 loads until it holds CR_NCHUNK x stamp, and
-//    reads the partials with sc1 loads only;
-//  - top / back blocks -> back blocks: the data is the flag (cdna_hip_programming.md §6
-//    Guideline 16, R2): every row of a step and every dtau entry goes out as two 8-byte
-//    granules {stamp, high word} {stamp, low word}, each ONE sc1 store, and each consumer
-//    thread re-reads its granules with sc1 loads until all carry this launch's stamp.
-// Stamps count launches (ticket / nwork + 1; bk[0] the ticket counter, the granules `gdcv`
-// (rows, then 32 x 2 for dtau), all zeroed by fte_setup). The plain dcv / dtau are written
-// too (k_cr_trial of the per-frame-delay mode reads them). A spin that outlives ~0.3 s gives
-// up and counts into *bad (the solve then reports a failed factorisation, not a hang).
-// Folding the partials and the top into this launch removed two kernel boundaries (r03).
+// The end of the single-GPU solve's reduction in one launch: the top block with the tau
+// border (k_cr_top's work, one workgroup) and every back-substitution level (nblk - 1
+// workgroups, one per eliminated block). A workgroup takes a ticket at entry; tickets are
+// dealt top first, then the back blocks coarse level first, so a workgroup only ever waits
+// for workgroups of lower tickets, which have already started: the grid drains whatever the
+// residency (two 8 BP-thread workgroups per CU). The tau partial sums come from the top
+// level's launch (cr_launch_top with_partials: its 64 extra workgroups run beside the top
+// block's elimination). Until r05 they were 64 workgroups of this launch, and the top waited
+// for them behind the W loads of ~450 resident back blocks: 45 us to dtau at 10,000 frames
+// (profiles/r05/back_all_timeline_10k_r05m.log). Hand-off (MI355X_MICROARCH.md, inter-
+// workgroup visibility, first table row / handoff-1to1): the data is the flag
+// (cdna_hip_programming.md §6 Guideline 16, R2): every row of a step and every dtau entry
+// goes out as two 8-byte granules {stamp, high word} {stamp, low word}, each ONE sc1 store,
+// and each consumer thread re-reads its granules with sc1 loads until all carry this
+// launch's stamp. Stamps count launches (ticket / nwork + 1; bk[0] the ticket counter, the
+// granules `gdcv` (rows, then 32 x 2 for dtau), all zeroed by fte_setup). The plain dcv /
+// dtau are written too (k_cr_trial of the per-frame-delay mode reads them). A spin that
+// outlives ~0.3 s gives up and counts into *bad (the solve then reports a failed
+// factorisation, not a hang). Folding the top into this launch removed a kernel boundary (r03).
 __device__ __forceinline__ void cr_publish_granules(unsigned long long* g, unsigned long long stamp, double v) {
   const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
   __hip_atomic_store(g, (stamp << 32) | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2009,7 +2081,7 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(5))) void k
                                                       double* __restrict__ normp, int late_lv) {
   __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32], sdv[CR_MAXBP], s_red[1024];
   __shared__ int s_tk;
-  const int nwork = CR_NCHUNK + d.nblk;  // partials, top, nblk - 1 back blocks
+  const int nwork = d.nblk;  // top, nblk - 1 back blocks
 #ifdef FTE_PROFILE
   const unsigned long long tb_entry = wall_clock64();
   unsigned long long tb_ready = 0;
@@ -2033,40 +2105,13 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(5))) void k
   int w = (int)(tk % (unsigned)nwork);
   const int BP = d.BP;
   unsigned long long* gtau = gdcv + (size_t)d.nblk * BP * 2;
-  unsigned long long* partw = reinterpret_cast<unsigned long long*>(part);
-  if (w < CR_NCHUNK) {
-    const int nE = d.Cg * d.Cg + d.Cg + d.GR * d.GR;
-    cr_tau_partial_chunk(d, st, Hloc, gloc, Tau, 0, d.N, 0, d.nblk, 1, Tc, w, [&](int e, double v) {
-      __hip_atomic_store(partw + (size_t)w * nE + e, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    });
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(bk + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    BACK_TRACE(w, 100);
-    return;
-  }
-  if (w == CR_NCHUNK) {
-    if (threadIdx.x == 0) {
-      const int want = CR_NCHUNK * (int)stamp;
-      const unsigned long long t0 = wall_clock64();
-      while (__hip_atomic_load(bk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-        if (wall_clock64() - t0 > 30000000ull) {
-          atomicAdd(bad, 1);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __syncthreads();
+  if (w == 0) {
+    // the tau border partial sums and the frames' |g| max come from the top level's launch
+    // (cr_launch_top with_partials), without the top block's own Tau term: added last here
     cr_top_body(
-        d, st, Wc, gmaxp, taubuf, dcv, dtau, bad, Xbuf, normp,
-        [&](size_t e) {
-          return __longlong_as_double(
-              (long long)__hip_atomic_load(partw + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        },
+        d, st, Wc, gmaxp, taubuf, dcv, dtau, bad, Xbuf, normp, [&](size_t e) { return part[e]; },
         [&](int c, double v) { cr_publish_granules(gtau + 2 * c, stamp, v); },
-        [&](int r, double v) { cr_publish_granules(gdcv + 2 * r, stamp, v); });
+        [&](int r, double v) { cr_publish_granules(gdcv + 2 * r, stamp, v); }, true, Tau);
     BACK_TRACE(w, 101);
     return;
   }
@@ -2074,7 +2119,7 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(5))) void k
   const int w_tr = w;
   int lv_tr = -1;
 #endif
-  w -= CR_NCHUNK + 1;
+  w -= 1;
   int s = 1, i = 1;
   for (int lv = d.nlev - 1; lv >= 0; --lv) {
     const int sv = 1 << lv, ne = (d.nblk - sv + 2 * sv - 1) / (2 * sv);
@@ -2519,7 +2564,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
                oW = take((size_t)n * BP * (2 * BP + GR)), oTau = take((size_t)n * GR * GR),
                oE2 = take((size_t)n * BP * BP), odL = take((size_t)n * BP * (BP + GR)),
                odR = take((size_t)n * BP * (BP + GR)),
-               odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)),
+               odc = take((size_t)n * BP), odt = take(GR), opart = take((size_t)CR_NCHUNK * (32 * 32 + 32 + 32 * 32 + 1)),
                onp = take(2 * (size_t)n), oTc = take(nlin * N * std::max(tc_stride(d.Cg), 1)), oFm = take(N), oFq = take(N), ost = take(16), oint = take(8),
                ogr = take((size_t)M * P), ogt = take(M), ont = take(2 * (size_t)n),
                obk = take((size_t)n / 2 + 2), ogd = take((size_t)n * BP * 2 + 64);
@@ -2655,7 +2700,8 @@ static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int 
                                        (NB <= 5 ? 2 * (size_t)d.BP + 1 : (size_t)d.BP) * d.BP);
 #define CR_LEVEL(nb)                                                                                               \
   hipLaunchKernelGGL((k_cr_level<nb>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, top, ne, astep, nsplit, \
-                     pend.symmask, pend.lo_s, 0, l0, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
+                     pend.symmask, pend.lo_s, 0, l0, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad, \
+                     CrTauSrc{})
   switch (NB) {
     case 1: CR_LEVEL(1); break;
     case 2: CR_LEVEL(2); break;
@@ -2719,14 +2765,18 @@ static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* 
 // The single surviving block a0 after nlev levels (step sl = 2^nlev): its pending terms,
 // then W_gb = D^-1 GB and Tau = GB^T W_gb on the register-tiled Gauss-Jordan of k_cr_level
 // (top_mode); k_cr_top finishes with the tau border.
+// with_partials: CR_NCHUNK more workgroups form the tau border partial sums and the frames'
+// |g| max (b.part) meanwhile, for k_cr_back_all (the single-GPU chain, a0 = 0)
 static void cr_launch_top(const FteDims& d, hipStream_t s, int nlev, int a0, int iend, const FteState* st,
-                          FteBuffers& b, int* bad, const CrPending& pend) {
+                          FteBuffers& b, int* bad, const CrPending& pend, bool with_partials = false) {
+  const CrTauSrc ts = with_partials ? CrTauSrc{b.Tc, b.gmaxp, b.part} : CrTauSrc{};
+  const int nwg = with_partials ? 1 + CR_NCHUNK : 1;
   const int sl = 1 << nlev, NB = d.BP >> 4;
   const size_t lds = sizeof(double) * (2 * (16 * 17 + 16 * (size_t)d.BP + 17 * (size_t)d.BP) + (size_t)d.BP * d.GR +
                                        (NB <= 5 ? 2 * (size_t)d.BP + 1 : (size_t)d.BP) * d.BP);
 #define CR_TOP(nb)                                                                                                \
-  hipLaunchKernelGGL((k_cr_level<nb>), dim3(1), dim3(1024), lds, s, d, sl, a0, iend, a0, 1, sl, 1, pend.symmask, \
-                     pend.lo_s, 1, 0, st, b.Dc, b.Ec, b.Ec2, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad)
+  hipLaunchKernelGGL((k_cr_level<nb>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, a0, 1, sl, 1, pend.symmask, \
+                     pend.lo_s, 1, 0, st, b.Dc, b.Ec, b.Ec2, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad, ts)
   switch (NB) {
     case 1: CR_TOP(1); break;
     case 2: CR_TOP(2); break;
@@ -2784,8 +2834,8 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   const int bend = d.nblk - 1;
   CrPending pend;
   cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad, false, &pend);
-  cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, pend);
-  // tau partials, the top block and every back-substitution level in one launch, chained by
+  cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, pend, true);
+  // the top block and every back-substitution level in one launch, chained by
   // per-launch stamps (running the top levels' few blocks one after the other inside one
   // workgroup was tried in r03 and took 30 us: one workgroup streams a block's W at ~2 us, so
   // the W loads of every block have to be in flight at once). Constant / no delays: the
@@ -2801,7 +2851,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
     return e ? std::atoi(e) : 30;
   }();
 #define CR_BACK_ALL(nb, grb)                                                                                   \
-  hipLaunchKernelGGL((k_cr_back_all<nb, grb>), dim3(CR_NCHUNK + d.nblk), dim3(nth_back), 0, s, d, bend, b.st,  \
+  hipLaunchKernelGGL((k_cr_back_all<nb, grb>), dim3(d.nblk), dim3(nth_back), 0, s, d, bend, b.st,  \
                      (const double*)b.Wc, (const double*)b.Hloc, (const double*)b.gloc, (const double*)b.Tau,   \
                      (const double*)b.Tc, b.part, (const double*)b.gmaxp, b.tau, b.dtau, b.dcv, b.bk, b.gdcv,    \
                      b.bad, Xt, b.normp, late_lv)

@@ -8,10 +8,11 @@ change of s0 moves x by ~1e-8 two frames later. Tolerances:
     diverges later); the first frame 1e-9.
   * vs the oracle in float64 numerics (same algebra, different summation order and the
     Woodbury form of the update): the same tolerances, first frame 1e-9, marker positions
-    1e-7 m. The 29-state default model runs 18 frames (the reference's own run of that model
-    diverges after frame 17, and so do the GPU and the oracle from each other,
-    profiles/r05/ekf_default_frames.log): its marker positions within north_star's 1e-4 m on
-    all 18, its states at 20x the head tolerances on the first 8.
+    1e-7 m. The 29-state default model runs 18 frames of the 6-camera golden clip (the
+    reference's own run of that model diverges after frame 17, and so do the GPU and the
+    oracle from each other, profiles/r05/ekf_default_frames.log) and 18 frames of a 12-camera
+    ring clip on which it is not sensitive to rounding (RING_SEED): its marker positions within
+    north_star's 1e-4 m on every frame, its states at 20x the head tolerances on the first 8.
   * a batch of sequences = the sequences run one by one, bit for bit.
 """
 import importlib
@@ -143,8 +144,17 @@ def test_core_ekf_dropin_writes_pickle(ctx, tmp_path):
 
 
 # ---- 12-camera ring (configs[4]): the reference's filter generalised to C cameras --------
-def _setup_ring(mode, N, n_cams=12, seed=61):
+# The 29-state default model's ring clip: seed 65, on which a 1e-12 relative change of s0
+# grows to at most 2e-6 m in the marker positions over 18 frames (the oracle's own runs,
+# tools/ekf_seed_scan.py, profiles/r05/ekf_seed_scan.log); on seed 61, the head model's clip,
+# it grows to 3e-4 m, so rounding-level GPU / oracle differences do too. Every clip tried
+# amplifies it past 1e-4 m within 24 frames.
+RING_SEED = {'head': 61, 'default': 65}
+
+
+def _setup_ring(mode, N, n_cams=12, seed=None):
     from acinoset_amd import synth
+    seed = RING_SEED[mode] if seed is None else seed
     scene = synth.ring_scene(n_cams)
     seq = synth.make_sequence(N, scene, mode=mode, seed=seed)
     uv, lik = seq.uv, seq.likelihood
@@ -188,7 +198,7 @@ def test_ekf_12cam_reference_numerics_matches_oracle(ctx, mode, N):
     2.3e-5, smoothed x 6.4e-6 and 9.3e-7 m in the marker positions on this clip), positions
     within 1e-5 m. Default: over its first 10 frames at 1e-3 (as
     test_ekf_matches_reference_default_early_frames)."""
-    scene, seq, s0, cp, covs = _setup_ring(mode, N)
+    scene, seq, s0, cp, covs = _setup_ring(mode, N, seed=61)
     out = cekf.run(seq.uv, seq.likelihood, cp, mode, 90.0, s0, cal_covs=covs, ctx=ctx)
     o = oekf.ekf(seq.uv, seq.likelihood, scene.K, scene.D, scene.R, scene.t, mode, 90.0, s0, 0.5,
                  float(scene.res[0]), ref_numerics=True, cal_covs=covs)
@@ -258,7 +268,7 @@ def test_ekf_analytic_h_rejects_reference_numerics(ctx):
 @pytest.mark.parametrize('mode,N', [('head', 60), ('default', 12)])
 def test_ekf_parallel_gains_match_sequential_smoother(ctx, mode, N):
     """The RTS pass without covariances (per-(sequence, frame) gains: k_ekf_gain_w for the
-    18-state head model, k_ekf_gain otherwise; the smoothed-state recursion k_ekf_smooth_xs
+    18-state head model, k_ekf_gain_t otherwise; the smoothed-state recursion k_ekf_smooth_xs
     at 18 / 87 states) against the sequential smoother that also forms the smoothed
     covariances (k_ekf_smooth), on the same filter output: the same gains
     (src/core/ekf.py:294) by another solve, so rounding-level agreement."""
@@ -267,6 +277,32 @@ def test_ekf_parallel_gains_match_sequential_smoother(ctx, mode, N):
     b = cekf.run(seq.uv, seq.likelihood, cp, mode, 90.0, s0, ref_numerics=False, cal_covs=covs, covariances=True,
                  ctx=ctx)
     np.testing.assert_array_equal(a['x_est'], b['x_est'])
+    sc = max(1.0, float(np.abs(b['x_smooth']).max()))
+    np.testing.assert_allclose(a['x_smooth'], b['x_smooth'], atol=1e-9 * sc, rtol=0)
+
+
+@pytest.mark.parametrize('indefinite', [False, True])
+def test_ekf_default_gains_tiled_and_pivoted_match_sequential_smoother(ctx, indefinite):
+    """The 87-state gains: k_ekf_gain_t (block elimination on MFMA tiles, taken while every
+    scalar pivot of P_pred is positive) and k_ekf_gain_piv (Gauss-Jordan with partial
+    pivoting, the gains k_ekf_gain_t flags) against the sequential smoother's solve
+    (k_ekf_smooth) on the same filter output, float64. With `indefinite` the process noise
+    of one joint angle is -1, so every P_pred[i+1] has a negative diagonal entry (the oracle
+    run of this setup: min eigenvalue ~ -1 on every frame) and every gain takes the pivoted
+    path."""
+    from acinoset_amd.kinematics import build_table
+    scene, seq, s0, cp, covs = _setup_ring('default', 12)
+    table = build_table('default')
+    P = table.P
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    Q = np.array(cekf.process_covariance(P, 1 / 90.0), np.float64)
+    if indefinite:
+        Q[5, 5] = -1.0
+    args = (90.0, 0.5, float(scene.res[0]), cekf.measurement_std(12, covs), Q, cekf.initial_covariance('default'), s0)
+    a = ctx.ekf_run(table, cams, seq.uv, seq.likelihood, *args, ref_numerics=False)
+    b = ctx.ekf_run(table, cams, seq.uv, seq.likelihood, *args, ref_numerics=False, covariances=True)
+    np.testing.assert_array_equal(a['x_est'], b['x_est'])
+    assert np.isfinite(a['x_smooth']).all()
     sc = max(1.0, float(np.abs(b['x_smooth']).max()))
     np.testing.assert_allclose(a['x_smooth'], b['x_smooth'], atol=1e-9 * sc, rtol=0)
 
