@@ -390,7 +390,11 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
   // (a) one observation per thread: projection, loss, Z_o, r_o; then the fixed-order sums
   double rho = 0.0;
   const int nobs = C * L;
-  for (int ch = 0; ch < nobs; ch += LIN_OCH) {
+  // one chunk's observations (LIN_OCH per chunk); a frame whose observations fit one chunk
+  // (6 cameras x 20 markers) runs it as straight-line code: in the loop, the compiler hoisted
+  // the projection's and the loss's f64 constants into VGPRs ahead of it and spilled them, 80 B
+  // of scratch per thread written back to HBM (205 MB per launch at 10,000 frames)
+  auto obs_chunk = [&](int ch) {
     const int no = min(LIN_OCH, nobs - ch);
     if (tid < no) {
       const int o = ch + tid, c = o / L, l = o - c * L;
@@ -468,6 +472,11 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
       s_qt[(l * C + c) * 3 + i] = z[sym3(i, 0)] * v[0] + z[sym3(i, 1)] * v[1] + z[sym3(i, 2)] * v[2];
     }
     __syncthreads();
+  };
+  if (nobs <= LIN_OCH) {
+    obs_chunk(0);
+  } else {
+    for (int ch = 0; ch < nobs; ch += LIN_OCH) obs_chunk(ch);
   }
 
   LPROF(57);

@@ -211,7 +211,7 @@ def main():
     bytes_launch = wl.n_frames * b_frame
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     iters_mean = rep['iters_sum'] / max(1, rep['n_problems'])
-    traffic, pmc = pmc_per_launch('k_sba_lm', n_pts * _group(C))
+    traffic, pmc = pmc_per_launch('k_sba_lm', n_pts * _lm_group(C, n_pts))
 
     out = {
         'metric': 'frames/sec to SBA convergence, 6-cam x 20-kp (points-only SBA, configs[1])',
@@ -337,6 +337,20 @@ def _group(C):
     return g
 
 
+def _lm_group(K, n_pts, n_cu=256):
+    """Lanes per point of k_sba_lm as run_lm (sba.hip) picks them: nextpow2(K), or in a
+    throughput-bound grid (> 16 waves per CU) groups of three slots per lane where that wastes
+    fewer lanes (K = 12: 4 lanes) - the PMC summary is keyed by the launch's thread count."""
+    g = _group(K)
+    if g > 64:
+        return 64
+    if g > K and (n_pts * g + 63) // 64 > 16 * n_cu:
+        g3 = _group((K + 2) // 3) if (K + 2) // 3 > 1 else 1
+        if 3 * g3 < g:
+            return max(g3, 2)
+    return g
+
+
 def host_cpu():
     """(model name, usable cores): the cores this process may run on, capped by the
     harness's per-GPU CPU share (OMP_NUM_THREADS, 16 on the GPU box) when it is set."""
@@ -458,7 +472,7 @@ def bench_sba_scale(ctx, torch, stream, n_frames=20000, n_cams=12, steps=10):
     L = 20
     bytes_launch = n_frames * (C * L * 17 + 6 * L * 8)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic, pmc = pmc_per_launch('k_sba_lm', n_pts * _group(C))
+    traffic, pmc = pmc_per_launch('k_sba_lm', n_pts * _lm_group(C, n_pts))
     fp64 = sba_fp64_roofline(int(mask.sum()), n_pts, rep['iters_sum'] / max(1, rep['n_problems']), kern_ms, pmc)
     return {'workload': f'sba_points C={C} frames={n_frames} L={L} (configs[4] shape, 1 GPU)',
             'frames_per_s': n_frames / dt, 'ms_per_step': dt * 1e3, 'n_points': int(n_pts),

@@ -11,10 +11,10 @@ rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r['Start_Timestamp']))
 rows = rows[len(rows) * 2 // 3:]
 acc = collections.defaultdict(list)
 for r in rows:
-    n = r['Kernel_Name'].split('(')[0].replace('void ', '')
+    n = r['Kernel_Name'].split('(')[0].replace('void ', '').split('<')[0]
     g = int(r['Grid_Size_X']) // max(int(r['Workgroup_Size_X']), 1)
     acc[(n, g)].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
-nit = max(1, len(acc[('k_fte_linearize', nf)]))
+nit = max(1, len(acc.get(('k_fte_linearize', nf), [])))
 tot = 0.0
 for k, v in sorted(acc.items(), key=lambda kv: -sum(kv[1])):
     tot += sum(v)
