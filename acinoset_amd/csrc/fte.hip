@@ -1095,9 +1095,11 @@ __global__ __launch_bounds__(1024) void k_cr_assemble_build(FteDims d, const dou
     }
     D[e] = dv;
     // E_i is upper triangular (frame distance 3 + ar - ac <= 3, and the distance-3 blocks are
-    // the model term's diagonal): its strictly lower 16 x 16 tiles are not stored; level 0 of
-    // k_cr_level, their only reader, takes them as zeros (cr_reduce's e_upper)
-    if ((r >> 4) <= (c >> 4)) E[e] = ev;
+    // the model term's diagonal): in the single-GPU solve its strictly lower 16 x 16 tiles are
+    // not stored; level 0 of k_cr_level, their only reader there, takes them as zeros
+    // (cr_reduce's e_upper). The frame-window ranks (rdiag set) store every tile: k_dist_pack
+    // copies a chain end's E as it is.
+    if (rdiag || (r >> 4) <= (c >> 4)) E[e] = ev;
   }
   for (int e = tid; e < BP * GR; e += blockDim.x) {
     const int r = e / GR, c = e - (e / GR) * GR;
@@ -2391,11 +2393,14 @@ __device__ __forceinline__ void fte_snapshot(FteState* st, FteState* snap) {
   __hip_atomic_store(reinterpret_cast<int*>(snap + 2), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(256) void k_fte_lm(FteDims d, FteState* __restrict__ st, FteOptsDev o, int init,
+// one workgroup of FTE_LM_THREADS: the per-frame cost partials and per-block norm partials summed
+// in a fixed order (256 threads took 16 us at 10,000 frames: 40 strided terms per thread)
+#define FTE_LM_THREADS 1024
+__global__ __launch_bounds__(FTE_LM_THREADS) void k_fte_lm(FteDims d, FteState* __restrict__ st, FteOptsDev o, int init,
                                                 const double* __restrict__ Fm, const double* __restrict__ Fq,
                                                 const double* __restrict__ normp, int spec,
                                                 FteState* __restrict__ snap = nullptr) {
-  __shared__ double s_red[4 * 256];
+  __shared__ double s_red[4 * FTE_LM_THREADS];
   const int tid = threadIdx.x;
   // every load is issued before the LM state is read: both copies of the measurement terms
   // (spec: the trial's are in Floc copy cur ^ 1) and the step / state norm partials
@@ -2886,7 +2891,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   // are the trial cost (no separate cost pass)
   hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
                      b.X, b.tau, b.st, 0, 0, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv, b.Tc);
-  hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 0, b.Floc, b.Fq, b.normp, 1, S.snap);
+  hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(FTE_LM_THREADS), 0, s, d, b.st, o, 0, b.Floc, b.Fq, b.normp, 1, S.snap);
 }
 
 // =======================================================================================
@@ -3319,7 +3324,7 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   FteOptsDev o{op.max_iters, op.ftol, op.xtol, op.gtol};
   hipLaunchKernelGGL(k_fte_cost, dim3(d.N), dim3(64), 0, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau, b.qinv,
                      b.st, 0, 0, 0, INT_MAX, b.Fm, b.Fq);
-  hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(256), 0, s, d, b.st, o, 1, b.Fm, b.Fq, b.normp, 0);
+  hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(FTE_LM_THREADS), 0, s, d, b.st, o, 1, b.Fm, b.Fq, b.normp, 0);
   // the linearisation of the initial state (buffer cur = 0); later ones are speculative
   if (op.max_iters > 0)
     hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
