@@ -1,11 +1,12 @@
 #!/bin/bash
 # r05 session U/V: k_fte_linearize changes (U: coalesced transposed Hloc stores, not kept; V: the
-# single-chunk observation phase without the hoisted-constant spills): FTE tests, 10k / 1k
+# single-chunk observation phase without the hoisted-constant spills; X: D stored as upper tiles):
+# FTE tests, 10k / 1k
 # iteration sequence, FTE 10k HBM traffic (PMC, calibrated)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$PWD/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
-TAG=r05v
+TAG=r05x
 step() { local n=$1 l=$2; shift 2; local t0=$(date +%s); timeout -k 10 $l "$@" > $OUT/$n.log 2>&1; local rc=$?;
   echo "[$n] rc=$rc $(( $(date +%s)-t0 ))s"; tail -n ${TAILN:-3} $OUT/$n.log; case $rc in 0|1) ;; *) echo fatal; exit $rc;; esac; }
 step pytest_fte_${TAG} 600 python -u -m pytest tests/test_gpu_fte.py tests/test_gpu_fte_cfg2.py tests/test_gpu_fullsize.py tests/test_gpu_dist.py tests/test_fte_reference.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider
