@@ -431,7 +431,7 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
                                                     double* __restrict__ xpred, double* __restrict__ xest,
                                                     double* __restrict__ Ppred, double* __restrict__ Pest,
                                                     double* __restrict__ scratch, long long* __restrict__ outliers,
-                                                    int* __restrict__ bad, unsigned long long* ekf_prof) {
+                                                    int* __restrict__ bad, [[maybe_unused]] unsigned long long* ekf_prof) {
   const int seq = blockIdx.x;
   const int tid = threadIdx.x, nth = blockDim.x, lane = tid & 63, wave = tid >> 6;
   const int n = d.n, P = d.P, m = d.m, LDP = d.npad + 1, Pp = d.Ppad;
@@ -1137,7 +1137,7 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
                                                       double* __restrict__ xpred, double* __restrict__ xest,
                                                       double* __restrict__ Ppred, double* __restrict__ Pest,
                                                       long long* __restrict__ outliers, int* __restrict__ bad,
-                                                      unsigned long long* ekf_prof) {
+                                                      [[maybe_unused]] unsigned long long* ekf_prof) {
   constexpr int P = PM, n = 3 * PM, LDP = n + 1, NZ1 = n + 1;
   static_assert(n + 1 <= 64 && 2 * P <= 64, "one column per lane");
   const int seq = blockIdx.x;

@@ -2082,9 +2082,8 @@ __device__ __forceinline__ void cr_publish_granules(unsigned long long* g, unsig
 
 template <int NB, int GRB>
 __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(5))) void k_cr_back_all(FteDims d, int bend, FteState* __restrict__ st,
-                                                      const double* __restrict__ Wc, const double* __restrict__ Hloc,
-                                                      const double* __restrict__ gloc, const double* __restrict__ Tau,
-                                                      const double* __restrict__ Tc, double* __restrict__ part,
+                                                      const double* __restrict__ Wc, const double* __restrict__ Tau,
+                                                      const double* __restrict__ part,
                                                       const double* __restrict__ gmaxp, double* __restrict__ taubuf,
                                                       double* __restrict__ dtau, double* __restrict__ dcv,
                                                       int* __restrict__ bk, unsigned long long* __restrict__ gdcv,
@@ -2195,7 +2194,7 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(5))) void k
       s >= (1 << late_lv));
   __syncthreads();
   // constant / no delays: this block's trial state and norms (k_cr_trial's work)
-  if (Xbuf) cr_trial_rows(d, st, i, threadIdx.x < BP ? sdv[threadIdx.x] : 0.0, xpre, dtau, Xbuf, nullptr, normp, false,
+  if (Xbuf) cr_trial_rows(d, st, i, (int)threadIdx.x < BP ? sdv[threadIdx.x] : 0.0, xpre, dtau, Xbuf, nullptr, normp, false,
                           s_red);
   BACK_TRACE(w_tr, lv_tr);
 }
@@ -2866,8 +2865,8 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   }();
 #define CR_BACK_ALL(nb, grb)                                                                                   \
   hipLaunchKernelGGL((k_cr_back_all<nb, grb>), dim3(d.nblk), dim3(nth_back), 0, s, d, bend, b.st,  \
-                     (const double*)b.Wc, (const double*)b.Hloc, (const double*)b.gloc, (const double*)b.Tau,   \
-                     (const double*)b.Tc, b.part, (const double*)b.gmaxp, b.tau, b.dtau, b.dcv, b.bk, b.gdcv,    \
+                     (const double*)b.Wc, (const double*)b.Tau, (const double*)b.part, (const double*)b.gmaxp, \
+                     b.tau, b.dtau, b.dcv, b.bk, b.gdcv,    \
                      b.bad, Xt, b.normp, late_lv)
 #define CR_BACK_ALL_G(nb) \
   if (d.GR <= 16)         \

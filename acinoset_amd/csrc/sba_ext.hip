@@ -275,8 +275,8 @@ __global__ __launch_bounds__(256) void k_ext_solve(ExtDims d, ExtState* __restri
   {  // block max
     s_red[threadIdx.x] = gm;
     __syncthreads();
-    for (int h = blockDim.x / 2; h > 0; h >>= 1) {
-      if (threadIdx.x < h) s_red[threadIdx.x] = fmax(s_red[threadIdx.x], s_red[threadIdx.x + h]);
+    for (int h = (int)blockDim.x / 2; h > 0; h >>= 1) {
+      if ((int)threadIdx.x < h) s_red[threadIdx.x] = fmax(s_red[threadIdx.x], s_red[threadIdx.x + h]);
       __syncthreads();
     }
     if (threadIdx.x == 0 && st->relin) st->gmax = s_red[0];
@@ -416,7 +416,7 @@ __global__ __launch_bounds__(256) void k_ext_lm(ExtDims d, ExtState* __restrict_
   auto bsum = [&](double v) {
     s_red[tid] = v;
     __syncthreads();
-    for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+    for (int h = (int)blockDim.x / 2; h > 0; h >>= 1) {
       if (tid < h) s_red[tid] += s_red[tid + h];
       __syncthreads();
     }
@@ -685,8 +685,8 @@ __global__ __launch_bounds__(256) void k_ext_pack1(ExtDims d, const ExtState* __
     for (int j = 0; j < 3; ++j) gm = fmax(gm, fabs(Vg[(size_t)p * 10 + 6 + j]));
   s_red[threadIdx.x] = gm;
   __syncthreads();
-  for (int h = blockDim.x / 2; h > 0; h >>= 1) {
-    if (threadIdx.x < h) s_red[threadIdx.x] = fmax(s_red[threadIdx.x], s_red[threadIdx.x + h]);
+  for (int h = (int)blockDim.x / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) s_red[threadIdx.x] = fmax(s_red[threadIdx.x], s_red[threadIdx.x + h]);
     __syncthreads();
   }
   if (threadIdx.x == 0) p1[nE + rank] = s_red[0];
@@ -709,8 +709,8 @@ __global__ __launch_bounds__(256) void k_ext_pack3(ExtDims d, const ExtState* __
   s_red[1][threadIdx.x] = b;
   s_red[2][threadIdx.x] = c;
   __syncthreads();
-  for (int h = blockDim.x / 2; h > 0; h >>= 1) {
-    if (threadIdx.x < h)
+  for (int h = (int)blockDim.x / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h)
       for (int k = 0; k < 3; ++k) s_red[k][threadIdx.x] += s_red[k][threadIdx.x + h];
     __syncthreads();
   }
