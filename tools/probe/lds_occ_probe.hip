@@ -40,12 +40,26 @@ void run(unsigned long long* d, double* s, int nwg, int nth = 384) {
   (void)nth;
 }
 
-int main() {
+int main(int argc, char**) {
   const int nwg = 4096;
   unsigned long long* d;
   double* s;
   (void)hipMalloc(&d, 16 * nwg);
   (void)hipMalloc(&s, 8);
+  if (argc > 1) {  // 256-thread workgroups between 24 and 32 KB, launch bound 256 vs 1024
+    run<24, 256>(d, s, nwg, 256);
+    run<24, 1024>(d, s, nwg, 256);
+    run<26, 256>(d, s, nwg, 256);
+    run<26, 1024>(d, s, nwg, 256);
+    run<27, 256>(d, s, nwg, 256);
+    run<27, 1024>(d, s, nwg, 256);
+    run<28, 256>(d, s, nwg, 256);
+    run<28, 1024>(d, s, nwg, 256);
+    run<30, 256>(d, s, nwg, 256);
+    run<30, 1024>(d, s, nwg, 256);
+    run<32, 1024>(d, s, nwg, 256);
+    return 0;
+  }
   run<40, 384>(d, s, nwg);
   run<40, 1024>(d, s, nwg);
   run<54, 384>(d, s, nwg);
