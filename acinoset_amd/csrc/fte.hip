@@ -1244,7 +1244,18 @@ __device__ __forceinline__ void cr_top_border_sums(const FteDims& d, const FteSt
 //   Tau_i = GB_i^T W_gb.
 // Survivors accumulate them lazily: a block applies dR_{j-s/2} + dL_{j+s/2} when it is
 // loaded at the next level (or by an apply workgroup), so a level is one launch.
-template <int NB>
+// E_r staged in LDS beside E_i: room for both coupling copies only up to BP = 80 with one
+// column-block of GB (GR = 16: up to 15 cameras with a constant shutter delay); otherwise
+// E_r is read from global memory (k_cr_level's sEr == nullptr path)
+__host__ __device__ __forceinline__ bool cr_er_lds(int NB, int GR) { return NB <= 5 && GR <= 16; }
+__host__ __device__ __forceinline__ size_t cr_level_lds_doubles(int BP, int GR) {
+  return 2 * (16 * 17 + 16 * (size_t)BP + 17 * (size_t)BP) + (size_t)BP * GR +
+         (cr_er_lds(BP >> 4, GR) ? 2 * (size_t)BP + 1 : (size_t)BP) * BP;
+}
+
+// GB2: the instance for two GB column-blocks (GR = 32, 16 constant delays; the host picks it
+// by d.GR), so the GR = 16 instances carry none of its code
+template <int NB, bool GB2 = false>
 __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int iend, int top, int ne, int astep,
                                                    int nsplit, unsigned symmask, int lo_s, int top_mode, int l0,
                                                    const FteState* __restrict__ st,
@@ -1261,7 +1272,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   // pivot tiles in LDS with row stride 17 doubles: the 16 rows an A fragment reads land on
   // distinct banks
   constexpr int BP = 16 * NB, TS = 17, BUF = 16 * TS + 16 * BP + BP * TS;
-  constexpr bool ER_LDS = NB <= 5;  // room for both coupling copies (BP <= 80)
+  constexpr bool ER_LDS = NB <= 5 && !GB2;  // room for both coupling copies (cr_er_lds)
   const int GR = d.GR, GRB = GR >> 4, WL = 2 * BP + GR, LDD = BP + GR, NBB = 2 * NB + GRB;
   const int hs = s >> 1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
@@ -1329,7 +1340,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
   double* G0 = lds + 2 * BUF;  // GB_i (pending applied), BP x GR, for Tau
   // LDS copies of the coupling blocks (A operands of the Schur terms): E_i (row major BP x
   // BP) and E_r (row stride BP + 1: the 16 rows of a fragment spread over the banks); E_r is
-  // read from global memory when BP = 96 leaves no room
+  // read from global memory when BP = 96 or GR = 32 leaves no room (cr_er_lds)
   double* sEi = G0 + BP * GR;
   double* sEr = ER_LDS && Er ? sEi + BP * BP : nullptr;
   const bool dwave = wave < NB;
@@ -1488,6 +1499,26 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     for (int K = 0; K < NB; ++K)
 #pragma unroll
       for (int q = 0; q < 4; ++q) G0[(K * 16 + lk + 4 * q) * GR + c0 + li] = t[K][q];
+  } else if (GB2 && nsplit > 1 && !dwave && !top_mode) {
+    // Two GB column-blocks (GR = 32: 16 delays) dealt over the nsplit workgroups of a block:
+    // Tau_i = GB_i^T W_gb (below) still reads all of GB_i from G0, so idle wave k (k = 0, 1)
+    // loads GB column-block k when another workgroup owns it, with the owner's loads and
+    // sums (the same bits), into G0 only (cr_nsplit leaves at least GRB idle waves)
+    const int k = wave - NB - (NBB - part + nsplit - 1) / nsplit;
+    if (k >= 0 && k < GRB && (2 * NB + k) % nsplit != part) {
+      const int c0 = k * 16;
+      load_cols(GBc + (size_t)i * BP * GR, GR, c0);
+#pragma unroll 1
+      for (int kk = 0; (lo_s << (kk >> 1)) <= hs; ++kk) {
+        const int sp = lo_s << (kk >> 1);
+        const double* q = (kk & 1) ? qL_at(sp) : qR_at(sp);
+        if (q) sub_cols(q + BP, LDD, c0);
+      }
+#pragma unroll
+      for (int K = 0; K < NB; ++K)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) G0[(K * 16 + lk + 4 * q) * GR + c0 + li] = t[K][q];
+    }
   }
   PROFA(32, 0);
   PROFA(33, NB);
@@ -2688,7 +2719,12 @@ static int cr_nsplit(const FteDims& d, int ne, int ns) {
       want = c;
       break;
     }
-  return std::min(std::max(need, want), NBB);
+  int n = std::min(std::max(need, want), NBB);
+  // two GB column-blocks (GR = 32) over several workgroups: each workgroup's idle column
+  // waves load the GB blocks it does not own (k_cr_level), so keep GRB of them idle
+  const int GRB = d.GR / 16;
+  while (GRB > 1 && n > 1 && n < NBB && 16 - NB - (NBB + n - 1) / n < GRB) ++n;
+  return n;
 }
 
 // Pending-term bookkeeping of one cyclic reduction (k_cr_level): the terms of the levels with
@@ -2709,12 +2745,16 @@ static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int 
   const int NB = d.BP >> 4, NBB = 2 * NB + d.GR / 16;
   const int nsplit = cr_nsplit(d, ne, ns);
   const int nwg = ne * nsplit + ns;
-  const size_t lds = sizeof(double) * (2 * (16 * 17 + 16 * (size_t)d.BP + 17 * (size_t)d.BP) + (size_t)d.BP * d.GR +
-                                       (NB <= 5 ? 2 * (size_t)d.BP + 1 : (size_t)d.BP) * d.BP);
-#define CR_LEVEL(nb)                                                                                               \
-  hipLaunchKernelGGL((k_cr_level<nb>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, top, ne, astep, nsplit, \
-                     pend.symmask, pend.lo_s, 0, l0, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad, \
+  const size_t lds = sizeof(double) * cr_level_lds_doubles(d.BP, d.GR);
+#define CR_LEVEL_(nb, gb2)                                                                                       \
+  hipLaunchKernelGGL((k_cr_level<nb, gb2>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, top, ne, astep, nsplit, \
+                     pend.symmask, pend.lo_s, 0, l0, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad,    \
                      CrTauSrc{})
+#define CR_LEVEL(nb)        \
+  if (d.GR > 16)            \
+    CR_LEVEL_(nb, true);    \
+  else                      \
+    CR_LEVEL_(nb, false)
   switch (NB) {
     case 1: CR_LEVEL(1); break;
     case 2: CR_LEVEL(2); break;
@@ -2724,6 +2764,7 @@ static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int 
     default: CR_LEVEL(6); break;
   }
 #undef CR_LEVEL
+#undef CR_LEVEL_
   // the kernel's deep-path test (full tiles)
   const int BPq = d.BP, BUF = 16 * 17 + 16 * BPq + BPq * 17;
   const bool deep = nsplit >= 3 && ((NBB + nsplit - 1) / nsplit) * BPq * 16 <= 2 * BUF;
@@ -2785,11 +2826,15 @@ static void cr_launch_top(const FteDims& d, hipStream_t s, int nlev, int a0, int
   const CrTauSrc ts = with_partials ? CrTauSrc{b.Tc, b.gmaxp, b.part} : CrTauSrc{};
   const int nwg = with_partials ? 1 + CR_NCHUNK : 1;
   const int sl = 1 << nlev, NB = d.BP >> 4;
-  const size_t lds = sizeof(double) * (2 * (16 * 17 + 16 * (size_t)d.BP + 17 * (size_t)d.BP) + (size_t)d.BP * d.GR +
-                                       (NB <= 5 ? 2 * (size_t)d.BP + 1 : (size_t)d.BP) * d.BP);
-#define CR_TOP(nb)                                                                                                \
-  hipLaunchKernelGGL((k_cr_level<nb>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, a0, 1, sl, 1, pend.symmask, \
-                     pend.lo_s, 1, 0, st, b.Dc, b.Ec, b.Ec2, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad, ts)
+  const size_t lds = sizeof(double) * cr_level_lds_doubles(d.BP, d.GR);
+#define CR_TOP_(nb, gb2)                                                                                             \
+  hipLaunchKernelGGL((k_cr_level<nb, gb2>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, a0, 1, sl, 1,           \
+                     pend.symmask, pend.lo_s, 1, 0, st, b.Dc, b.Ec, b.Ec2, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad, ts)
+#define CR_TOP(nb)      \
+  if (d.GR > 16)        \
+    CR_TOP_(nb, true);  \
+  else                  \
+    CR_TOP_(nb, false)
   switch (NB) {
     case 1: CR_TOP(1); break;
     case 2: CR_TOP(2); break;
@@ -2799,6 +2844,7 @@ static void cr_launch_top(const FteDims& d, hipStream_t s, int nlev, int a0, int
     default: CR_TOP(6); break;
   }
 #undef CR_TOP
+#undef CR_TOP_
 }
 
 static void cr_launch_assemble_build(const FteDims& d, hipStream_t s, const FteBuffers& b, int b0 = 0,

@@ -23,8 +23,8 @@ from acinoset_amd import _native, dist, kinematics as pkin, synth
 pytestmark = pytest.mark.gpu
 
 
-def _problem(N, mode='default_nolure', sd=True, inter='vel', seed=2, sd_mode='const'):
-    scene = synth.load_scene_file()
+def _problem(N, mode='default_nolure', sd=True, inter='vel', seed=2, sd_mode='const', n_cams=None):
+    scene = synth.load_scene_file() if n_cams is None else synth.ring_scene(n_cams)
     seq = synth.make_sequence(N, scene, mode=mode, seed=seed, tau_max=0.004 if sd else 0.0)
     w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
     prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter,
@@ -44,6 +44,24 @@ def test_fte_dist_virtual_matches_single(ctx, mode, N, sd, inter, world):
                                intermode=prob.im)
     Xd, td, rd = dist.fte_solve_virtual(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
                                         shutter_delay=sd, intermode=prob.im, world=world)
+    assert rd['iters'] == r1['iters'] and rd['n_accepted'] == r1['n_accepted'], (rd, r1)
+    assert rd['status'] == r1['status'] and rd['n_bad_pivots'] == 0
+    assert abs(rd['cost_after'] - r1['cost_after']) <= 1e-11 * r1['cost_after']
+    np.testing.assert_allclose(Xd, X1, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(td, t1, rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize('n_cams,mode', [(12, 'default_nolure'), (16, 'default_nolure'), (16, 'default')])
+def test_fte_dist_virtual_many_cameras_matches_single(ctx, n_cams, mode):
+    """Frame windows with a ring of 12 / 16 cameras (synth.ring_scene): a tau border of 16
+    constant delays takes two GB column-blocks (GR = 32) in every rank's reduction and in the
+    reduced system; 'default' the 96-row super-blocks. 3 ranks against the single-GPU solve."""
+    prob, cams, X0 = _problem(30, mode, n_cams=n_cams)
+    table = pkin.build_table(mode)
+    X1, t1, r1 = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, intermode=prob.im)
+    assert r1['status_name'] in ('ftol', 'xtol', 'gtol'), r1
+    Xd, td, rd = dist.fte_solve_virtual(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
+                                        intermode=prob.im, world=3)
     assert rd['iters'] == r1['iters'] and rd['n_accepted'] == r1['n_accepted'], (rd, r1)
     assert rd['status'] == r1['status'] and rd['n_bad_pivots'] == 0
     assert abs(rd['cost_after'] - r1['cost_after']) <= 1e-11 * r1['cost_after']

@@ -17,8 +17,8 @@ from acinoset_amd import _native, kinematics as pkin, synth
 pytestmark = pytest.mark.gpu
 
 
-def _problem(N, mode='default_nolure', sd=True, inter='vel', seed=2, tau_max=0.004, sd_mode='const'):
-    scene = synth.load_scene_file()
+def _problem(N, mode='default_nolure', sd=True, inter='vel', seed=2, tau_max=0.004, sd_mode='const', n_cams=None):
+    scene = synth.load_scene_file() if n_cams is None else synth.ring_scene(n_cams)
     seq = synth.make_sequence(N, scene, mode=mode, seed=seed, tau_max=tau_max if sd else 0.0)
     w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
     prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter,
@@ -54,6 +54,7 @@ def test_fte_eval_matches_oracle(ctx, sd, inter):
 
 
 @pytest.mark.parametrize('mode,sd,inter,N', [('default_nolure', True, 'vel', 40), ('head', True, 'vel', 60),
+                                             ('upper_body', True, 'vel', 30),
                                              ('default_nolure', False, 'pos', 30),
                                              ('default_nolure', True, 'acc', 30)])
 def test_fte_solve_matches_oracle(ctx, mode, sd, inter, N):
@@ -203,3 +204,34 @@ def test_fte_rejected_steps_match_oracle(ctx, sd_mode):
     assert float(np.sqrt(np.mean(np.sum((pg - po) ** 2, -1)))) < 1e-4
     np.testing.assert_allclose(tau, to, rtol=0, atol=5e-5)
     np.testing.assert_allclose(rep['cost_after'], info['cost_after'], rtol=1e-6)
+
+
+@pytest.mark.parametrize('n_cams,mode,sd_mode', [(12, 'default_nolure', 'const'), (16, 'default_nolure', 'const'),
+                                                (12, 'default_nolure', 'variable'), (16, 'default', 'const')])
+def test_fte_many_cameras_matches_oracle(ctx, n_cams, mode, sd_mode):
+    """More observations per frame than one aggregation chunk of k_fte_linearize (LIN_OCH =
+    128; 12 and 16 cameras x 20-21 markers = 240-336), so the observation sums run over 2-3
+    chunks. A constant shutter delay per camera gives a tau border of 12 or 16 delays: at 16
+    (FTE_MAXC) the border plus the gradient column is two column-blocks (GR = 32) and
+    k_cr_level reads E_r from global memory (cr_er_lds). 'default' (with the lure, P = 29)
+    takes the 96-row super-blocks (NB = 6). A ring of cameras (synth.ring_scene), solved to
+    convergence, against the oracle at the contract of test_fte_solve_matches_oracle."""
+    N = 20
+    seq, prob, cams = _problem(N, mode=mode, n_cams=n_cams, sd_mode=sd_mode)
+    assert seq.uv.shape[1] == n_cams and n_cams * seq.uv.shape[2] > 128
+    X0 = ofte.initial_state(prob, np.arange(N), seq.pos3d[:, 0, 0])
+    Xo, to, info = ofte.solve(prob, X0)
+    table = pkin.build_table(prob.mode)
+    X, tau, rep = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, sd_mode=sd_mode)
+    assert rep['status_name'] in ('ftol', 'xtol', 'gtol'), rep
+    assert info['status'] in ('ftol', 'xtol', 'gtol'), info
+    assert rep['iters'] == info['iters'], (rep, info)
+    pg = okin.marker_positions(prob.mode, X[2:])
+    po = okin.marker_positions(prob.mode, Xo[2:])
+    rms = float(np.sqrt(np.mean(np.sum((pg - po) ** 2, -1))))
+    assert rms < 1e-6, (rms, rep, info)
+    assert abs(_reproj_rms(prob, X, tau) - _reproj_rms(prob, Xo, to)) < 1e-3
+    np.testing.assert_allclose(tau, to, atol=1e-6)
+    np.testing.assert_allclose(rep['cost_after'], info['cost_after'], rtol=1e-9, atol=1e-9)
+    truth = seq.pos3d[:, 0]
+    assert float(np.sqrt(np.mean(np.sum((pg - truth) ** 2, -1)))) < 0.02
