@@ -188,6 +188,21 @@ def test_ekf_12cam_float64_matches_oracle(ctx, mode, N):
     np.testing.assert_allclose(out['P_est'][:3], o['P_est'][:3], atol=(1e-6 if mode == 'head' else 1e-4) * sc, rtol=0)
 
 
+@pytest.mark.parametrize('n_cams', [24, 32])
+def test_ekf_head_many_cameras_matches_oracle(ctx, n_cams):
+    """Rings of 24 / 32 cameras (the kernel choice and the per-frame observation count grow
+    with the cameras): float64 head model, 30 frames, against the oracle. The marker positions
+    within 1e-6 m (north_star: 1e-4 m; measured 1.3e-7 / 3.7e-7 m, profiles/r05/ekf_manycam_r05.log:
+    the state differences grow with the measurement rows, 3e-6 at 6 cameras to 3e-4 at 32 in
+    the acceleration states), the same outlier count."""
+    scene, seq, s0, cp, covs = _setup_ring('head', 30, n_cams=n_cams)
+    out = cekf.run(seq.uv, seq.likelihood, cp, 'head', 90.0, s0, ref_numerics=False, cal_covs=covs, ctx=ctx)
+    o = oekf.ekf(seq.uv, seq.likelihood, scene.K, scene.D, scene.R, scene.t, 'head', 90.0, s0, 0.5,
+                 float(scene.res[0]), ref_numerics=False, cal_covs=covs)
+    _check_positions('head', len(pkin.get_pose_params('head')), out, o, 1e-6)
+    assert int(out['outliers']) == o['outliers']
+
+
 @pytest.mark.parametrize('mode,N', [('head', 250), ('default', 10)])
 def test_ekf_12cam_reference_numerics_matches_oracle(ctx, mode, N):
     """The reference's float32 state rounding and float32 Jacobian perturbation (the

@@ -100,6 +100,24 @@ def test_sba_ext_synthetic_noiseless_converges(ctx):
     assert rep['n_bad_pivots'] == 0
 
 
+@pytest.mark.parametrize('C', [12, 16])
+def test_sba_ext_many_cameras_matches_oracle(ctx, C):
+    """A ring of 12 / 16 cameras (EXT_MAXC = 16: a 96 x 96 reduced camera system), 0.5 px
+    noise, 20 iterations, against the oracle at test_sba_ext_matches_oracle's tolerances."""
+    K, D, R0, t0, X0, uv, pi, ci = _synthetic(400, C, 11)
+    uv = uv + np.random.default_rng(12).normal(0, 0.5, uv.shape)
+    cams = _native.pack_cameras(K, D, R0, t0)
+    cams_out, X, rb, ra, rep = ctx.sba_extrinsics(cams, uv, pi, ci, X0, ctx.sba_ext_opts(max_iters=20))
+    Xo, Ro, to, info = oext.sba_extrinsics(uv, X0, pi.astype(np.int64), ci.astype(np.int64), K, D.reshape(-1, 4),
+                                           R0, t0, max_iters=20)
+    assert rep['status_name'] == info['status'] and rep['n_bad_pivots'] == 0
+    assert rep['iters'] == info['iters'] and rep['n_accepted'] == info['n_accepted']
+    assert abs(rep['cost_after'] - info['cost_after']) <= 1e-12 * info['cost_after']
+    np.testing.assert_allclose(X, Xo, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(cams_out[:, 8:17].reshape(-1, 3, 3), Ro, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(cams_out[:, 17:20], to.reshape(-1, 3), rtol=0, atol=1e-9)
+
+
 def test_sba_ext_unobserved_point_and_order_invariance(ctx):
     K, D, R0, t0, X0, uv, pi, ci = _synthetic(100, 6, 5)
     X0 = np.vstack([X0, [[0.1, 0.2, 0.3]]])  # point 100 has no observations
