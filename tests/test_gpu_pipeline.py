@@ -87,6 +87,28 @@ def test_pipeline_12cam_head_matches_oracle(ctx, from_sba, ref_numerics):
         assert float(np.sqrt(np.mean(np.sum((pe - seqs[k].pos3d[:, 0, :3]) ** 2, -1)))) < 0.05
 
 
+@pytest.mark.parametrize('n_cams', [24, 40])
+def test_pipeline_many_cameras_matches_oracle(ctx, n_cams):
+    """24- and 40-camera rings (up to 40 observation slots per point: SBA lane groups of 32 / 64
+    lanes; the EKF's per-frame observations grow with the cameras), head model on the SBA
+    points, float64: SBA points 1e-7 m with the same NaN pattern, the EKF's marker positions
+    within 1e-6 m of the oracle's (the state tolerances of the 12-camera test would flag the
+    acceleration states, whose rounding-level differences grow with the measurement rows:
+    profiles/r05/ekf_manycam_r05.log), outliers within 1."""
+    from oracle import kinematics as okin
+    scene, seqs, uv, lik, covs, table, out = _run(ctx, n_cams, 'default_nolure', 'head', 1, 20, True, False)
+    P = table.P
+    pts, s0, o = _oracle(scene, uv[0], lik[0], seqs[0].markers, 'head', 0.5, True, False, covs)
+    g = out['pts'][0]
+    np.testing.assert_array_equal(np.isnan(g), np.isnan(pts))
+    m = ~np.isnan(pts)
+    np.testing.assert_allclose(g[m], pts[m], rtol=0, atol=1e-7)
+    for key in ('x_est', 'x_smooth'):
+        d = np.abs(okin.marker_positions('head', out[key][0][:, :P]) - okin.marker_positions('head', o[key][:, :P]))
+        assert d.max() < 1e-6, (key, d.max())
+    assert abs(int(out['outliers'][0]) - o['outliers']) <= 1
+
+
 def test_pipeline_6cam_default_model_matches_oracle(ctx):
     """The reference's 6-camera scene and its 21-marker 'default' model (identity marker
     map, lure line fit) over the frames before that filter loses the synthetic subject."""
