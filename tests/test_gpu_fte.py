@@ -207,18 +207,21 @@ def test_fte_rejected_steps_match_oracle(ctx, sd_mode):
 
 
 @pytest.mark.parametrize('n_cams,mode,sd_mode', [(12, 'default_nolure', 'const'), (16, 'default_nolure', 'const'),
-                                                (12, 'default_nolure', 'variable'), (16, 'default', 'const')])
+                                                (12, 'default_nolure', 'variable'), (16, 'default', 'const'),
+                                                (16, 'head', 'const'), (16, 'upper_body', 'const')])
 def test_fte_many_cameras_matches_oracle(ctx, n_cams, mode, sd_mode):
     """More observations per frame than one aggregation chunk of k_fte_linearize (LIN_OCH =
     128; 12 and 16 cameras x 20-21 markers = 240-336), so the observation sums run over 2-3
     chunks. A constant shutter delay per camera gives a tau border of 12 or 16 delays: at 16
     (FTE_MAXC) the border plus the gradient column is two column-blocks (GR = 32) and
     k_cr_level reads E_r from global memory (cr_er_lds). 'default' (with the lure, P = 29)
-    takes the 96-row super-blocks (NB = 6). A ring of cameras (synth.ring_scene), solved to
-    convergence, against the oracle at the contract of test_fte_solve_matches_oracle."""
+    takes the 96-row super-blocks (NB = 6); 'head' and 'upper_body' (3 and 7 markers: one
+    chunk) the 32- and 48-row ones (NB = 2, 3), whose deep levels deal one column-block per
+    workgroup. A ring of cameras (synth.ring_scene), solved to convergence, against the
+    oracle at the contract of test_fte_solve_matches_oracle."""
     N = 20
     seq, prob, cams = _problem(N, mode=mode, n_cams=n_cams, sd_mode=sd_mode)
-    assert seq.uv.shape[1] == n_cams and n_cams * seq.uv.shape[2] > 128
+    assert seq.uv.shape[1] == n_cams and (mode in ('head', 'upper_body') or n_cams * seq.uv.shape[2] > 128)
     X0 = ofte.initial_state(prob, np.arange(N), seq.pos3d[:, 0, 0])
     Xo, to, info = ofte.solve(prob, X0)
     table = pkin.build_table(prob.mode)
@@ -233,5 +236,7 @@ def test_fte_many_cameras_matches_oracle(ctx, n_cams, mode, sd_mode):
     assert abs(_reproj_rms(prob, X, tau) - _reproj_rms(prob, Xo, to)) < 1e-3
     np.testing.assert_allclose(tau, to, atol=1e-6)
     np.testing.assert_allclose(rep['cost_after'], info['cost_after'], rtol=1e-9, atol=1e-9)
+    # the fit itself (the oracle's too): within a few cm of the truth (the 3-marker head model
+    # with 16 free delays: 2.6 cm)
     truth = seq.pos3d[:, 0]
-    assert float(np.sqrt(np.mean(np.sum((pg - truth) ** 2, -1)))) < 0.02
+    assert float(np.sqrt(np.mean(np.sum((pg - truth) ** 2, -1)))) < 0.05
