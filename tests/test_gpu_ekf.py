@@ -188,6 +188,27 @@ def test_ekf_12cam_float64_matches_oracle(ctx, mode, N):
     np.testing.assert_allclose(out['P_est'][:3], o['P_est'][:3], atol=(1e-6 if mode == 'head' else 1e-4) * sc, rtol=0)
 
 
+@pytest.mark.parametrize('mode,N', [('head', 1), ('head', 2), ('head', 3), ('default', 1), ('default', 2)])
+def test_ekf_shortest_clips_match_oracle(ctx, mode, N):
+    """Clips of 1-3 frames (no RTS gain at N = 1; one gain at N = 2), 12-camera ring, float64,
+    with and without the smoothed covariances, against the oracle at the tolerances of
+    test_ekf_12cam_float64_matches_oracle (the first state 1e-9; x 5e-5, dx 5e-4, ddx 5e-3,
+    smoothed x 2e-5, x20 for the default model; marker positions 1e-7 / 1e-4 m); the last
+    smoothed state is the last filtered one."""
+    scene, seq, s0, cp, covs = _setup_ring(mode, max(N, 3))
+    uv, lik = seq.uv[:N], seq.likelihood[:N]
+    o = oekf.ekf(uv, lik, scene.K, scene.D, scene.R, scene.t, mode, 90.0, s0, 0.5, float(scene.res[0]),
+                 ref_numerics=False, cal_covs=covs)
+    P = len(pkin.get_pose_params(mode))
+    for cov in (False, True):
+        out = cekf.run(uv, lik, cp, mode, 90.0, s0, ref_numerics=False, cal_covs=covs, covariances=cov, ctx=ctx)
+        assert out['x_est'].shape == o['x_est'].shape and out['x_smooth'].shape == o['x_smooth'].shape
+        _check(out, P, o['x_est'][:, :P], o['x_est'][:, P:2 * P], o['x_est'][:, 2 * P:], o['x_smooth'][:, :P],
+               scale=1.0 if mode == 'head' else DEFAULT_SCALE)
+        _check_positions(mode, P, out, o, 1e-7 if mode == 'head' else DEFAULT_POS_TOL)
+        np.testing.assert_array_equal(out['x_smooth'][-1], out['x_est'][-1])
+
+
 @pytest.mark.parametrize('n_cams', [24, 32])
 def test_ekf_head_many_cameras_matches_oracle(ctx, n_cams):
     """Rings of 24 / 32 cameras (the kernel choice and the per-frame observation count grow

@@ -14,7 +14,9 @@ ctx = _native.Context(0)
 for n_cams, mode, N, sdm in [(6, 'default_nolure', 7, 'const'), (12, 'default_nolure', 7, 'const'),
                              (15, 'default_nolure', 7, 'const'), (16, 'default_nolure', 7, 'const'),
                              (16, 'default_nolure', 7, 'none'), (12, 'default', 7, 'const'),
-                             (16, 'default', 7, 'const'), (16, 'default_nolure', 31, 'const')]:
+                             (16, 'default', 7, 'const'), (16, 'default_nolure', 31, 'const'),
+                             (16, 'default_nolure', 400, 'const'), (12, 'default_nolure', 400, 'const'),
+                             (16, 'head', 400, 'const'), (16, 'default', 200, 'const')]:
     scene = synth.ring_scene(n_cams) if n_cams != 6 else synth.load_scene_file()
     sd = sdm != 'none'
     seq = synth.make_sequence(N, scene, mode=mode, seed=2, tau_max=0.004 if sd else 0.0)
