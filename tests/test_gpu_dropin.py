@@ -57,9 +57,10 @@ def test_pairwise_triangulation_matches_reference():
     np.testing.assert_allclose(X, g['pair_xyz'], atol=1e-9)
 
 
-def test_triangulate_dense_matches_oracle(ctx):
+@pytest.mark.parametrize('n_cams', [6, 16])
+def test_triangulate_dense_matches_oracle(ctx, n_cams):
     from acinoset_amd import _native
-    scene = synth.load_scene_file()
+    scene = synth.load_scene_file() if n_cams == 6 else synth.ring_scene(n_cams)
     seq = synth.make_sequence(12, scene, seed=9)
     N, C, L, _ = seq.uv.shape
     valid = (seq.likelihood > 0.5)
