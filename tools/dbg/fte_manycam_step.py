@@ -11,17 +11,18 @@ from oracle import fte as ofte  # noqa: E402
 from acinoset_amd import _native, kinematics as pkin, synth  # noqa: E402
 
 ctx = _native.Context(0)
-for n_cams, mode, N, sdm in [(6, 'default_nolure', 7, 'const'), (12, 'default_nolure', 7, 'const'),
+for n_cams, mode, N, sdm, inter in [(16, 'default_nolure', 31, 'const', 'pos'), (16, 'default_nolure', 31, 'const', 'acc'),
+                                    (16, 'default', 31, 'const', 'acc')] + [(*c, 'vel') for c in [(6, 'default_nolure', 7, 'const'), (12, 'default_nolure', 7, 'const'),
                              (15, 'default_nolure', 7, 'const'), (16, 'default_nolure', 7, 'const'),
                              (16, 'default_nolure', 7, 'none'), (12, 'default', 7, 'const'),
                              (16, 'default', 7, 'const'), (16, 'default_nolure', 31, 'const'),
                              (16, 'default_nolure', 400, 'const'), (12, 'default_nolure', 400, 'const'),
-                             (16, 'head', 400, 'const'), (16, 'default', 200, 'const')]:
+                             (16, 'head', 400, 'const'), (16, 'default', 200, 'const')]]:
     scene = synth.ring_scene(n_cams) if n_cams != 6 else synth.load_scene_file()
     sd = sdm != 'none'
     seq = synth.make_sequence(N, scene, mode=mode, seed=2, tau_max=0.004 if sd else 0.0)
     w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
-    prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode='vel',
+    prob = ofte.Problem(mode, seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=sd, intermode=inter,
                         sd_mode='const')
     cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
     X0 = ofte.initial_state(prob, np.arange(N), seq.pos3d[:, 0, 0])
@@ -44,7 +45,7 @@ for n_cams, mode, N, sdm in [(6, 'default_nolure', 7, 'const'), (12, 'default_no
                                     intermode=prob.im, opts=ctx.fte_default_opts(max_iters=1))
         Xo, to, info = ofte.solve(prob, X0, max_iters=1)
         dt = float(np.abs(np.asarray(tau) - np.asarray(to)).max()) if sd else 0.0
-        print(f'C={n_cams:2d} {mode:15s} N={N:2d} sd={sdm:5s}: step |X-Xo| {float(np.abs(X - Xo).max()):.2e} '
+        print(f'C={n_cams:2d} {mode:15s} N={N:3d} sd={sdm:5s} {inter}: step |X-Xo| {float(np.abs(X - Xo).max()):.2e} '
               f'|tau-to| {dt:.2e} bad {rep["n_bad_pivots"]} acc {rep["n_accepted"]}/{info["n_accepted"]} {ev}',
               flush=True)
     except Exception as e:
