@@ -3,7 +3,9 @@
 * SBA observation lists with many observations per point (slot groups of 64 lanes, and
   more slots than lanes: K = 100 takes the 4-slots-per-lane kernel), ragged counts;
 * FTE at the smallest trajectories (N = 2, 3, 4 frames: one or two super-blocks, zero or
-  one cyclic-reduction level) and with two cameras.
+  one cyclic-reduction level) and with two cameras; max_iters = 0; frames without a single
+  observation (zero weights);
+* EKF frames whose likelihoods are all below the threshold (prediction only).
 
 Tolerances as the main parity tests: SBA points 1e-7 m; FTE keypoints 1e-6 m RMS, tau
 1e-6 s, same accept count.
@@ -66,3 +68,63 @@ def test_fte_smallest_trajectories_match_oracle(ctx, N, cams):
     po = okin.marker_positions(prob.mode, Xo[2:])
     assert float(np.sqrt(np.mean(np.sum((pg - po) ** 2, -1)))) < 1e-6
     np.testing.assert_allclose(tau, to, rtol=0, atol=1e-6)
+
+
+def _fte20():
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(20, scene, mode='default_nolure', seed=2, tau_max=0.004)
+    w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    return scene, seq, w, cams
+
+
+def test_fte_max_iters_zero_returns_start(ctx):
+    scene, seq, w, cams = _fte20()
+    prob = ofte.Problem('default_nolure', seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=True,
+                        intermode='vel')
+    X0 = ofte.initial_state(prob, np.arange(20), seq.pos3d[:, 0, 0])
+    X, tau, rep = ctx.fte_solve(pkin.build_table('default_nolure'), cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
+                                opts=ctx.fte_default_opts(max_iters=0))
+    Xo, to, info = ofte.solve(prob, X0, max_iters=0)
+    assert rep['status_name'] == info['status'] == 'maxiter' and rep['iters'] == info['iters'] == 0
+    np.testing.assert_array_equal(X, X0)
+    assert abs(rep['cost_after'] - info['cost_after']) <= 1e-12 * info['cost_after']
+
+
+def test_fte_frames_without_observations_match_oracle(ctx):
+    """Two consecutive frames with every weight zero: only the motion model holds them."""
+    scene, seq, w, cams = _fte20()
+    w[5:7] = 0.0
+    prob = ofte.Problem('default_nolure', seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=True,
+                        intermode='vel')
+    X0 = ofte.initial_state(prob, np.arange(20), seq.pos3d[:, 0, 0])
+    X, tau, rep = ctx.fte_solve(pkin.build_table('default_nolure'), cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0)
+    Xo, to, info = ofte.solve(prob, X0)
+    assert rep['status_name'] == info['status'] and rep['iters'] == info['iters'], (rep, info)
+    pg = okin.marker_positions(prob.mode, X[2:])
+    po = okin.marker_positions(prob.mode, Xo[2:])
+    assert float(np.sqrt(np.mean(np.sum((pg - po) ** 2, -1)))) < 1e-6
+    np.testing.assert_allclose(tau, to, rtol=0, atol=1e-6)
+    assert abs(rep['cost_after'] - info['cost_after']) <= 1e-9 * info['cost_after']
+
+
+def test_ekf_frames_below_threshold_match_oracle(ctx):
+    """Frames 3-5 with every likelihood below the threshold (no update, prediction only), head
+    model, 12-camera ring, float64: the 12-camera tolerances of tests/test_gpu_ekf.py."""
+    import importlib
+    from oracle import ekf as oekf
+    from test_gpu_ekf import TOL, _setup_ring
+    cekf = importlib.import_module('acinoset_amd.core.ekf')
+    scene, seq, s0, cp, covs = _setup_ring('head', 12)
+    lik = seq.likelihood.copy()
+    lik[3:6] = 0.0
+    out = cekf.run(seq.uv, lik, cp, 'head', 90.0, s0, ref_numerics=False, cal_covs=covs, ctx=ctx)
+    o = oekf.ekf(seq.uv, lik, scene.K, scene.D, scene.R, scene.t, 'head', 90.0, s0, 0.5, float(scene.res[0]),
+                 ref_numerics=False, cal_covs=covs)
+    P = 6
+    np.testing.assert_allclose(out['x_est'][:, :P], o['x_est'][:, :P], rtol=0, atol=TOL['x'])
+    np.testing.assert_allclose(out['x_est'][:, P:2 * P], o['x_est'][:, P:2 * P], rtol=0, atol=TOL['dx'])
+    np.testing.assert_allclose(out['x_est'][:, 2 * P:], o['x_est'][:, 2 * P:], rtol=0, atol=TOL['ddx'])
+    np.testing.assert_allclose(out['x_smooth'][:, :P], o['x_smooth'][:, :P], rtol=0, atol=TOL['smoothed_x'])
+    assert int(out['outliers']) == o['outliers']
+
