@@ -314,13 +314,21 @@ class HipSbaExtRank:
 
 
 def split_points(pt_idx, n_pts, world):
-    """Contiguous point shards: (per-rank point ranges, per-rank observation ids, local ids)."""
+    """Contiguous point shards: (per-rank point ranges, per-rank observation ids, local ids).
+    Every rank computes every shard, so a shard the rank solve cannot take (no point, or no
+    observation: acs_sba_ext_dist_create needs both) raises the same ValueError on every rank
+    before any collective, instead of one rank failing while the others wait in the
+    all-reduce."""
     pt_idx = np.asarray(pt_idx)
+    if world < 1 or n_pts < world:
+        raise ValueError(f'split_points: {n_pts} points over {world} ranks (each rank needs at least one)')
     bounds = [(n_pts * r) // world for r in range(world + 1)]
     shards = []
     for r in range(world):
         lo, hi = bounds[r], bounds[r + 1]
         obs = np.nonzero((pt_idx >= lo) & (pt_idx < hi))[0]
+        if len(obs) == 0:
+            raise ValueError(f'split_points: rank {r} of {world} (points {lo}..{hi - 1}) has no observation')
         shards.append((lo, hi, obs, pt_idx[obs] - lo))
     return shards
 

@@ -178,6 +178,17 @@ def _ext_ranks(world, max_iters=200):
     return ranks
 
 
+def test_split_points_rejects_empty_shards():
+    """More ranks than points, or a shard whose points have no observation: the same
+    ValueError on every rank (each computes every shard) before any collective."""
+    pi = np.array([0, 0, 1, 2, 2, 4], np.int64)   # point 3 unobserved
+    assert [len(s[2]) for s in dist.split_points(pi, 5, 2)] == [3, 3]
+    with pytest.raises(ValueError, match='each rank needs at least one'):
+        dist.split_points(pi, 5, 8)
+    with pytest.raises(ValueError, match='has no observation'):
+        dist.split_points(pi, 5, 5)          # rank 3 holds point 3 only
+
+
 @pytest.mark.parametrize('world', [2, 3, 7])
 def test_ext_dist_protocol_matches_monolithic(world):
     from oracle import sba_ext as ose
