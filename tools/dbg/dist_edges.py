@@ -15,7 +15,7 @@ ctx = _native.Context(0)
 scene = synth.load_scene_file()
 cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
 table = pkin.build_table('default_nolure')
-for N, world in [(10, 8), (20, 8), (6, 4), (12, 8)]:
+for N, world in [(10, 8), (20, 8), (6, 4), (12, 8), (3, 8), (2, 4), (4, 16)]:
     try:
         seq = synth.make_sequence(N, scene, mode='default_nolure', seed=2, tau_max=0.004)
         w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
