@@ -16,8 +16,10 @@ from test_gpu_ekf import _setup_ring  # noqa: E402
 
 cekf = importlib.import_module('acinoset_amd.core.ekf')
 ctx = _native.Context(0)
-for mode, N, cams in [('head', 30, 6), ('head', 30, 16), ('head', 30, 24), ('head', 30, 32), ('default', 12, 16),
-                      ('default', 12, 24)]:
+CASES = [('head', 30, 6), ('head', 30, 16), ('head', 30, 24), ('head', 30, 32), ('default', 12, 16), ('default', 12, 24)]
+if len(sys.argv) > 1 and sys.argv[1] == 'max':
+    CASES = [('head', 10, 48), ('head', 10, 64), ('default', 4, 48), ('default', 4, 64)]
+for mode, N, cams in CASES:
     try:
         scene, seq, s0, cp, covs = _setup_ring(mode, N, n_cams=cams)
         out = cekf.run(seq.uv, seq.likelihood, cp, mode, 90.0, s0, ref_numerics=False, cal_covs=covs,
