@@ -87,10 +87,9 @@ def test_pipeline_12cam_head_matches_oracle(ctx, from_sba, ref_numerics):
         assert float(np.sqrt(np.mean(np.sum((pe - seqs[k].pos3d[:, 0, :3]) ** 2, -1)))) < 0.05
 
 
-@pytest.mark.parametrize('n_cams', [24, 40])
+@pytest.mark.parametrize('n_cams', [24, 40, 64])
 def test_pipeline_many_cameras_matches_oracle(ctx, n_cams):
-    """24- and 40-camera rings (up to 40 observation slots per point: SBA lane groups of 32 / 64
-    lanes; the EKF's per-frame observations grow with the cameras), head model on the SBA
+    """24-, 40- and 64-camera rings (64: the ABI maximum; SBA lane groups of 32 / 64 lanes; the EKF's per-frame observations grow with the cameras), head model on the SBA
     points, float64: SBA points 1e-7 m with the same NaN pattern, the EKF's marker positions
     within 1e-6 m of the oracle's (the state tolerances of the 12-camera test would flag the
     acceleration states, whose rounding-level differences grow with the measurement rows:
