@@ -1,7 +1,8 @@
 """GPU edge cases at the size limits of the kernels, against the oracle:
 
 * SBA observation lists with many observations per point (slot groups of 64 lanes, and
-  more slots than lanes: K = 100 takes the 4-slots-per-lane kernel), ragged counts;
+  more slots than lanes: K = 100 and the maximum K = 256 take the 4-slots-per-lane kernel),
+  ragged counts;
 * FTE at the smallest trajectories (N = 2, 3, 4 frames: one or two super-blocks, zero or
   one cyclic-reduction level) and with two cameras; max_iters = 0; frames without a single
   observation (zero weights);
@@ -19,7 +20,7 @@ from oracle import fisheye, fte as ofte, kinematics as okin, sba as osba
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('kmax', [40, 100])
+@pytest.mark.parametrize('kmax', [40, 100, 256])
 def test_sba_many_observations_per_point(ctx, kmax):
     scene = synth.load_scene_file()
     C = scene.n_cams
