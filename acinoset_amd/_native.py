@@ -38,7 +38,7 @@ SYMBOLS = (
     'acs_sba_ext_default_opts', 'acs_sba_extrinsics', 'acs_sba_points_dense_io',
     'acs_fte_dist_create', 'acs_fte_dist_init', 'acs_fte_dist_round', 'acs_fte_dist_poll',
     'acs_fte_dist_gather', 'acs_fte_dist_scatter', 'acs_fte_dist_result',
-    'acs_fte_dist_destroy',
+    'acs_fte_dist_destroy', 'acs_fte_dist_reset', 'acs_alloc_events', 'acs_ekf_singular_count',
     'acs_sba_ext_dist_create', 'acs_sba_ext_dist_init', 'acs_sba_ext_dist_round', 'acs_sba_ext_dist_poll',
     'acs_sba_ext_dist_result', 'acs_sba_ext_dist_destroy', 'acs_ekf_run',
     'acs_sba_ekf_pipeline',
@@ -128,7 +128,7 @@ class SbaExtReport(C.Structure):
 
 
 # must equal ACS_ABI_VERSION in include/acinoset_hip.h (checked when the library loads)
-ABI_VERSION = 4
+ABI_VERSION = 5
 _lib = None
 _lock = threading.Lock()
 _P = C.c_void_p
@@ -173,6 +173,9 @@ def _declare(lib):
         'acs_fte_dist_scatter': (C.c_int, [_P, _P]),
         'acs_fte_dist_result': (C.c_int, [_P, _P, _P, C.POINTER(FteReport), u32]),
         'acs_fte_dist_destroy': (C.c_int, [_P]),
+        'acs_fte_dist_reset': (C.c_int, [_P, _P, _P, u32]),
+        'acs_alloc_events': (C.c_int64, []),
+        'acs_ekf_singular_count': (C.c_int, [_P, C.POINTER(i32)]),
         'acs_sba_ext_dist_create': (C.c_int, [_P, _P, i32, _P, _P, _P, i64, _P, i64, C.POINTER(SbaExtOpts), i32, i32,
                                               C.POINTER(_P), C.POINTER(i64), u32]),
         'acs_sba_ext_dist_init': (C.c_int, [_P, _P]),
@@ -194,6 +197,12 @@ def _declare(lib):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+
+
+def alloc_events():
+    """acs_alloc_events: device / pinned-host allocations + frees the library has made in this
+    process (no GPU needed)."""
+    return int(load_library().acs_alloc_events())
 
 
 def load_library():
@@ -419,13 +428,20 @@ class Context:
                     eps=1e-3, jacobian='fd'):
         """acs_ekf_run on device pointers (ACS_DEVICE_PTRS: inputs resident in HBM, outputs
         written there; asynchronous on the context stream, no outliers report): the layouts of
-        ekf_run, every pointer an int (torch data_ptr())."""
+        ekf_run, every pointer an int (torch data_ptr()). Being asynchronous, the call does not
+        check for singular solves itself: read them afterwards with ekf_singular_count()."""
         v = lambda p: C.c_void_p(p) if p else None  # noqa: E731
         self.check(self.lib.acs_ekf_run(self.h, v(ints_p), n_ints, v(reals_p), n_reals, v(cams_p), n_cams, v(meas_p),
                                         v(lik_p), S, N, float(fps), float(thresh), float(max_pixel_err), v(r_std_p),
                                         v(Q_p), v(P0_p), v(s0_p), ekf_numerics_mode(ref_numerics, jacobian),
                                         float(eps), v(x_pred_p), v(x_est_p), v(x_smooth_p), None, None, None,
                                         ACS_DEVICE_PTRS), 'acs_ekf_run')
+
+    def ekf_singular_count(self):
+        """Singular solves of the last EKF enqueue on this context (waits for its stream)."""
+        n = C.c_int32(0)
+        self.check(self.lib.acs_ekf_singular_count(self.h, C.byref(n)), 'acs_ekf_singular_count')
+        return int(n.value)
 
     # ---- configs[4]: SBA + EKF fused ------------------------------------------------
     def sba_ekf_pipeline(self, table, cams, meas, likelihood, obs_markers, fps, thresh, max_pixel_err, r_std_base, Q,

@@ -38,7 +38,19 @@ struct acs_ctx {
   // solve reads the LM status of iteration n while iteration n + 1 runs)
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
+  // device counter of singular solves of the last EKF enqueue (acs_ekf_run / the pipeline);
+  // its own allocation, so that a device-pointer call can be checked after the fact
+  // (acs_ekf_singular_count) whatever the workspace slots did since
+  int* ekf_bad = nullptr;
 };
+
+// Every device / pinned-host allocation and free the library makes goes through these, and
+// counts one event in a process-wide counter (acs_alloc_events): a timed region that reuses its
+// buffers shows no change.
+hipError_t acs_dev_malloc(void** p, size_t bytes);
+hipError_t acs_dev_free(void* p);
+hipError_t acs_host_malloc(void** p, size_t bytes, unsigned flags);
+hipError_t acs_host_free(void* p);
 
 // Coherent pinned host buffer of at least `bytes` (grow-only).
 // Returns nullptr (and sets the error) on failure.

@@ -1,6 +1,29 @@
 // ctx.hip — context lifecycle, workspace, staging, and the small elementwise entry
 // points (projection a1, residual vector a2, redescending loss a9).
+#include <atomic>
+
 #include "common.hpp"
+
+static std::atomic<long long> g_alloc_events{0};
+
+hipError_t acs_dev_malloc(void** p, size_t bytes) {
+  g_alloc_events.fetch_add(1, std::memory_order_relaxed);
+  return hipMalloc(p, bytes);
+}
+hipError_t acs_dev_free(void* p) {
+  if (!p) return hipSuccess;
+  g_alloc_events.fetch_add(1, std::memory_order_relaxed);
+  return hipFree(p);
+}
+hipError_t acs_host_malloc(void** p, size_t bytes, unsigned flags) {
+  g_alloc_events.fetch_add(1, std::memory_order_relaxed);
+  return hipHostMalloc(p, bytes, flags);
+}
+hipError_t acs_host_free(void* p) {
+  if (!p) return hipSuccess;
+  g_alloc_events.fetch_add(1, std::memory_order_relaxed);
+  return hipHostFree(p);
+}
 
 int acs_fail(acs_ctx* ctx, int code, const char* fmt, ...) {
   if (ctx) {
@@ -19,13 +42,13 @@ void* acs_ws(acs_ctx* ctx, int slot, size_t bytes) {
   if (ctx->ws_bytes[slot] >= bytes) return ctx->ws[slot];
   if (ctx->ws[slot]) {
     (void)hipStreamSynchronize(ctx->stream);
-    (void)hipFree(ctx->ws[slot]);
+    (void)acs_dev_free(ctx->ws[slot]);
     ctx->ws[slot] = nullptr;
     ctx->ws_bytes[slot] = 0;
   }
   size_t n = bytes + bytes / 4;  // grow with slack
   n = (n + 255) & ~size_t(255);
-  if (hipMalloc(&ctx->ws[slot], n) != hipSuccess) {
+  if (acs_dev_malloc(&ctx->ws[slot], n) != hipSuccess) {
     ctx->ws[slot] = nullptr;
     acs_fail(ctx, ACS_E_NOMEM, "hipMalloc(%zu) failed for workspace slot %d", n, slot);
     return nullptr;
@@ -38,13 +61,13 @@ void* acs_pinned(acs_ctx* ctx, size_t bytes) {
   if (ctx->pinned_bytes >= bytes) return ctx->pinned;
   if (ctx->pinned) {
     (void)hipStreamSynchronize(ctx->stream);
-    (void)hipHostFree(ctx->pinned);
+    (void)acs_host_free(ctx->pinned);
     ctx->pinned = nullptr;
     ctx->pinned_bytes = 0;
   }
   const size_t n = (bytes + 255) & ~size_t(255);
   // coherent (fine-grained): kernels write their state snapshots straight into it
-  if (hipHostMalloc(&ctx->pinned, n, hipHostMallocCoherent) != hipSuccess) {
+  if (acs_host_malloc(&ctx->pinned, n, hipHostMallocCoherent) != hipSuccess) {
     ctx->pinned = nullptr;
     acs_fail(ctx, ACS_E_NOMEM, "hipHostMalloc(%zu) failed", n);
     return nullptr;
@@ -79,6 +102,8 @@ void* acs_out_buf(acs_ctx* ctx, int slot, void* dst, size_t bytes, uint32_t flag
 extern "C" {
 
 int acs_abi_version(void) { return ACS_ABI_VERSION; }
+
+int64_t acs_alloc_events(void) { return g_alloc_events.load(std::memory_order_relaxed); }
 
 int acs_device_count(int* n) {
   int c = 0;
@@ -122,8 +147,9 @@ int acs_ctx_destroy(acs_ctx* ctx) {
   ACS_DEVICE_GUARD(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (int i = 0; i < WS_NSLOTS; ++i)
-    if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
-  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->ws[i]) (void)acs_dev_free(ctx->ws[i]);
+  if (ctx->pinned) (void)acs_host_free(ctx->pinned);
+  if (ctx->ekf_bad) (void)acs_dev_free(ctx->ekf_bad);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
   return ACS_OK;

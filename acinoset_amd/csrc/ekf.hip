@@ -2002,7 +2002,7 @@ __global__ __launch_bounds__(256) void k_ekf_gain_piv(EkfDims d, const double* _
   double* fcol = M + (size_t)n * LDM;      // n: column k before the step
   int* s_pv = (int*)(fcol + n);            // n: pivot row of step k
   __shared__ unsigned long long s_used[2];
-  __shared__ int s_sing;
+  __shared__ int s_sing, s_skip[2];
   for (int e = tid; e < n * 2 * n; e += nth) {
     const int r = e / (2 * n), c = e - r * 2 * n;
     M[(size_t)r * LDM + c] = c < n ? Pp1[(size_t)r * n + c] : (c - n == r ? 1.0 : 0.0);
@@ -2034,12 +2034,22 @@ __global__ __launch_bounds__(256) void k_ekf_gain_piv(EkfDims d, const double* _
         }
       }
       if (tid == 0) {
+        // no usable pivot (every unused entry of column k zero or NaN): take the first unused
+        // row so that the pivot stays inside the matrix, count the step as singular and skip its
+        // elimination (the host raises the error; the gain's values are then meaningless)
+        const bool sing = !(best > 0.0);
+        if (bi >= n) {
+          bi = 0;
+          while (bi < n - 1 && ((s_used[bi >> 6] >> (bi & 63)) & 1ull)) ++bi;
+        }
         s_pv[k] = bi;
         s_used[bi >> 6] |= 1ull << (bi & 63);
-        if (!(best > 0.0)) s_sing += 1;
+        s_skip[k & 1] = sing ? 1 : 0;
+        if (sing) s_sing += 1;
       }
     }
     __syncthreads();
+    if (s_skip[k & 1]) continue;  // uniform; double-buffered against step k + 1's write
     const int pv = s_pv[k];
     const double p = M[(size_t)pv * LDM + k];
     const double ip = p != 0.0 ? 1.0 / p : 0.0;
@@ -2247,7 +2257,15 @@ int acs_ekf_enqueue(acs_ctx* ctx, int n_ints, int n_reals, const int* hdr, int n
   double *dxp = io.x_pred, *dxe = io.x_est, *dxs = io.x_smooth, *dPe = io.P_est, *dPs = io.P_smooth;
   long long* dout = (long long*)(scr + std::max(scr_f, scr_s));
   io.outliers = dout;
-  int* dbad = (int*)(dout + n_seq);
+  // the singular-solve counter lives in its own context allocation (acs_ekf_singular_count
+  // reads it after a device-pointer call); the scratch word after the outlier counts stays
+  // reserved so the per-gain flags keep their place
+  if (!ctx->ekf_bad) {
+    void* p = nullptr;
+    ACS_HIP(ctx, acs_dev_malloc(&p, 256));
+    ctx->ekf_bad = (int*)p;
+  }
+  int* dbad = ctx->ekf_bad;
   io.bad = dbad;
   ACS_HIP(ctx, hipMemsetAsync(dbad, 0, sizeof(int), s));
   const size_t U = std::max(ekf_wg_fk_doubles(P, Jn, L, d.Ppad), ekf_wg_la_doubles(d.npad, d.Ppad));
@@ -2438,6 +2456,21 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
       for (int q = 0; q < n_seq; ++q) outliers[q] = ho[q];
     ACS_CHECK(ctx, hbad == 0, "ekf: %d singular solve(s) (I + A P_xx in the update or P_pred in a gain)", hbad);
   }
+  return ACS_OK;
+}
+
+// Singular solves of the last EKF enqueue on this context (acs_ekf_run or the pipeline):
+// waits for the stream. A device-pointer call without an outlier report stays asynchronous and
+// does not check the counter itself; this reads it afterwards.
+int acs_ekf_singular_count(acs_ctx* ctx, int32_t* count) {
+  ACS_DEVICE_GUARD(ctx);
+  ACS_CHECK(ctx, count != nullptr, "acs_ekf_singular_count: null count");
+  *count = 0;
+  if (!ctx->ekf_bad) return ACS_OK;
+  int h = 0;
+  ACS_HIP(ctx, hipMemcpyAsync(&h, ctx->ekf_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  ACS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  *count = h;
   return ACS_OK;
 }
 

@@ -2519,6 +2519,17 @@ __global__ __launch_bounds__(256) void k_fte_init_state(double* __restrict__ X, 
   if (i == 0) *bad = 0;
 }
 
+// the LM state of a new solve (acs_fte_dist_create's st0): first round pending, lambda0
+__global__ void k_fte_state_reset(FteState* __restrict__ st, double lam0) {
+  if (threadIdx.x != 0) return;
+  FteState z;
+  memset(&z, 0, sizeof(z));
+  z.lam = lam0;
+  z.relin = 1;
+  z.first = 1;
+  *st = z;
+}
+
 struct FteBuffers {
   int* I;
   double *Rl, *cams, *meas, *w, *qinv, *X, *tau;
@@ -2622,7 +2633,7 @@ static int fte_setup(acs_ctx* ctx, FteSetup& S, const int32_t* skel_ints, int64_
   int rc;
   if (owned) {
     void* p = nullptr;
-    ACS_HIP(ctx, hipMalloc(&p, off * sizeof(double)));
+    ACS_HIP(ctx, acs_dev_malloc(&p, off * sizeof(double)));
     *owned = p;
     arena = (double*)p;
     b.I = (int*)(arena + oI);
@@ -2907,7 +2918,8 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
   // blocks of levels >= late_lv wait for their inputs before loading W (ACS_BACK_LATE_LV; 30: never)
   static const int late_lv = [] {
     const char* e = std::getenv("ACS_BACK_LATE_LV");
-    return e ? std::atoi(e) : 30;
+    const int v = e ? std::atoi(e) : 30;
+    return v < 0 ? 0 : (v > 30 ? 30 : v);  // k_cr_back_all shifts 1 << late_lv
   }();
 #define CR_BACK_ALL(nb, grb)                                                                                   \
   hipLaunchKernelGGL((k_cr_back_all<nb, grb>), dim3(d.nblk), dim3(nth_back), 0, s, d, bend, b.st,  \
@@ -3247,6 +3259,7 @@ struct acs_fte_dist {
   DistLayout Lo;
   FteOptsDev o;
   int R, rank, span, a0, bend, klev;
+  double lam0;  // the LM's initial damping (acs_fte_dist_reset restarts from it)
   int k_lo, k_hi, f_lo, f_hi, b_hi_build, c_lo, c_hi, own_lo, own_hi, out_lo, out_hi;
   // rounds captured as hipGraphs (one graph launch instead of ~60 kernel launches); key =
   // (input payload, output payload, stream): two graphs for the two payload buffers
@@ -3568,13 +3581,14 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
   int rc = fte_setup(ctx, h->S, skel_ints, n_ints, skel_reals, n_reals, cams, n_cams, meas, w, n_frames,
                      shutter_delay, Ts, qinv, sd_mode, intermode, X, tau, op.redesc_a, op.redesc_b, op.redesc_c, flags, &h->own);
   if (rc) {
-    if (h->own) (void)hipFree(h->own);
+    if (h->own) (void)acs_dev_free(h->own);
     delete h;
     return rc;
   }
   const FteDims& d = h->S.d;
   h->R = world;
   h->rank = rank;
+  h->lam0 = op.lambda0;
   h->o = FteOptsDev{op.max_iters, op.ftol, op.xtol, op.gtol};
   // chain length 2^k: smallest k >= 1 with R 2^k >= nblk - 1
   h->klev = 1;
@@ -3615,8 +3629,8 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
                oE2 = take(nb * BP * BP), odL = take(nb * BP * (BP + GR)), odR = take(nb * BP * (BP + GR)),
                op_ = take((size_t)CR_NCHUNK * (16 * 16 + 16 + 32 * 32)), ogm = take(4);
   void* p = nullptr;
-  if (hipMalloc(&p, off * sizeof(double)) != hipSuccess) {
-    (void)hipFree(h->own);
+  if (acs_dev_malloc(&p, off * sizeof(double)) != hipSuccess) {
+    (void)acs_dev_free(h->own);
     delete h;
     return acs_fail(ctx, ACS_E_NOMEM, "fte_dist: reduced-system allocation failed");
   }
@@ -3641,7 +3655,7 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
   st0.first = 1;
   ACS_HIP(ctx, hipMemcpyAsync(h->S.b.st, &st0, sizeof(st0), hipMemcpyHostToDevice, ctx->stream));
   ACS_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  bool snap_ok = hipHostMalloc((void**)&h->snap, sizeof(int32_t) * ACS_DIST_RING, hipHostMallocDefault) == hipSuccess;
+  bool snap_ok = acs_host_malloc((void**)&h->snap, sizeof(int32_t) * ACS_DIST_RING, hipHostMallocDefault) == hipSuccess;
   for (auto& e : h->snap_ev)
     if (snap_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
       e = nullptr;
@@ -3660,6 +3674,40 @@ int acs_fte_dist_create(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, 
   return ACS_OK;
 }
 
+// A solve restarted on the same handle: X / tau from the caller (host or, with
+// ACS_DEVICE_PTRS, device pointers; tau NULL = zeros), the LM state of acs_fte_dist_create
+// (first round pending, lambda0), the back-substitution tickets and granules zeroed. The
+// arena, the reduced-system arrays, the status ring and the captured round graphs are kept:
+// no allocation, so a timed multi-GPU solve can reuse one handle per rank.
+int acs_fte_dist_reset(acs_fte_dist* h, const double* X, const double* tau, uint32_t flags) {
+  ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
+  ACS_CHECK(h ? h->ctx : nullptr, h && X, "fte_dist_reset: null handle or X");
+  acs_ctx* ctx = h->ctx;
+  const FteDims& d = h->S.d;
+  FteBuffers& b = h->S.b;
+  hipStream_t s = ctx->stream;
+  // rounds of the previous solve still queued finish first (their snapshots are then stale)
+  ACS_HIP(ctx, hipStreamSynchronize(s));
+  const double* Xs = X;
+  const double* ts = tau;
+  if (!(flags & ACS_DEVICE_PTRS)) {
+    ACS_HIP(ctx, hipMemcpyAsync(b.X, X, sizeof(double) * d.M * d.P, hipMemcpyHostToDevice, s));
+    if (tau) ACS_HIP(ctx, hipMemcpyAsync(b.tau, tau, sizeof(double) * d.NT, hipMemcpyHostToDevice, s));
+    Xs = b.X;
+    ts = tau ? b.tau : nullptr;
+  }
+  const int n = d.nblk, BP = d.BP, GR = d.GR;
+  const size_t MP = (size_t)d.M * d.P;
+  const size_t ngd = (size_t)n * BP * 2 + 64;
+  const size_t nI = std::max(std::max(std::max(MP, (size_t)n + 1), ngd), (size_t)std::max(d.NT, GR));
+  hipLaunchKernelGGL(k_fte_init_state, dim3(acs_grid((int64_t)nI, 256)), dim3(256), 0, s, b.X, Xs, MP, b.tau, ts,
+                     d.NT, b.bad, b.dtau, GR, b.bk, n + 1, b.gdcv, ngd);
+  hipLaunchKernelGGL(k_fte_state_reset, dim3(1), dim3(64), 0, s, b.st, h->lam0);
+  ACS_HIP(ctx, hipGetLastError());
+  h->rounds = 0;
+  return ACS_OK;
+}
+
 int acs_fte_dist_destroy(acs_fte_dist* h) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   if (!h) return ACS_OK;
@@ -3668,9 +3716,9 @@ int acs_fte_dist_destroy(acs_fte_dist* h) {
     if (c.exec) (void)hipGraphExecDestroy(c.exec);
   for (auto& e : h->snap_ev)
     if (e) (void)hipEventDestroy(e);
-  if (h->snap) (void)hipHostFree(h->snap);
-  if (h->own) (void)hipFree(h->own);
-  if (h->own_red) (void)hipFree(h->own_red);
+  if (h->snap) (void)acs_host_free(h->snap);
+  if (h->own) (void)acs_dev_free(h->own);
+  if (h->own_red) (void)acs_dev_free(h->own_red);
   delete h;
   return ACS_OK;
 }

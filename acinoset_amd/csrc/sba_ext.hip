@@ -889,7 +889,7 @@ int acs_sba_ext_dist_create(acs_ctx* ctx, const double* cams, int32_t n_cams, co
                oPart = take((size_t)h->nchunk * nE), odc = take(96), oSg = take(96 * 96), onp = take(2 * (size_t)n_pts),
                ocn = take(64), ost = take(16), obad = take(2), ouv = take(2 * (size_t)n_pts * K),
                omk = take(((size_t)n_pts * K + 7) / 8), ocid = take(((size_t)n_pts * K + 7) / 8);
-  if (hipMalloc(&h->own, off * sizeof(double)) != hipSuccess) {
+  if (acs_dev_malloc(&h->own, off * sizeof(double)) != hipSuccess) {
     delete h;
     return acs_fail(ctx, ACS_E_NOMEM, "sba_ext_dist: allocation failed");
   }
@@ -924,7 +924,7 @@ int acs_sba_ext_dist_create(acs_ctx* ctx, const double* cams, int32_t n_cams, co
   st0.first = 1;
   ACS_HIP(ctx, hipMemcpyAsync(h->st, &st0, sizeof(st0), hipMemcpyHostToDevice, s));
   ACS_HIP(ctx, hipStreamSynchronize(s));
-  bool snap_ok = hipHostMalloc((void**)&h->snap, sizeof(int32_t) * EXT_DIST_RING, hipHostMallocDefault) == hipSuccess;
+  bool snap_ok = acs_host_malloc((void**)&h->snap, sizeof(int32_t) * EXT_DIST_RING, hipHostMallocDefault) == hipSuccess;
   for (auto& e : h->snap_ev)
     if (snap_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
       e = nullptr;
@@ -948,8 +948,8 @@ int acs_sba_ext_dist_destroy(acs_sba_ext_dist* h) {
   (void)hipStreamSynchronize(h->ctx->stream);
   for (auto& e : h->snap_ev)
     if (e) (void)hipEventDestroy(e);
-  if (h->snap) (void)hipHostFree(h->snap);
-  if (h->own) (void)hipFree(h->own);
+  if (h->snap) (void)acs_host_free(h->snap);
+  if (h->own) (void)acs_dev_free(h->own);
   delete h;
   return ACS_OK;
 }

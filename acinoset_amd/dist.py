@@ -129,6 +129,31 @@ class HipFteRank:
     def _ptr(self, t):
         return C.c_void_p(t.data_ptr())
 
+    def reset(self, X0, tau0=None):
+        """Restart the solve on this handle from X0 ((N + 2, P)) and tau0 (None = zeros): host
+        arrays, or torch device tensors on the context's device (ACS_DEVICE_PTRS). No
+        allocation: the arena, payloads and captured round graphs are reused
+        (acs_fte_dist_reset), so a timed multi-GPU solve creates its ranks once."""
+        torch = self.torch
+        if isinstance(X0, torch.Tensor):
+            for t, n in ((X0, (self.N + 2) * self.P), (tau0, int(np.prod(self.tau_shape)))):
+                if t is None:
+                    continue
+                if (t.device.type != 'cuda' or t.device.index != self.ctx.device or t.dtype != torch.float64
+                        or not t.is_contiguous() or t.numel() != n):
+                    raise ValueError(f'reset: a contiguous float64 cuda:{self.ctx.device} tensor of {n} elements '
+                                     f'expected, got {t.dtype} {tuple(t.shape)} on {t.device}')
+            tp = self._ptr(tau0) if tau0 is not None else None
+            self.ctx.check(self.ctx.lib.acs_fte_dist_reset(self.h, self._ptr(X0), tp, _native.ACS_DEVICE_PTRS),
+                           'acs_fte_dist_reset')
+        else:
+            X = _native._c64(X0).reshape(self.N + 2, self.P)
+            tau = None if tau0 is None else _native._c64(tau0).reshape(self.tau_shape)
+            self.ctx.check(self.ctx.lib.acs_fte_dist_reset(self.h, _native._ptr(X),
+                                                           _native._ptr(tau) if tau is not None else None, 0),
+                           'acs_fte_dist_reset')
+        self.which = 0
+
     def init(self):
         self.which = 0
         self.ctx.check(self.ctx.lib.acs_fte_dist_init(self.h, self._ptr(self.bufs[0])), 'acs_fte_dist_init')
@@ -152,10 +177,18 @@ class HipFteRank:
     def scatter(self, p2):
         self.ctx.check(self.ctx.lib.acs_fte_dist_scatter(self.h, self._ptr(p2)), 'acs_fte_dist_scatter')
 
-    def result(self):
+    def result(self, X_out=None, tau_out=None):
+        """(X, tau, report). With torch device tensors X_out / tau_out the solution is copied
+        into them on the device (ACS_DEVICE_PTRS) and they are returned instead of host arrays."""
+        rep = _native.FteReport()
+        if X_out is not None:
+            self.ctx.check(self.ctx.lib.acs_fte_dist_result(self.h, self._ptr(X_out),
+                                                            self._ptr(tau_out) if tau_out is not None else None,
+                                                            C.byref(rep), _native.ACS_DEVICE_PTRS),
+                           'acs_fte_dist_result')
+            return X_out, tau_out, rep.as_dict()
         X = np.empty((self.N + 2, self.P))
         tau = np.empty(self.tau_shape)
-        rep = _native.FteReport()
         self.ctx.check(self.ctx.lib.acs_fte_dist_result(self.h, _native._ptr(X), _native._ptr(tau), C.byref(rep), 0),
                        'acs_fte_dist_result')
         return X, tau, rep.as_dict()

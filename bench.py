@@ -551,6 +551,9 @@ def bench_ekf(ctx, torch, n_seq, n_frames, n_cams, world, rank, mode='default', 
     dt = (time.perf_counter() - t0) / steps
     gpu_ms = e0.elapsed_time(e1) / steps
     assert np.array_equal(d_xs.cpu().numpy(), out['x_smooth']), 'device-resident EKF differs from the host-array call'
+    # the device-pointer calls do not check for singular solves themselves (asynchronous):
+    # read the last call's counter after the timed region
+    singular = ctx.ekf_singular_count()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -568,6 +571,7 @@ def bench_ekf(ctx, torch, n_seq, n_frames, n_cams, world, rank, mode='default', 
             'inputs': 'device-resident (ACS_DEVICE_PTRS)',
             'us_per_frame_per_seq': dt / n_frames * 1e6, 'scaling': 'weak (replicas)',
             'smoothed_rms_vs_truth_m': rms, 'filter': 'tracks' if rms < 0.05 else 'diverged',
+            'singular_solves_last_call': singular,
             'outliers_frac': float(np.mean(out['outliers'])) / max(1.0, float(np.sum(lik > 0.5)) * 2 / n_seq),
             'numerics': ('reference (float32 state rounding, FD Jacobian eps 1e-3)' if jacobian == 'fd' else
                          'float64, analytic H from the FK Jacobian (SURVEY §8(f)2)'),
@@ -662,12 +666,55 @@ def bench_pipeline(ctx, torch, stream, world, rank, n_seq=80, n_frames=250, n_ca
                                  'order on one CU, so the step is bound by the per-frame update latency, not HBM'}}
 
 
+def fte_iter_profile(frames):
+    """The newest committed per-iteration profile of the FTE at `frames` frames
+    (profiles/r*/fte_iter_<frames/1000>k.json, tools/fte_iter_json.py: rocprofv3 kernel times
+    and the calibrated PMC HBM bytes of one LM iteration, per launch). None if not profiled."""
+    import glob
+    root = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(root, 'profiles', 'r*', f'fte_iter_{frames // 1000}k.json')))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    d['file'] = os.path.relpath(files[-1], root)
+    return d
+
+
+def fte_roofline(n_frames, iters, ms_per_solve, P, C, L, frames_profiled=None):
+    """FP64 roofline of a whole FTE solve with the algorithmic flops of SURVEY.md §8(d) (per
+    frame per GN step: 2 (2CL) P^2 for J^T J + ~80 kflop FK / Jacobian + 6 P^3 banded solve),
+    plus, from the committed profile of one LM iteration at this size, the dominant kernel's
+    share of the iteration and the HBM bytes per iteration against §8(d)'s algorithmic
+    2,872 B per frame (C L (2 b + 1) observations + 4 P b state, b = 8)."""
+    flop_frame = 2 * (2 * C * L) * P * P + 80e3 + 6 * P ** 3
+    tfs = n_frames * iters * flop_frame / (ms_per_solve * 1e-3) / 1e12
+    r = {'bound': 'fp64', 'achieved': tfs, 'peak': FP64_PEAK_TFS, 'unit': 'TFLOP/s', 'frac': tfs / FP64_PEAK_TFS,
+         'flop_per_frame_step': flop_frame, 'note': 'whole solve (all kernels), algorithmic flops of SURVEY.md 8(d)'}
+    prof = fte_iter_profile(n_frames)
+    if prof:
+        alg = n_frames * (C * L * 17 + 4 * P * 8)
+        dom = prof['dominant']
+        r.update({'traffic': prof['hbm_bytes_per_iter'], 'traffic_unit': 'B per LM iteration (PMC, calibrated)',
+                  'algorithmic_bytes_per_iter': alg, 'traffic_vs_algorithmic': prof['hbm_bytes_per_iter'] / alg,
+                  'kernel_us_per_iter': prof['kernel_us_per_iter'],
+                  'dominant_kernel': {'kernel': dom['kernel'], 'share_of_iteration': dom['share'],
+                                      'us_per_iter': dom['us'], 'hbm_bytes_per_iter': dom['hbm_bytes']},
+                  'by_kernel_share': {k: round(v['share'], 4) for k, v in prof['by_kernel'].items()},
+                  'profile_source': prof['file']})
+    return r
+
+
 def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl', steps=3):
     """configs[3]: one FTE trajectory of `n_frames` frames; with W ranks its super-blocks
     are split into W frame windows (acinoset_amd.dist, one all-reduce per LM step over
     RCCL). Strong scaling: the total work is fixed. W = 1 runs acs_fte_solve. Inputs are
-    resident in HBM on every rank before the timed solves (device pointers)."""
+    resident in HBM on every rank before the timed solves (device pointers), and the solution
+    is written to device tensors. A rank's handle is created once, before the timed region,
+    and every timed solve restarts it (acs_fte_dist_reset): the timed region makes no
+    allocation (the library's allocation counter is reported)."""
     import torch.distributed as tdist
+    from acinoset_amd import _native
     from acinoset_amd import dist as adist
     seq, cams, meas, w, X0, table, qinv = _fte_problem(ctx, n_frames)
     import datetime
@@ -680,6 +727,10 @@ def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl',
     d_X = dev['X'].clone()
     d_tau = dev['tau'].clone()
     N, Cn = meas.shape[0], meas.shape[1]
+    r = None
+    if world > 1:
+        r = adist.HipFteRank(ctx, table, cams, meas, w, seq.Ts, qinv, X0, rank=rank, world=world, dev=dev)
+    allreduce = adist.torch_allreduce(group) if world > 1 else None
 
     def run():
         if world == 1:
@@ -689,42 +740,51 @@ def bench_fte_window(ctx, torch, stream, n_frames, world, rank, exchange='nccl',
                                     dev['cams'].data_ptr(), Cn, dev['meas'].data_ptr(), dev['w'].data_ptr(), N, True,
                                     seq.Ts, dev['qinv'].data_ptr(), 1, d_X.data_ptr(), d_tau.data_ptr())
             return d_X, d_tau, rep
-        r = adist.HipFteRank(ctx, table, cams, meas, w, seq.Ts, qinv, X0, rank=rank, world=world, dev=dev)
-        try:
-            adist.lm_loop([r], adist.torch_allreduce(group))
-            return r.result()
-        finally:
-            r.close()
-    X, tau, rep = run()                                             # warm-up + result
-    if world == 1:
+        r.reset(dev['X'], dev['tau'])
+        adist.lm_loop([r], allreduce)
+        return r.result(d_X, d_tau)
+    try:
+        X, tau, rep = run()                                         # warm-up (graphs captured) + result
         X, tau = X.cpu().numpy(), tau.cpu().numpy()
-    pos = ctx.fk(table, X[2:])
-    pos_rms = float(np.sqrt(np.mean(np.sum((pos - seq.pos3d[:, 0]) ** 2, -1))))
+        pos = ctx.fk(table, X[2:])
+        pos_rms = float(np.sqrt(np.mean(np.sum((pos - seq.pos3d[:, 0]) ** 2, -1))))
+        if world > 1:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        a0 = _native.alloc_events()
+        t0 = time.perf_counter()
+        each = []
+        for _ in range(steps):
+            t1 = time.perf_counter()
+            run()                                                   # returns after the solve
+            each.append(time.perf_counter() - t1)
+        torch.cuda.synchronize()
+        if world > 1:
+            tdist.barrier()
+        dt = (time.perf_counter() - t0) / steps
+        allocs = _native.alloc_events() - a0
+    finally:
+        if r is not None:
+            r.close()
     if world > 1:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    each = []
-    for _ in range(steps):
-        t1 = time.perf_counter()
-        run()                                                       # returns after the solve
-        each.append(time.perf_counter() - t1)
-    torch.cuda.synchronize()
-    if world > 1:
-        tdist.barrier()
-    dt = (time.perf_counter() - t0) / steps
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
+        t = torch.tensor([dt, float(allocs)], dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt = float(t.item())
-    return {'workload': f'fte C=6 frames={n_frames} L=20 P={table.P} sd=const intermode=vel (configs[3])',
-            'ranks': world, 'scaling': 'strong', 'frames_per_s': n_frames / dt, 'ms_per_solve': dt * 1e3,
-            'ms_per_solve_each_rank0': [round(e * 1e3, 3) for e in each],
-            'status': rep['status_name'], 'iters': rep['iters'], 'cost_after': rep['cost_after'],
-            'pos_rms_vs_truth_m': pos_rms, 'tau_err_max_s': float(np.abs(tau - seq.tau).max()),
-            'exchange': 'none' if world == 1 else (f'torch.distributed {exchange}: one all-reduce per LM step '
-                                                    '(chain-end reduced system + trial cost, one payload) + the '
-                                                    'solution rows once')}
+        dt, allocs = float(t[0].item()), int(t[1].item())
+    L = table.L
+    out = {'workload': f'fte C={Cn} frames={n_frames} L={L} P={table.P} sd=const intermode=vel (configs[3])',
+           'ranks': world, 'scaling': 'strong', 'frames_per_s': n_frames / dt, 'ms_per_solve': dt * 1e3,
+           'ms_per_solve_each_rank0': [round(e * 1e3, 3) for e in each],
+           'status': rep['status_name'], 'iters': rep['iters'], 'cost_after': rep['cost_after'],
+           'pos_rms_vs_truth_m': pos_rms, 'tau_err_max_s': float(np.abs(tau - seq.tau).max()),
+           'alloc_events_in_timed_region': allocs,
+           'exchange': 'none' if world == 1 else (f'torch.distributed {exchange}: one all-reduce per LM step '
+                                                   '(chain-end reduced system + trial cost, one payload) + the '
+                                                   'solution rows once')}
+    out['roofline'] = fte_roofline(n_frames, rep['iters'], dt * 1e3, table.P, Cn, L)
+    if world > 1:
+        out['roofline'].pop('traffic', None)      # the committed profile is of the single-GPU iteration
+        out['roofline']['note'] += '; per-iteration profile fields are of the single-GPU solve'
+    return out
 
 
 def fte_cpu_baseline(wl):
@@ -782,19 +842,12 @@ def bench_fte(ctx, torch, stream, n_frames=1000, steps=5, cpu=True):
     pos = ctx.fk(table, X[2:])
     pos_rms = float(np.sqrt(np.mean(np.sum((pos - wl.seq.pos3d[:, 0]) ** 2, -1))))
     rms = workloads.fte_reproj_rms(ctx, wl, X, tau)
-    # algorithmic flops per frame per GN step = 2 (2CL) P^2 (J^T J) + ~80 kflop
-    # (FK + Jacobian) + 6 P^3 (banded Cholesky-equivalent solve)
-    P = table.P
-    flop_frame = 2 * (2 * C * L) * P * P + 80e3 + 6 * P ** 3
-    tfs = N * rep['iters'] * flop_frame / dt / 1e12
     out = {'workload': f'fte C={C} frames={N} L={L} P={table.P} sd=const intermode=vel (configs[2])',
            'frames_per_s': N / dt, 'ms_per_solve': dt * 1e3, 'status': rep['status_name'], 'iters': rep['iters'],
            'accepted': rep['n_accepted'], 'cost_before': rep['cost_before'], 'cost_after': rep['cost_after'],
            'reproj_rms_px': rms, 'pos_rms_vs_truth_m': pos_rms,
            'tau_err_max_s': float(np.abs(tau - wl.seq.tau).max()),
-           'roofline': {'bound': 'fp64', 'achieved': tfs, 'peak': FP64_PEAK_TFS, 'unit': 'TFLOP/s',
-                        'frac': tfs / FP64_PEAK_TFS, 'flop_per_frame_step': flop_frame,
-                        'note': 'whole solve (all kernels), algorithmic flops of SURVEY.md 8(d)'}}
+           'roofline': fte_roofline(N, rep['iters'], dt * 1e3, table.P, C, L)}
     if cpu:
         out['cpu_baseline'], (Xo, to, info) = fte_cpu_baseline(wl)
         ro = workloads.fte_reproj_rms(ctx, wl, Xo, to)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ACS_ABI_VERSION 4
+#define ACS_ABI_VERSION 5
 #define ACS_CAM_STRIDE 20
 
 /* status codes */
@@ -91,6 +91,9 @@ int acs_ctx_set_stream(acs_ctx* ctx, void* hip_stream);  /* NULL = context's own
 int acs_ctx_sync(acs_ctx* ctx);
 int acs_abi_version(void);
 int acs_device_count(int* n);
+/* Device and pinned-host allocations + frees the library has made in this process (a
+ * counter; no GPU needed): a timed region that reuses its buffers leaves it unchanged. */
+int64_t acs_alloc_events(void);
 void acs_sba_default_opts(acs_sba_opts* o);
 
 /* ---- a1: fisheye projection (src/lib/calib.py:132-136, src/core/fte.py:80-96) -------
@@ -225,6 +228,11 @@ int acs_fte_dist_gather(acs_fte_dist* h, double* p2);
 int acs_fte_dist_scatter(acs_fte_dist* h, const double* p2);
 int acs_fte_dist_result(acs_fte_dist* h, double* X, double* tau, acs_fte_report* report, uint32_t flags);
 int acs_fte_dist_destroy(acs_fte_dist* h);
+/* A new solve on the same handle from X ((n_frames + 2) x P) and tau (NULL = zeros), host
+ * pointers or ACS_DEVICE_PTRS: the LM restarts as after acs_fte_dist_create (then
+ * acs_fte_dist_init), with no allocation (the arena, payload sizes and captured round graphs
+ * are kept), so a timed multi-GPU solve reuses one handle per rank. */
+int acs_fte_dist_reset(acs_fte_dist* h, const double* X, const double* tau, uint32_t flags);
 
 /* ---- next: fisheye triangulation -------------------------------------
  * acs_triangulate_pairs: triangulate_points_fisheye (src/lib/calib.py:120-129) for n
@@ -308,6 +316,11 @@ int acs_ekf_run(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const do
                 double max_pixel_err, const double* r_std_base, const double* Q, const double* P0,
                 const double* s0, int32_t ref_numerics, double eps, double* x_pred, double* x_est,
                 double* x_smooth, double* P_est, double* P_smooth, int64_t* outliers, uint32_t flags);
+/* Singular solves (I + A P_xx in an update, P_pred in a gain) of the last EKF enqueue on this
+ * context (acs_ekf_run or acs_sba_ekf_pipeline); waits for the context stream. A call that
+ * synchronises anyway (host arrays, or an outlier report) already fails on them; a
+ * device-pointer call without outliers does not check, and this reads the count afterwards. */
+int acs_ekf_singular_count(acs_ctx* ctx, int32_t* count);
 
 /* ---- configs[4]: SBA + EKF fused on one observation tensor ------------------------------
  * core.sba (src/core/sba.py:27-70) and core.ekf (src/core/ekf.py:26-298) of the same

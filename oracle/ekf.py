@@ -134,20 +134,21 @@ def analytic_jacobian(x, mode, K, D, R, t):
 
 
 def ekf(meas, likelihood, K, D, R, t, mode, fps, s0, thresh=0.5, max_pixel_err=2704.0, ref_numerics=True,
-        cal_covs=None, jacobian='fd'):
+        cal_covs=None, jacobian='fd', Q=None, P0=None):
     """meas (N, C, L, 2) pixels (NaN = missing), likelihood (N, C, L). Returns a dict with
     the filtered / predicted / smoothed states and covariances and the outlier count.
     `cal_covs`: per-camera calibration covariances (default: the reference's six, :210;
     the reference asserts six cameras, :213, other rigs pass their own). `jacobian`:
-    'fd' (the reference's forward differences) or 'analytic' (float64 only)."""
+    'fd' (the reference's forward differences) or 'analytic' (float64 only). `Q`, `P0` (test
+    extension): the process noise and initial covariance instead of the reference's (:154-208)."""
     assert jacobian == 'fd' or not ref_numerics, 'the analytic H runs in float64'
     N, C, L, _ = meas.shape
     P = len(POSE[mode])
     n = 3 * P
     sT = 1.0 / fps
     F = transition(P, sT)
-    Q = process_noise(P, sT)
-    Pm = initial_covariance(mode)
+    Q = process_noise(P, sT) if Q is None else np.asarray(Q, np.float64)
+    Pm = initial_covariance(mode) if P0 is None else np.asarray(P0, np.float64)
     covs = CAL_COVS if cal_covs is None else list(cal_covs)
     assert C == len(covs), (C, len(covs))
     base = np.repeat([2 * c / min(covs) for c in covs], 2 * L)

@@ -373,3 +373,76 @@ np.savez({str(tmp_path / 'out.npz')!r}, x_est=b['x_est'], x_smooth=b['x_smooth']
     P = 6
     _check(a, P, b['x_est'][:, :P], b['x_est'][:, P:2 * P], b['x_est'][:, 2 * P:], b['x_smooth'][:, :P])
     assert abs(int(a['outliers']) - int(b['outliers'])) <= 1
+
+
+@pytest.mark.parametrize('where', ['P0', 'Q'])
+def test_ekf_head_indefinite_fallbacks_match_oracle(ctx, where):
+    """The small-state filter's pivoted fallbacks (k_ekf_filter_w1: ekf_w1_pivoted when the
+    SPD certificate of W = P_xx (I + A P_xx) fails; k_ekf_gain_w: the pivoted gain when P_pred
+    is not positive definite), forced on the 12-camera head model in float64: a negative
+    initial variance of one pose parameter (P0) or a negative process noise entry (Q, every
+    frame). Against the oracle, which inverts S and P_pred with np.linalg.inv (pivoted LU),
+    and against the sequential smoother (k_ekf_smooth, covariances=True) on the same filter
+    output. The oracle run itself shows the pose block of P_pred indefinite where the test
+    wants it, so the diagonal-pivot solves cannot have been taken there (Sylvester)."""
+    from acinoset_amd.kinematics import build_table
+    N = 20
+    scene, seq, s0, cp, covs = _setup_ring('head', N)
+    table = build_table('head')
+    P = table.P
+    Q = np.array(cekf.process_covariance(P, 1 / 90.0), np.float64)
+    P0 = np.array(cekf.initial_covariance('head'), np.float64)
+    if where == 'P0':
+        P0[5, 5] = -0.05
+    else:
+        Q[5, 5] = -1e-3
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    args = (90.0, 0.5, float(scene.res[0]), cekf.measurement_std(12, covs), Q, P0, s0)
+    a = ctx.ekf_run(table, cams, seq.uv, seq.likelihood, *args, ref_numerics=False)
+    b = ctx.ekf_run(table, cams, seq.uv, seq.likelihood, *args, ref_numerics=False, covariances=True)
+    o = oekf.ekf(seq.uv, seq.likelihood, scene.K, scene.D, scene.R, scene.t, 'head', 90.0, s0, 0.5,
+                 float(scene.res[0]), ref_numerics=False, cal_covs=covs, Q=Q, P0=P0)
+    # the oracle's own P_pred: the pose block indefinite on the first frame (both cases) and,
+    # with the negative process noise, P_pred not positive definite on most later frames too
+    ev0 = np.linalg.eigvalsh(o['P_pred'][0][:P, :P])
+    assert ev0.min() < 0, ev0
+    if where == 'Q':
+        assert sum(np.linalg.eigvalsh(o['P_pred'][i]).min() < 0 for i in range(1, N)) >= N // 2
+    assert np.isfinite(a['x_est']).all() and np.isfinite(a['x_smooth']).all()
+    np.testing.assert_array_equal(a['x_est'], b['x_est'])
+    sc = max(1.0, float(np.abs(b['x_smooth']).max()))
+    np.testing.assert_allclose(a['x_smooth'], b['x_smooth'], atol=1e-9 * sc, rtol=0)
+    _check(a, P, o['x_est'][:, :P], o['x_est'][:, P:2 * P], o['x_est'][:, 2 * P:], o['x_smooth'][:, :P])
+    _check_positions('head', P, a, o, 1e-6)
+
+
+def test_ekf_singular_count_after_device_call(ctx):
+    """acs_ekf_singular_count: 0 after a regular device-pointer call (which does not check the
+    counter itself), and the count of a host-array call that raised on singular solves."""
+    import torch
+    from acinoset_amd.kinematics import build_table
+    scene, seq, s0, cp, covs = _setup_ring('head', 12)
+    table = build_table('head')
+    P = table.P
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    Q = np.array(cekf.process_covariance(P, 1 / 90.0), np.float64)
+    P0 = np.array(cekf.initial_covariance('head'), np.float64)
+    rstd = cekf.measurement_std(12, covs)
+    dv = torch.device('cuda', ctx.device)
+    T = lambda a, dt=torch.float64: torch.from_numpy(np.ascontiguousarray(a)).to(dv, dt).contiguous()  # noqa
+    d_ints, d_reals = T(table.ints, torch.int32), T(table.reals)
+    d_in = [T(x) for x in (cams, seq.uv, seq.likelihood, rstd, Q, P0, s0[None])]
+    n = 3 * P
+    d_xe = torch.empty((1, 12, n), dtype=torch.float64, device=dv)
+    d_xs = torch.empty_like(d_xe)
+    ctx.ekf_run_dev(d_ints.data_ptr(), d_ints.numel(), d_reals.data_ptr(), d_reals.numel(), d_in[0].data_ptr(), 12,
+                    d_in[1].data_ptr(), d_in[2].data_ptr(), 1, 12, 90.0, 0.5, float(scene.res[0]),
+                    d_in[3].data_ptr(), d_in[4].data_ptr(), d_in[5].data_ptr(), d_in[6].data_ptr(), d_xe.data_ptr(),
+                    d_xs.data_ptr(), ref_numerics=False)
+    assert ctx.ekf_singular_count() == 0
+    # zero process noise and initial covariance: P_pred = 0 in every gain
+    Z = np.zeros_like(Q)
+    with pytest.raises(RuntimeError, match='singular'):
+        ctx.ekf_run(table, cams, seq.uv, seq.likelihood, 90.0, 0.5, float(scene.res[0]), rstd, Z, Z, s0,
+                    ref_numerics=False)
+    assert ctx.ekf_singular_count() > 0

@@ -16,7 +16,7 @@ def _header_functions():
 def test_library_loads_and_exports_header_symbols():
     from acinoset_amd import _native
     lib = _native.load_library()
-    assert lib.acs_abi_version() == _native.ABI_VERSION == 4
+    assert lib.acs_abi_version() == _native.ABI_VERSION == 5
     nm = subprocess.run(['nm', '-D', '--defined-only', _native.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r'\b(acs_[a-z0-9_]+)\b', nm))
     missing = [f for f in _header_functions() if f not in exported]
@@ -41,3 +41,11 @@ def test_kernels_are_gfx950_code_objects():
     from acinoset_amd import _native
     data = open(_native.LIB_PATH, 'rb').read()
     assert b'amdgcn-amd-amdhsa--gfx950' in data
+
+
+def test_alloc_counter_needs_no_gpu():
+    """acs_alloc_events (the allocation counter the bench's timed multi-GPU region is checked
+    with) is callable without a device and never decreases."""
+    from acinoset_amd import _native
+    a = _native.alloc_events()
+    assert a >= 0 and _native.alloc_events() >= a
