@@ -1834,7 +1834,7 @@ __device__ __forceinline__ void block_sum2_lo128(double& a, double& b, double* s
 __device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* st, int i, double dv, double x,
                                               const double* __restrict__ dtau, double* __restrict__ Xbuf,
                                               double* __restrict__ taubuf, double* __restrict__ normp, bool taus,
-                                              double* s_red) {
+                                              double* s_red, bool tau_norm = true) {
   const int P = d.P, e = threadIdx.x, cur = st->cur;
   double dn = 0.0, xn = 0.0;
   if (e < 3 * P) {
@@ -1851,8 +1851,10 @@ __device__ __forceinline__ void cr_trial_rows(const FteDims& d, const FteState* 
     double* taun = taubuf + (cur ^ 1) * d.NT;
     const double t = (e == 0) ? 0.0 : dtau[e];
     taun[e] = (e == 0) ? 0.0 : fmin(fmax(tau[e] + t, -d.Ts), d.Ts);
-    dn += t * t;
-    xn += tau[e] * tau[e];
+    if (tau_norm) {  // the replicated delays count once over the frame-window ranks (rank 0)
+      dn += t * t;
+      xn += tau[e] * tau[e];
+    }
   }
   if (3 * P <= 128 && d.C <= 128 && blockDim.x >= 128) {
     block_sum2_lo128(dn, xn, s_red);
@@ -2230,6 +2232,101 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(5))) void k
   BACK_TRACE(w_tr, lv_tr);
 }
 #undef BACK_TRACE
+
+// A frame-window rank's chain back substitution in one launch (the rank-round counterpart of
+// k_cr_back_all, for the constant / no-delay modes): the chain ends a0 and bend (< nblk) have
+// their step rows from the reduced solve (k_dist_scatter, plain dcv) and dtau from k_cr_top;
+// the interior blocks a0 + s(2m + 1) < min(bend, nblk) are substituted coarse level first,
+// ticket-ordered as k_cr_back_all (a workgroup only waits for lower tickets, which have
+// started), each publishing its rows as {stamp, word} granules; every block, ends included,
+// then forms its trial rows and norm partials (k_cr_trial's work; the replicated delays by
+// block a0's workgroup, their norms counted on rank 0 only). Replaces klev k_cr_back launches
+// and k_cr_trial: the same sums in the same order, so the same bits.
+template <int NB, int GRB>
+__global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(5))) void k_cr_back_chain(
+    FteDims d, int a0, int bend, int klev, int tau_norm, const FteState* __restrict__ st, const double* __restrict__ Wc,
+    const double* __restrict__ dtau, double* __restrict__ dcv, int* __restrict__ bk,
+    unsigned long long* __restrict__ gdcv, int* __restrict__ bad, double* __restrict__ Xbuf,
+    double* __restrict__ taubuf, double* __restrict__ normp) {
+  __shared__ double sl[CR_MAXBP], sr_[CR_MAXBP], st_[32], sdv[CR_MAXBP], s_red[1024];
+  __shared__ int s_tk;
+  const int iend = min(bend, d.nblk), nends = bend < d.nblk ? 2 : 1;
+  int nint = 0;
+  for (int lv = klev - 1; lv >= 0; --lv) {
+    const int sv = 1 << lv;
+    nint += max(0, (iend - a0 - sv + 2 * sv - 1) / (2 * sv));
+  }
+  const int nwork = nends + nint;
+  if (threadIdx.x == 0) s_tk = atomicAdd(bk, 1);
+  __syncthreads();
+  const unsigned tk = (unsigned)s_tk;
+  if (st->status != 0) return;
+  const unsigned long long stamp = tk / (unsigned)nwork + 1u;
+  int w = (int)(tk % (unsigned)nwork);
+  const int BP = d.BP, t = threadIdx.x;
+  if (w < nends) {
+    // a chain end: its rows came from the reduced solve
+    const int e = w == 0 ? a0 : bend;
+    const double xpre = cr_trial_x(d, st, e, Xbuf);
+    const double v = t < BP ? dcv[(size_t)e * BP + t] : 0.0;
+    cr_trial_rows(d, st, e, v, xpre, dtau, Xbuf, taubuf, normp, e == a0 && d.Cg != 0, s_red, tau_norm != 0);
+    return;
+  }
+  w -= nends;
+  int s = 1, i = a0 + 1;
+  for (int lv = klev - 1; lv >= 0; --lv) {
+    const int sv = 1 << lv, ne = max(0, (iend - a0 - sv + 2 * sv - 1) / (2 * sv));
+    if (w < ne) {
+      s = sv;
+      i = a0 + sv * (2 * w + 1);
+      break;
+    }
+    w -= ne;
+  }
+  const double xpre = cr_trial_x(d, st, i, Xbuf);
+  cr_back_block<2 * NB, 2 * GRB>(
+      d, i, s, bend, Wc, sl, sr_, st_,
+      [&](int l, int r) {
+        if (t >= BP && t >= 32) return;
+        const bool wl = t < BP, wr = t < BP && r > 0, wt = t < 32;
+        // a neighbour that is a chain end is read from dcv; an interior one from its granules
+        const bool gl_on = wl && l != a0, gr_on = wr && r != bend;
+        const unsigned long long* gl = gdcv + ((size_t)l * BP + (wl ? t : 0)) * 2;
+        const unsigned long long* gr = gdcv + ((size_t)(r > 0 ? r : l) * BP + (wl ? t : 0)) * 2;
+        const unsigned long long t0 = wall_clock64();
+        unsigned long long a0w = 0, a1w = 0, b0w = 0, b1w = 0;
+        for (;;) {
+          if (gl_on) {
+            a0w = __hip_atomic_load(gl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a1w = __hip_atomic_load(gl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (gr_on) {
+            b0w = __hip_atomic_load(gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            b1w = __hip_atomic_load(gr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          const bool ok = (!gl_on || ((a0w >> 32) == stamp && (a1w >> 32) == stamp)) &&
+                          (!gr_on || ((b0w >> 32) == stamp && (b1w >> 32) == stamp));
+          if (ok) break;
+          if (wall_clock64() - t0 > 30000000ull) {
+            atomicAdd(bad, 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (wl) sl[t] = gl_on ? __hiloint2double((int)(unsigned)a0w, (int)(unsigned)a1w) : dcv[(size_t)l * BP + t];
+        if (wl)
+          sr_[t] = !wr ? 0.0 : (gr_on ? __hiloint2double((int)(unsigned)b0w, (int)(unsigned)b1w) : dcv[(size_t)r * BP + t]);
+        if (wt) st_[t] = t < d.Cg ? dtau[t] : 0.0;
+      },
+      [&](int row, double v) {
+        const size_t e = (size_t)i * BP + row;
+        cr_publish_granules(gdcv + 2 * e, stamp, v);
+        dcv[e] = v;
+        sdv[row] = v;
+      });
+  __syncthreads();
+  cr_trial_rows(d, st, i, t < BP ? sdv[t] : 0.0, xpre, dtau, Xbuf, nullptr, normp, false, s_red);
+}
 
 // trial state X + delta, tau + dtau (clipped), norm partials per super-block. Variable
 // shutter delay: block i back-substitutes the delays of frames 3i-2..3i (X rows 3i..3i+2),
@@ -3783,6 +3880,16 @@ static int dist_phase1_body(acs_fte_dist* h, double* p1) {
   return ACS_OK;
 }
 
+// ACS_DIST_BACK_LEVELS=1: the rank chain's back substitution as one k_cr_back launch per level
+// plus k_cr_trial (the round-5 form, kept for A/B timing); default: k_cr_back_chain
+static bool dist_back_levels() {
+  static const bool v = [] {
+    const char* e = std::getenv("ACS_DIST_BACK_LEVELS");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 static int dist_phase2_body(acs_fte_dist* h, const double* p1) {
   ACS_DEVICE_GUARD(h ? h->ctx : nullptr);
   acs_ctx* ctx = h->ctx;
@@ -3813,7 +3920,37 @@ static int dist_phase2_body(acs_fte_dist* h, const double* p1) {
   // this chain: ends from the reduced solve, interior by back substitution, then the trial
   // rows of the whole chain (its end blocks are shared: both neighbours step them alike) and
   // the replicated delays; the norm partials of the owned blocks go to phase 3's payload
-  if (h->a0 < d.nblk) {
+  if (h->a0 < d.nblk && !d.var && !dist_back_levels()) {
+    hipLaunchKernelGGL(k_dist_scatter, dim3(1), dim3(128), 0, s, d, b.st, h->rank, h->a0, h->bend, r.dcv, b.dcv);
+    // the chain's back substitution and trial rows in one launch (k_cr_back_chain)
+    const int iend = std::min(h->bend, d.nblk);
+    int nint = 0;
+    for (int lv = h->klev - 1; lv >= 0; --lv) {
+      const int sv = 1 << lv;
+      nint += std::max(0, (iend - h->a0 - sv + 2 * sv - 1) / (2 * sv));
+    }
+    const int nwork = (h->bend < d.nblk ? 2 : 1) + nint;
+    const int nth_back = (8 * d.BP + 63) / 64 * 64;
+#define CR_BACK_CHAIN(nb, grb)                                                                                  \
+  hipLaunchKernelGGL((k_cr_back_chain<nb, grb>), dim3(nwork), dim3(nth_back), 0, s, d, h->a0, h->bend, h->klev,  \
+                     h->rank == 0 ? 1 : 0, (const FteState*)b.st, (const double*)b.Wc, (const double*)b.dtau, b.dcv, \
+                     b.bk, b.gdcv, b.bad, b.X, b.tau, b.normp)
+#define CR_BACK_CHAIN_G(nb) \
+  if (d.GR <= 16)           \
+    CR_BACK_CHAIN(nb, 1);   \
+  else                      \
+    CR_BACK_CHAIN(nb, 2)
+    switch (d.BP >> 4) {
+      case 1: CR_BACK_CHAIN_G(1); break;
+      case 2: CR_BACK_CHAIN_G(2); break;
+      case 3: CR_BACK_CHAIN_G(3); break;
+      case 4: CR_BACK_CHAIN_G(4); break;
+      case 5: CR_BACK_CHAIN_G(5); break;
+      default: CR_BACK_CHAIN_G(6); break;
+    }
+#undef CR_BACK_CHAIN_G
+#undef CR_BACK_CHAIN
+  } else if (h->a0 < d.nblk) {
     hipLaunchKernelGGL(k_dist_scatter, dim3(1), dim3(128), 0, s, d, b.st, h->rank, h->a0, h->bend, r.dcv, b.dcv);
     for (int lv = h->klev - 1; lv >= 0; --lv) {
       const int st = 1 << lv;

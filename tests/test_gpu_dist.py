@@ -289,3 +289,43 @@ def test_fte_dist_reset_reuses_handles_without_allocation(ctx):
     assert rc['iters'] == rf['iters'] and rc['n_accepted'] == rf['n_accepted']
     np.testing.assert_array_equal(Xc, Xf)
     np.testing.assert_array_equal(tc, tf)
+
+
+def test_fte_dist_chain_back_launch_equals_per_level_launches(ctx, tmp_path):
+    """k_cr_back_chain (a rank chain's back substitution and trial rows in one launch) against
+    the round-5 form (one k_cr_back launch per level + k_cr_trial, forced by
+    ACS_DIST_BACK_LEVELS=1, read once per process: a child process): 3 and 8 virtual ranks,
+    the same iterations and bit-identical X and tau (same sums in the same order)."""
+    import subprocess
+    import sys
+    prob, cams, X0 = _problem(61, 'head', True, 'acc')
+    table = pkin.build_table('head')
+    ours = {}
+    for world in (3, 8):
+        ours[world] = dist.fte_solve_virtual(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
+                                             intermode=prob.im, world=world)
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = f"""
+import sys, numpy as np
+sys.path.insert(0, {os.path.dirname(here)!r}); sys.path.insert(0, {here!r})
+from test_gpu_dist import _problem
+from acinoset_amd import _native, dist, kinematics as pkin
+ctx = _native.Context(0)
+prob, cams, X0 = _problem(61, 'head', True, 'acc')
+table = pkin.build_table('head')
+out = {{}}
+for world in (3, 8):
+    X, tau, rep = dist.fte_solve_virtual(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0,
+                                         intermode=prob.im, world=world)
+    out[f'X{{world}}'] = X; out[f't{{world}}'] = tau; out[f'i{{world}}'] = rep['iters']
+np.savez({str(tmp_path / 'lv.npz')!r}, **out)
+"""
+    env = dict(os.environ, ACS_DIST_BACK_LEVELS='1')
+    r = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lv = np.load(tmp_path / 'lv.npz')
+    for world in (3, 8):
+        X, tau, rep = ours[world]
+        assert rep['iters'] == int(lv[f'i{world}'])
+        np.testing.assert_array_equal(X, lv[f'X{world}'])
+        np.testing.assert_array_equal(tau, lv[f't{world}'])
