@@ -1386,9 +1386,11 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
             for (int b = 0; b < P; ++b) tv = fma(pxx[a][b], h[b], tv);
             q = fma(h[a], tv, q);
           }
-          // |r| > 3 sqrt(S_rr), S_rr = q + sd^2, compared squared (no sqrt, no division)
+          // |r| > 3 sqrt(S_rr), S_rr = q + sd^2, compared squared (no sqrt, no division); a
+          // negative S_rr (P_xx not positive definite) is no outlier, as the reference's
+          // comparison with sqrt(S_rr) = NaN is false (src/core/ekf.py:272-275)
           const double Srr = q + sd2[r];
-          out = out || sr[r] * sr[r] > 9.0 * Srr;
+          out = out || (Srr >= 0.0 && sr[r] * sr[r] > 9.0 * Srr);
         }
         const unsigned long long bal = __ballot(out);
         if ((tid & 63) == 0) nout += __popcll(bal);

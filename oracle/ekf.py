@@ -173,7 +173,8 @@ def ekf(meas, likelihood, K, D, R, t, mode, fps, s0, thresh=0.5, max_pixel_err=2
         Rm = np.diag(r_std ** 2)
         resid = np.nan_to_num(meas[i].reshape(-1) - h)
         S = H @ Pm @ H.T + Rm
-        tmp = SIGMA_BOUND * np.sqrt(np.diag(S))
+        with np.errstate(invalid='ignore'):  # a negative diag(S) gives NaN: no outlier, as the reference
+            tmp = SIGMA_BOUND * np.sqrt(np.diag(S))
         outliers += int(np.sum((np.abs(resid[0::2]) > tmp[0::2]) | (np.abs(resid[1::2]) > tmp[1::2])))
         Kg = Pm @ H.T @ np.linalg.inv(S)
         s = s + Kg @ resid

@@ -395,7 +395,7 @@ def test_ekf_head_indefinite_fallbacks_match_oracle(ctx, where):
     if where == 'P0':
         P0[5, 5] = -0.05
     else:
-        Q[5, 5] = -1e-3
+        Q[5, 5] = -1.0
     cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
     args = (90.0, 0.5, float(scene.res[0]), cekf.measurement_std(12, covs), Q, P0, s0)
     a = ctx.ekf_run(table, cams, seq.uv, seq.likelihood, *args, ref_numerics=False)
@@ -414,6 +414,9 @@ def test_ekf_head_indefinite_fallbacks_match_oracle(ctx, where):
     np.testing.assert_allclose(a['x_smooth'], b['x_smooth'], atol=1e-9 * sc, rtol=0)
     _check(a, P, o['x_est'][:, :P], o['x_est'][:, P:2 * P], o['x_est'][:, 2 * P:], o['x_smooth'][:, :P])
     _check_positions('head', P, a, o, 1e-6)
+    # the 3-sigma count: a row whose S_rr is negative is no outlier (the reference compares
+    # with sqrt(S_rr) = NaN)
+    assert abs(int(a['outliers']) - o['outliers']) <= 1
 
 
 def test_ekf_singular_count_after_device_call(ctx):
