@@ -146,13 +146,15 @@ class Sequence:
 def make_sequence(n_frames: int, scene: Optional[Scene] = None, mode: str = 'default_nolure',
                   fps: float = 90.0, noise_px: float = 1.0, dropout: float = 0.05,
                   outliers: float = 0.01, tau_max: float = 0.0, speed: Optional[float] = None,
-                  gait_amp: float = 0.2, seed: int = 0) -> Sequence:
-    """Seeded synthetic sequence per SURVEY.md §8(d)."""
+                  gait_amp: float = 0.2, seed: int = 0, drift: float = 1.0) -> Sequence:
+    """Seeded synthetic sequence per SURVEY.md §8(d). `gait_amp` (rad) and `drift` (a factor on
+    the joint angles' random-walk drift) set how far the joints move from zero."""
     scene = scene or load_scene_file()
     idx = get_pose_params(mode)
     markers = get_markers(mode)
     P, L, C, N = len(idx), len(markers), scene.n_cams, n_frames
     Ts = 1.0 / fps
+    drift_scale = drift
     rng0 = np.random.default_rng(seed)
     t = np.arange(N) * Ts
     if speed is None:
@@ -174,8 +176,8 @@ def make_sequence(n_frames: int, scene: Optional[Scene] = None, mode: str = 'def
             continue
         amp = gait_amp if name.startswith('theta_') and int(name.split('_')[1]) >= 6 else 0.25 * gait_amp
         phase = rng0.uniform(0, 2 * np.pi)
-        drift = np.cumsum(rng0.normal(0, 0.05 * np.sqrt(Ts), N))
-        x[:, i] = amp * np.sin(gait + phase) + 0.2 * drift
+        walk = np.cumsum(rng0.normal(0, 0.05 * np.sqrt(Ts), N))
+        x[:, i] = amp * np.sin(gait + phase) + 0.2 * drift_scale * walk
     tau = np.zeros(C)
     if tau_max > 0:
         tau[1:] = rng0.uniform(-tau_max, tau_max, C - 1)
