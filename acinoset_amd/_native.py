@@ -39,6 +39,7 @@ SYMBOLS = (
     'acs_fte_dist_create', 'acs_fte_dist_init', 'acs_fte_dist_round', 'acs_fte_dist_poll',
     'acs_fte_dist_gather', 'acs_fte_dist_scatter', 'acs_fte_dist_result',
     'acs_fte_dist_destroy', 'acs_fte_dist_reset', 'acs_alloc_events', 'acs_ekf_singular_count',
+    'acs_fte_debug_blocks',
     'acs_sba_ext_dist_create', 'acs_sba_ext_dist_init', 'acs_sba_ext_dist_round', 'acs_sba_ext_dist_poll',
     'acs_sba_ext_dist_result', 'acs_sba_ext_dist_destroy', 'acs_ekf_run',
     'acs_sba_ekf_pipeline',
@@ -161,6 +162,8 @@ def _declare(lib):
                                     C.POINTER(FteOpts), C.POINTER(FteReport), u32]),
         'acs_fte_eval': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, dbl, _P, i32, i32, _P, _P,
                                    _P, _P, _P, u32]),
+        'acs_fte_debug_blocks': (C.c_int, [_P, _P, i64, _P, i64, _P, i32, _P, _P, i32, i32, dbl, _P, i32, i32, _P, _P,
+                                           dbl, i32, _P, C.POINTER(i64), u32]),
         'acs_triangulate_pairs': (C.c_int, [_P, _P, i32, _P, _P, _P, _P, i64, _P, u32]),
         'acs_triangulate_dense': (C.c_int, [_P, _P, i32, _P, _P, i64, _P, _P, u32]),
         'acs_sba_ext_default_opts': (None, [C.POINTER(SbaExtOpts)]),
@@ -596,6 +599,27 @@ class Context:
                                          _ptr(H), 0),
                    'acs_fte_eval')
         return cost, grad, H
+
+    def fte_debug_blocks(self, table, cams, meas, w, Ts, qinv, X, tau=None, lam=0.0, levels=0, shutter_delay=True,
+                         intermode=1):
+        """acs_fte_debug_blocks (test hook): the damped super-blocks D (n_blk, BP, BP) of the FTE's
+        block-tridiagonal system at (X, tau), after `levels` cyclic-reduction levels with the
+        pending Schur terms applied (blocks 2^levels m then hold the D the next level factors).
+        Returns (D, levels run)."""
+        ints, reals, cams, meas, w, qinv, N, Cn = self._fte_args(table, cams, meas, w, Ts, qinv, shutter_delay,
+                                                                 intermode)
+        X = _c64(X).reshape(N + 2, table.P)
+        tau = self._tau_init(tau, N, Cn, 0)
+        nblk = (N + 2 + 2) // 3
+        BP = ((3 * table.P + 15) // 16) * 16
+        D = np.empty((nblk, BP, BP))
+        dims = (C.c_int64 * 3)()
+        self.check(self.lib.acs_fte_debug_blocks(self.h, _ptr(ints), len(ints), _ptr(reals), len(reals), _ptr(cams), Cn,
+                                                 _ptr(meas), _ptr(w), N, int(bool(shutter_delay)), float(Ts),
+                                                 _ptr(qinv), 0, int(intermode), _ptr(X), _ptr(tau), float(lam),
+                                                 int(levels), _ptr(D), dims, 0), 'acs_fte_debug_blocks')
+        assert dims[0] == nblk and dims[1] == BP, (list(dims), nblk, BP)
+        return D, int(dims[2])
 
     # ---- triangulation (SURVEY §8f-1) -------------------------------------------------
     def triangulate_pairs(self, cams, uv_a, uv_b, cam_a, cam_b):

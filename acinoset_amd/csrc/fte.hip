@@ -1297,7 +1297,6 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll 1
     for (int k = 0; (lo_s << (k >> 1)) <= hs; ++k) {
       const int sp = lo_s << (k >> 1);
-      const bool sy = (symmask >> (__ffs(sp) - 1)) & 1u;
       const double* pq = (k & 1) ? ((j + sp < iend) ? dL + (size_t)(j + sp) * BP * LDD : nullptr)
                                  : ((j - sp >= a0) ? dR + (size_t)(j - sp) * BP * LDD : nullptr);
       if (!pq) continue;
@@ -1306,8 +1305,11 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
       for (int q = 0; q < NQ; ++q) {
         const int e = tid + 1024 * q;
         const int r = e / LDD, c = e - r * LDD;
-        // D parts of the pending terms hold their upper tiles only (symmetric)
-        const int es = (sy && c < BP && (r >> 4) > (c >> 4)) ? c * LDD + r : e;
+        // D parts of the pending terms are read as their upper triangle, mirrored (the one-wave-
+        // per-column-block levels store upper tiles only, sy; the deep path full tiles, whose
+        // computed lower half is not bitwise the transpose): every D a level factors is then
+        // bitwise symmetric, as the assembled D is
+        const int es = (c < BP && r > c) ? c * LDD + r : e;
         v[q] = e < n ? pq[es] : 0.0;
       }
 #pragma unroll
@@ -1404,17 +1406,19 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
       for (int q = 0; q < 4; ++q) t[K][q] = src[(r0 + lk + 4 * q) * ld + K * 16 + li];
   };
-  // pending D terms of a level that took the one-wave-per-column-block path (its symmask bit) are
-  // stored as upper tiles: tile (r0/16, K) with K < r0/16 is the transpose of tile (K, r0/16);
-  // the deep path writes full tiles (rows read contiguously)
-  auto sub_rows = [&](const double* src, int ld, int r0, bool sy) {
+  // pending D terms are read as their upper triangle, mirrored: element (r, c) with r > c from
+  // (c, r). A level that took the one-wave-per-column-block path (its symmask bit) stores upper
+  // tiles only; the deep path writes full tiles, whose lower half is the computed (not bitwise
+  // transposed) product: the mirror keeps every factored D bitwise symmetric
+  auto sub_rows = [&](const double* src, int ld, int r0, bool /*sy*/) {
     double v[NB][4];
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        v[K][q] = (sy && K * 16 < r0) ? src[(K * 16 + li) * ld + r0 + lk + 4 * q]
-                                      : src[(r0 + lk + 4 * q) * ld + K * 16 + li];
+      for (int q = 0; q < 4; ++q) {
+        const bool lower = K * 16 < r0 || (K * 16 == r0 && li < lk + 4 * q);
+        v[K][q] = lower ? src[(K * 16 + li) * ld + r0 + lk + 4 * q] : src[(r0 + lk + 4 * q) * ld + K * 16 + li];
+      }
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
@@ -1657,6 +1661,9 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
       };
       if (rr < NB) {  // left term E_i^T [W_l | W_gb], output tile I
         if (Jt >= NB && Jt < 2 * NB) continue;
+        // E_i^T W_l is symmetric and read as its upper triangle (sub_rows / the survivors):
+        // its strictly lower tiles are not formed
+        if (Jt < NB && rr > Jt) continue;
         const dbl4 acc = chain([&](int I, int K, int ks) { return sEi[(K * 16 + 4 * ks + lk) * BP + I * 16 + li]; }, rr);
         double* o = dL + (size_t)i * BP * LDD;
 #pragma unroll
@@ -1664,6 +1671,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
       } else if (rr < 2 * NB) {  // right term E_r [W_r | W_gb] and the new coupling -E_r W_l
         if (!Er) continue;
         const int I = rr - NB;
+        if (Jt >= NB && Jt < 2 * NB && I > Jt - NB) continue;  // E_r W_r: upper tiles only (as above)
         const dbl4 acc = sEr ? chain([&](int I_, int K, int ks) { return sEr[(I_ * 16 + li) * (BP + 1) + K * 16 + 4 * ks + lk]; }, I)
                              : chain([&](int I_, int K, int ks) {
                                  return (l0 && K < I_) ? 0.0 : Er[(I_ * 16 + li) * BP + K * 16 + 4 * ks + lk];
@@ -3642,6 +3650,49 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
         }
       }
     }
+  }
+  return ACS_OK;
+}
+
+// Test hook (include/acinoset_hip.h): the damped super-blocks D_i of the normal matrix at
+// (X, tau), as k_cr_assemble_build forms them, after `levels` cyclic-reduction levels of
+// acs_fte_solve's reduction with every pending Schur term applied (levels = 0: as assembled;
+// L > 0: blocks j = 2^L m hold the D the next level factors). Constant / no shutter delay.
+int acs_fte_debug_blocks(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
+                         int64_t n_reals, const double* cams, int32_t n_cams, const double* meas, const double* w,
+                         int32_t n_frames, int32_t shutter_delay, double Ts, const double* qinv, int32_t sd_mode,
+                         int32_t intermode, const double* X, const double* tau, double lam, int32_t levels,
+                         double* D_out, int64_t* dims, uint32_t flags) {
+  ACS_DEVICE_GUARD(ctx);
+  ACS_CHECK(ctx, D_out && levels >= 0, "acs_fte_debug_blocks: null D_out or levels < 0");
+  ACS_CHECK(ctx, !(shutter_delay && sd_mode == 1), "acs_fte_debug_blocks: constant or no shutter delay only");
+  FteSetup S;
+  int rc;
+  if ((rc = fte_setup(ctx, S, skel_ints, n_ints, skel_reals, n_reals, cams, n_cams, meas, w, n_frames, shutter_delay,
+                      Ts, qinv, sd_mode, intermode, X, tau, 3.0, 10.0, 20.0, flags)))
+    return rc;
+  const FteDims& d = S.d;
+  FteBuffers& b = S.b;
+  hipStream_t s = ctx->stream;
+  FteState st0;
+  std::memset(&st0, 0, sizeof(st0));
+  st0.lam = lam;
+  st0.relin = 1;
+  ACS_HIP(ctx, hipMemcpyAsync(b.st, &st0, sizeof(st0), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
+                     b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr, b.Tc);
+  cr_launch_assemble_build(d, s, b);
+  const int L = std::min((int)levels, d.nlev);
+  if (L > 0) cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, L, b.bad, true);
+  ACS_HIP(ctx, hipGetLastError());
+  const size_t bytes = sizeof(double) * (size_t)d.nblk * d.BP * d.BP;
+  ACS_HIP(ctx, hipMemcpyAsync(D_out, b.Dc, bytes, (flags & ACS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice
+                                                                            : hipMemcpyDeviceToHost, s));
+  ACS_HIP(ctx, hipStreamSynchronize(s));
+  if (dims) {
+    dims[0] = d.nblk;
+    dims[1] = d.BP;
+    dims[2] = L;
   }
   return ACS_OK;
 }

@@ -188,6 +188,17 @@ int acs_fte_eval(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const d
                  const double* w, int32_t n_frames, int32_t shutter_delay, double Ts,
                  const double* qinv, int32_t sd_mode, int32_t intermode, const double* X,
                  const double* tau, double* cost3, double* grad, double* H, uint32_t flags);
+/* Test hook: the damped 3-frame super-blocks D_i (n_blk x BP x BP, BP = 3P padded to 16) of
+ * acs_fte_solve's block-tridiagonal system at (X, tau) with damping lam, after `levels`
+ * cyclic-reduction levels with every pending Schur term applied (0: as assembled; L > 0:
+ * blocks 2^L m hold the D the next level factors). dims = {n_blk, BP, levels run}. Constant
+ * or no shutter delay; host pointers, or ACS_DEVICE_PTRS for every array. */
+int acs_fte_debug_blocks(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const double* skel_reals,
+                         int64_t n_reals, const double* cams, int32_t n_cams, const double* meas,
+                         const double* w, int32_t n_frames, int32_t shutter_delay, double Ts,
+                         const double* qinv, int32_t sd_mode, int32_t intermode, const double* X,
+                         const double* tau, double lam, int32_t levels, double* D_out, int64_t* dims,
+                         uint32_t flags);
 
 /* ---- §8(e): frame-window distributed FTE (configs[3]) --------------------------------
  * One handle per rank (rank of world); every rank gets the full-size inputs of
