@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(1024) void k_cr_assemble_build(FteDims d, const dou
                                                             double* __restrict__ Ec, double* __restrict__ GBc,
                                                             double* __restrict__ gmaxp, int b0, int lo, int hi,
                                                             int end_l, int end_r, double* __restrict__ rdiag,
-                                                            double* __restrict__ graw) {
+                                                            double* __restrict__ graw, int d_full) {
   if (st->status != 0) return;
   constexpr int BP = 16 * NB, NE = (BP * BP + 1023) / 1024;
   const int i = blockIdx.x + b0, tid = threadIdx.x;
@@ -1093,7 +1093,11 @@ __global__ __launch_bounds__(1024) void k_cr_assemble_build(FteDims d, const dou
       const int dist = 3 + ar - ac;
       if (dist <= 3) ev = rowA(ar)[dist * PP + pr * P + pc];
     }
-    D[e] = dv;
+    // D is symmetric by construction (element (r, c) and (c, r) are the same row-block entry):
+    // the single-GPU solve stores its upper 16 x 16 tiles only and the levels that read it as
+    // assembled (k_cr_level d_up) take the lower ones from the transposed tile; the frame-window
+    // ranks (rdiag set: k_dist_pack copies chain ends whole) and d_full store every tile
+    if (rdiag || d_full || (r >> 4) <= (c >> 4)) D[e] = dv;
     // E_i is upper triangular (frame distance 3 + ar - ac <= 3, and the distance-3 blocks are
     // the model term's diagonal): in the single-GPU solve its strictly lower 16 x 16 tiles are
     // not stored; level 0 of k_cr_level, their only reader there, takes them as zeros
@@ -1255,7 +1259,10 @@ __host__ __device__ __forceinline__ size_t cr_level_lds_doubles(int BP, int GR) 
 
 // GB2: the instance for two GB column-blocks (GR = 32, 16 constant delays; the host picks it
 // by d.GR), so the GR = 16 instances carry none of its code
-template <int NB, bool GB2 = false>
+// DUP: D as k_cr_assemble_build stores it, upper tiles only (levels 0 and 1 of the single-GPU
+// solve, and its top block when nlev <= 1): a compile-time switch, as a run-time one made the
+// kernel spill
+template <int NB, bool GB2 = false, bool DUP = false>
 __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int iend, int top, int ne, int astep,
                                                    int nsplit, unsigned symmask, int lo_s, int top_mode, int l0,
                                                    const FteState* __restrict__ st,
@@ -1291,7 +1298,10 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     for (int q = 0; q < NQ; ++q) {
       const int e = tid + 1024 * q;
       const int r = e / LDD, c = e - r * LDD;
-      vd[q] = e < n ? (c < BP ? D[r * BP + c] : G[r * GR + c - BP]) : 0.0;
+      // d_up: D as k_cr_assemble_build stored it, upper 16 x 16 tiles only (the lower ones from
+      // the transposed tile); the survivors write it back whole
+      vd[q] = e < n ? (c < BP ? (DUP && (r >> 4) > (c >> 4) ? D[c * BP + r] : D[r * BP + c]) : G[r * GR + c - BP])
+                    : 0.0;
     }
     // one pending term per trip (dR then dL of each level, ascending)
 #pragma unroll 1
@@ -1443,7 +1453,23 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
       for (int q = 0; q < 4; ++q) t[K][q] -= v[K][q];
   };
   if (dwave) {
-    load_rows(Dc + (size_t)i * BP * BP, BP, wave * 16);
+    if constexpr (DUP) {
+      // D as assembled: upper tiles only; tile (wave, K < wave) is the transpose of (K, wave)
+      // (one base and stride per tile, selected: the per-element form kept both address sets
+      // live and spilled)
+      const double* src = Dc + (size_t)i * BP * BP;
+      const int r0 = wave * 16;
+#pragma unroll
+      for (int K = 0; K < NB; ++K) {
+        const bool tr = K * 16 < r0;
+        const double* b = src + (tr ? (K * 16 + li) * BP + r0 + lk : (r0 + lk) * BP + K * 16 + li);
+        const int st = tr ? 4 : 4 * BP;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[K][q] = b[q * st];
+      }
+    } else {
+      load_rows(Dc + (size_t)i * BP * BP, BP, wave * 16);
+    }
     // dR then dL of each level; both terms' loads in flight at once where the registers allow
     // (NB <= 5), one at a time at NB = 6
 #pragma unroll 1
@@ -2856,21 +2882,23 @@ struct CrPending {
 // path of k_cr_level writes full tiles).
 static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int iend, int top, int ne, int ns,
                            int astep, const FteState* st, FteBuffers& b, const double* Ein, double* Eout, int* bad,
-                           const CrPending& pend, int l0 = 0) {
+                           const CrPending& pend, int l0 = 0, int d_up = 0) {
   if (ne + ns == 0) return 0;
   const int NB = d.BP >> 4, NBB = 2 * NB + d.GR / 16;
   const int nsplit = cr_nsplit(d, ne, ns);
   const int nwg = ne * nsplit + ns;
   const size_t lds = sizeof(double) * cr_level_lds_doubles(d.BP, d.GR);
-#define CR_LEVEL_(nb, gb2)                                                                                       \
-  hipLaunchKernelGGL((k_cr_level<nb, gb2>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, top, ne, astep, nsplit, \
-                     pend.symmask, pend.lo_s, 0, l0, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad,    \
+#define CR_LEVEL_(nb, gb2, dup)                                                                                  \
+  hipLaunchKernelGGL((k_cr_level<nb, gb2, dup>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, top, ne, astep,    \
+                     nsplit, pend.symmask, pend.lo_s, 0, l0, st, b.Dc, Ein, Eout, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad, \
                      CrTauSrc{})
-#define CR_LEVEL(nb)        \
-  if (d.GR > 16)            \
-    CR_LEVEL_(nb, true);    \
-  else                      \
-    CR_LEVEL_(nb, false)
+#define CR_LEVEL(nb)                \
+  if (d.GR > 16)                    \
+    CR_LEVEL_(nb, true, false);     \
+  else if (d_up)                    \
+    CR_LEVEL_(nb, false, true);     \
+  else                              \
+    CR_LEVEL_(nb, false, false)
   switch (NB) {
     case 1: CR_LEVEL(1); break;
     case 2: CR_LEVEL(2); break;
@@ -2887,6 +2915,25 @@ static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int 
   return (ne > 0 && !deep) ? 1 : 0;
 }
 
+static bool cr_defer() {
+  static const bool v = [] {
+    const char* e = std::getenv("ACS_CR_DEFER");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+// the single-GPU solve stores D as its upper tiles (k_cr_assemble_build) and levels 0-1 read it
+// so (k_cr_level DUP): constant / no delays (the per-frame-delay mode builds through k_cr_build),
+// one GB column-block (the GB2 instances have no DUP form), survivors not deferred
+// (ACS_D_FULL=1: D stored whole, for A/B timing)
+static bool fte_d_upper(const FteDims& d) {
+  static const bool full = [] {
+    const char* e = std::getenv("ACS_D_FULL");
+    return e && e[0] == '1';
+  }();
+  return !d.var && d.GR <= 16 && !cr_defer() && !full;
+}
+
 // Block cyclic reduction of super-blocks [a0, top] (blocks < iend may be eliminated; a
 // chain end at iend survives), nlev levels, then (final_apply) every pending Schur term is
 // applied to the survivors. Survivor workgroups apply the previous level's terms at every
@@ -2898,11 +2945,8 @@ static int cr_launch_level(const FteDims& d, hipStream_t s, int sl, int a0, int 
 // top block).
 static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* st, FteBuffers& b, int a0, int iend,
                                int top, int nlev, int* bad, bool final_apply = true, CrPending* pend_out = nullptr,
-                               bool e_upper = true) {
-  static const bool defer = [] {
-    const char* e = std::getenv("ACS_CR_DEFER");
-    return e && e[0] == '1';
-  }();
+                               bool e_upper = true, bool d_upper = false) {
+  const bool defer = cr_defer();
   const double* Ein = b.Ec;
   double* Eout = b.Ec2;
   CrPending pend;
@@ -2913,9 +2957,11 @@ static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* 
     if (sl > 1)
       for (int j = a0; j <= top; j += 2 * sl) ++ns;
     if (ns && defer && ne * cr_nsplit(d, ne, ns) + ns > 256) ns = 0;  // defer
-    // level 0 of a chain built by k_cr_assemble_build / k_cr_build: every E is upper triangular
+    // level 0 of a chain built by k_cr_assemble_build / k_cr_build: every E is upper triangular.
+    // d_upper (D stored as upper tiles): levels 0 and 1 read D as assembled (the level-1
+    // survivors rewrite theirs whole; every block eliminated later is one of them)
     const int sym = cr_launch_level(d, s, sl, a0, iend, top, ne, ns, 2 * sl, st, b, Ein, Eout, bad, pend,
-                                    lv == 0 && e_upper ? 1 : 0);
+                                    lv == 0 && e_upper ? 1 : 0, d_upper && lv <= 1 ? 1 : 0);
     if (ns) pend.lo_s = sl;  // the survivors now hold every term of the levels below sl
     pend.symmask |= (unsigned)sym << lv;
     double* t = const_cast<double*>(Ein);
@@ -2925,7 +2971,7 @@ static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* 
   if (nlev > 0 && final_apply) {
     int ns = 0;
     for (int j = a0; j <= top; j += sl) ++ns;
-    cr_launch_level(d, s, sl, a0, iend, top, 0, ns, sl, st, b, Ein, Eout, bad, pend);
+    cr_launch_level(d, s, sl, a0, iend, top, 0, ns, sl, st, b, Ein, Eout, bad, pend, 0, d_upper && nlev <= 1 ? 1 : 0);
     pend.lo_s = sl;
   }
   if (pend_out) *pend_out = pend;
@@ -2938,19 +2984,22 @@ static const double* cr_reduce(const FteDims& d, hipStream_t s, const FteState* 
 // with_partials: CR_NCHUNK more workgroups form the tau border partial sums and the frames'
 // |g| max (b.part) meanwhile, for k_cr_back_all (the single-GPU chain, a0 = 0)
 static void cr_launch_top(const FteDims& d, hipStream_t s, int nlev, int a0, int iend, const FteState* st,
-                          FteBuffers& b, int* bad, const CrPending& pend, bool with_partials = false) {
+                          FteBuffers& b, int* bad, const CrPending& pend, bool with_partials = false,
+                          int d_up = 0) {
   const CrTauSrc ts = with_partials ? CrTauSrc{b.Tc, b.gmaxp, b.part} : CrTauSrc{};
   const int nwg = with_partials ? 1 + CR_NCHUNK : 1;
   const int sl = 1 << nlev, NB = d.BP >> 4;
   const size_t lds = sizeof(double) * cr_level_lds_doubles(d.BP, d.GR);
-#define CR_TOP_(nb, gb2)                                                                                             \
-  hipLaunchKernelGGL((k_cr_level<nb, gb2>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, a0, 1, sl, 1,           \
+#define CR_TOP_(nb, gb2, dup)                                                                                        \
+  hipLaunchKernelGGL((k_cr_level<nb, gb2, dup>), dim3(nwg), dim3(1024), lds, s, d, sl, a0, iend, a0, 1, sl, 1,      \
                      pend.symmask, pend.lo_s, 1, 0, st, b.Dc, b.Ec, b.Ec2, b.GBc, b.Wc, b.Tau, b.dL, b.dR, bad, ts)
-#define CR_TOP(nb)      \
-  if (d.GR > 16)        \
-    CR_TOP_(nb, true);  \
-  else                  \
-    CR_TOP_(nb, false)
+#define CR_TOP(nb)               \
+  if (d.GR > 16)                 \
+    CR_TOP_(nb, true, false);    \
+  else if (d_up)                 \
+    CR_TOP_(nb, false, true);    \
+  else                           \
+    CR_TOP_(nb, false, false)
   switch (NB) {
     case 1: CR_TOP(1); break;
     case 2: CR_TOP(2); break;
@@ -2965,12 +3014,13 @@ static void cr_launch_top(const FteDims& d, hipStream_t s, int nlev, int a0, int
 
 static void cr_launch_assemble_build(const FteDims& d, hipStream_t s, const FteBuffers& b, int b0 = 0,
                                      int nblk = -1, int lo = 0, int hi = INT_MAX, int end_l = -1, int end_r = -1,
-                                     double* rdiag = nullptr, double* graw = nullptr) {
+                                     double* rdiag = nullptr, double* graw = nullptr, int d_full = 0) {
   if (nblk < 0) nblk = d.nblk;
   if (nblk <= 0) return;
 #define CR_ABUILD(nb)                                                                                          \
   hipLaunchKernelGGL((k_cr_assemble_build<nb>), dim3(nblk), dim3(1024), asm_build_lds_bytes(d), s, d, b.X, \
-                     b.qinv, b.st, b.Hloc, b.gloc, b.Dc, b.Ec, b.GBc, b.gmaxp, b0, lo, hi, end_l, end_r, rdiag, graw)
+                     b.qinv, b.st, b.Hloc, b.gloc, b.Dc, b.Ec, b.GBc, b.gmaxp, b0, lo, hi, end_l, end_r, rdiag, graw, \
+                     d_full)
   switch (d.BP >> 4) {
     case 1: CR_ABUILD(1); break;
     case 2: CR_ABUILD(2); break;
@@ -3004,12 +3054,16 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
                        b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1);
     cr_launch_build(d, s, d.nblk, b.st, b.Ab, b.gb, b.Bt, b.Dc, b.Ec, b.GBc, 0, -1, -1, b.Adiag);
   } else {
-    cr_launch_assemble_build(d, s, b);
+    cr_launch_assemble_build(d, s, b, 0, -1, 0, INT_MAX, -1, -1, nullptr, nullptr, fte_d_upper(d) ? 0 : 1);
   }
   const int bend = d.nblk - 1;
   CrPending pend;
-  cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad, false, &pend);
-  cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, pend, true);
+  // D stored as upper tiles by k_cr_assemble_build (constant / no delays; the per-frame-delay
+  // mode builds through k_cr_build, whole): read as assembled by levels 0-1 and by the top block
+  // when no survivor ever rewrote it (nlev <= 1); off with ACS_CR_DEFER (survivors deferred)
+  const bool dup = fte_d_upper(d);
+  cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, d.nlev, b.bad, false, &pend, true, dup);
+  cr_launch_top(d, s, d.nlev, 0, d.nblk, b.st, b, b.bad, pend, true, dup && d.nlev <= 1 ? 1 : 0);
   // the top block and every back-substitution level in one launch, chained by
   // per-launch stamps (running the top levels' few blocks one after the other inside one
   // workgroup was tried in r03 and took 30 us: one workgroup streams a block's W at ~2 us, so
@@ -3681,9 +3735,10 @@ int acs_fte_debug_blocks(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints,
   ACS_HIP(ctx, hipMemcpyAsync(b.st, &st0, sizeof(st0), hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
                      b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr, b.Tc);
-  cr_launch_assemble_build(d, s, b);
   const int L = std::min((int)levels, d.nlev);
-  if (L > 0) cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, L, b.bad, true);
+  // as the solve stores it (upper tiles) unless the assembled D itself is asked for
+  cr_launch_assemble_build(d, s, b, 0, -1, 0, INT_MAX, -1, -1, nullptr, nullptr, L == 0 || !fte_d_upper(d) ? 1 : 0);
+  if (L > 0) cr_reduce(d, s, b.st, b, 0, d.nblk, d.nblk - 1, L, b.bad, true, nullptr, true, fte_d_upper(d));
   ACS_HIP(ctx, hipGetLastError());
   const size_t bytes = sizeof(double) * (size_t)d.nblk * d.BP * d.BP;
   ACS_HIP(ctx, hipMemcpyAsync(D_out, b.Dc, bytes, (flags & ACS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice
