@@ -1259,6 +1259,22 @@ __host__ __device__ __forceinline__ size_t cr_level_lds_doubles(int BP, int GR) 
 
 // GB2: the instance for two GB column-blocks (GR = 32, 16 constant delays; the host picks it
 // by d.GR), so the GR = 16 instances carry none of its code
+// Wave-to-wave hand-off inside a workgroup through an LDS word: the producer's LDS stores land
+// (lgkmcnt 0) before the flag; the consumer spins on the flag, then reads (LDS ops of a wave
+// execute in order).
+__device__ __forceinline__ void cr_flag_set(int* f, int v) {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt not waited for
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void cr_flag_wait(const int* f, int v) {
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
+}
+// s_barrier after this wave's LDS stores have landed, without waiting for its global loads
+__device__ __forceinline__ void cr_lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+}
+
 // DUP: D as k_cr_assemble_build stores it, upper tiles only (levels 0 and 1 of the single-GPU
 // solve, and its top block when nlev <= 1): a compile-time switch, as a run-time one made the
 // kernel spill
@@ -1325,6 +1341,9 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
       for (int q = 0; q < NQ; ++q) vd[q] -= v[q];
     }
+    // DUP: the lower tiles were read from the upper ones, which other waves of this workgroup
+    // are about to overwrite: every read lands before the first store
+    if constexpr (DUP) __syncthreads();
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int e = tid + 1024 * q;
@@ -1338,6 +1357,12 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     return;
   }
   const int part = (int)blockIdx.x % nsplit;
+  // pivot-row hand-off flags (R_kK of step k carries stamp k + 1; double-buffered like the
+  // pivot buffers): cleared before any wave can read them (LDS-only barrier: the global loads
+  // issued below are not waited for)
+  __shared__ int s_rflag[2][8];
+  if (tid < 16) s_rflag[tid >> 3][tid & 7] = -1;
+  cr_lds_barrier();
   // top_mode: the last surviving block a0 itself (no neighbours, only its GB column-blocks:
   // W_gb = D^-1 GB and Tau = GB^T W_gb for k_cr_top), after its pending terms
   const int i = top_mode ? a0 : a0 + s * (2 * ((int)blockIdx.x / nsplit) + 1);
@@ -1585,6 +1610,8 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
           t[K] = acc;
 #pragma unroll
           for (int q = 0; q < 4; ++q) Rk[(lk + 4 * q) * BP + K * 16 + li] = acc[q];
+          // hand R_kK to the next pivot wave now, not at the barrier (cr_flag_*)
+          if (k + 1 < NB) cr_flag_set(&s_rflag[k & 1][K], k + 1);
         }
         PROFA(34 + k, k);
       } else {
@@ -1592,12 +1619,18 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
         for (int q = 0; q < 4; ++q) Ck[(wave * 16 + lk + 4 * q) * TS + li] = t[k][q];
       }
     }
-    __syncthreads();
+    // The next pivot's wave (k + 1) does not wait here for the whole pivot row: it starts its
+    // diagonal update and tile inverse as soon as R_k,k+1 is flagged, takes each later R_kK at
+    // its flag, and arrives at this step's barrier inside its inverse (after 4 scalar steps),
+    // when the pivot wave's row panel is done. Every wave still passes one barrier per step.
+    const bool early = dwave && wave == k + 1;
+    if (!early) __syncthreads();
     if (dwave) {
       if (wave == k + 1) {
         // next pivot: its diagonal tile first, then its inverse with the remaining row
         // updates (MFMA) slotted between the pivot steps (VALU)
         PROFA(44 + k, k + 1);
+        cr_flag_wait(&s_rflag[k & 1][k + 1], k + 1);
         {
           dbl4 acc = t[k + 1];
 #pragma unroll
@@ -1609,8 +1642,11 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
         tile16_gj_inverse_hook<true>(v, lane, part ? nullptr : bad, [&](auto sc) {
           constexpr int S = decltype(sc)::value;
           const int K = k + 2 + S / 4, ks = S % 4;  // constants once the k loop is unrolled
-          if (K < NB)
+          if (K < NB) {
+            if (ks == 0) cr_flag_wait(&s_rflag[k & 1][K], k + 1);
             t[K] = mfma64(-Ck[(wave * 16 + li) * TS + 4 * ks + lk], Rk[(4 * ks + lk) * BP + K * 16 + li], t[K]);
+          }
+          if constexpr (S == 3) __syncthreads();  // this wave's arrival at step k's barrier
         });
 #pragma unroll
         for (int q = 0; q < 4; ++q) t[k + 1][q] = v[q];
