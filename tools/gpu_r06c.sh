@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$PWD/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
 T=${T:-r06c}
-timeout -k 10 900 python -u -m pytest tests/test_gpu_fte_symmetry.py tests/test_gpu_fte.py tests/test_gpu_fte_cfg2.py tests/test_gpu_dist.py tests/test_gpu_fullsize.py tests/test_gpu_fullsize_oracle.py tests/test_fte_reference.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_fte_$T.log 2>&1; rc=$?; tail -n 4 $OUT/pytest_fte_$T.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python -u -m pytest tests/test_gpu_fte_symmetry.py tests/test_gpu_fte.py tests/test_gpu_fte_cfg2.py tests/test_gpu_dist.py tests/test_gpu_fullsize.py tests/test_gpu_fullsize_oracle.py tests/test_fte_reference.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_fte_$T.log 2>&1; rc=$?; tail -n 12 $OUT/pytest_fte_$T.log; case $rc in 0|1) ;; *) exit $rc;; esac
 for V in up full; do
   for F in 10000 1000; do
     if [ $V = full ]; then export ACS_D_FULL=1; else unset ACS_D_FULL; fi
