@@ -1323,6 +1323,7 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll 1
     for (int k = 0; (lo_s << (k >> 1)) <= hs; ++k) {
       const int sp = lo_s << (k >> 1);
+      const bool sy = (symmask >> (__ffs(sp) - 1)) & 1u;
       const double* pq = (k & 1) ? ((j + sp < iend) ? dL + (size_t)(j + sp) * BP * LDD : nullptr)
                                  : ((j - sp >= a0) ? dR + (size_t)(j - sp) * BP * LDD : nullptr);
       if (!pq) continue;
@@ -1331,11 +1332,9 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
       for (int q = 0; q < NQ; ++q) {
         const int e = tid + 1024 * q;
         const int r = e / LDD, c = e - r * LDD;
-        // D parts of the pending terms are read as their upper triangle, mirrored (the one-wave-
-        // per-column-block levels store upper tiles only, sy; the deep path full tiles, whose
-        // computed lower half is not bitwise the transpose): every D a level factors is then
-        // bitwise symmetric, as the assembled D is
-        const int es = (c < BP && r > c) ? c * LDD + r : e;
+        // D parts of the pending terms of a one-wave-per-column-block level (sy) hold their
+        // upper tiles only; the deep path writes full tiles
+        const int es = (sy && c < BP && (r >> 4) > (c >> 4)) ? c * LDD + r : e;
         v[q] = e < n ? pq[es] : 0.0;
       }
 #pragma unroll
@@ -1441,19 +1440,20 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
 #pragma unroll
       for (int q = 0; q < 4; ++q) t[K][q] = src[(r0 + lk + 4 * q) * ld + K * 16 + li];
   };
-  // pending D terms are read as their upper triangle, mirrored: element (r, c) with r > c from
-  // (c, r). A level that took the one-wave-per-column-block path (its symmask bit) stores upper
-  // tiles only; the deep path writes full tiles, whose lower half is the computed (not bitwise
-  // transposed) product: the mirror keeps every factored D bitwise symmetric
-  auto sub_rows = [&](const double* src, int ld, int r0, bool /*sy*/) {
+  // pending D terms of a level that took the one-wave-per-column-block path (its symmask bit) are
+  // stored as upper tiles: tile (r0/16, K) with K < r0/16 is the transpose of tile (K, r0/16);
+  // the deep path writes full tiles (rows read contiguously). (Reading every pending term as its
+  // mirrored upper triangle makes each factored D bitwise symmetric, but moves the rounding of
+  // the single-GPU and frame-window reductions apart: measured in r06c, the head-model 3-rank
+  // solve then took 14 LM iterations against the single GPU's 12 at the same cost. Not kept.)
+  auto sub_rows = [&](const double* src, int ld, int r0, bool sy) {
     double v[NB][4];
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool lower = K * 16 < r0 || (K * 16 == r0 && li < lk + 4 * q);
-        v[K][q] = lower ? src[(K * 16 + li) * ld + r0 + lk + 4 * q] : src[(r0 + lk + 4 * q) * ld + K * 16 + li];
-      }
+      for (int q = 0; q < 4; ++q)
+        v[K][q] = (sy && K * 16 < r0) ? src[(K * 16 + li) * ld + r0 + lk + 4 * q]
+                                      : src[(r0 + lk + 4 * q) * ld + K * 16 + li];
 #pragma unroll
     for (int K = 0; K < NB; ++K)
 #pragma unroll
@@ -1723,9 +1723,6 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
       };
       if (rr < NB) {  // left term E_i^T [W_l | W_gb], output tile I
         if (Jt >= NB && Jt < 2 * NB) continue;
-        // E_i^T W_l is symmetric and read as its upper triangle (sub_rows / the survivors):
-        // its strictly lower tiles are not formed
-        if (Jt < NB && rr > Jt) continue;
         const dbl4 acc = chain([&](int I, int K, int ks) { return sEi[(K * 16 + 4 * ks + lk) * BP + I * 16 + li]; }, rr);
         double* o = dL + (size_t)i * BP * LDD;
 #pragma unroll
@@ -1733,7 +1730,6 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
       } else if (rr < 2 * NB) {  // right term E_r [W_r | W_gb] and the new coupling -E_r W_l
         if (!Er) continue;
         const int I = rr - NB;
-        if (Jt >= NB && Jt < 2 * NB && I > Jt - NB) continue;  // E_r W_r: upper tiles only (as above)
         const dbl4 acc = sEr ? chain([&](int I_, int K, int ks) { return sEr[(I_ * 16 + li) * (BP + 1) + K * 16 + 4 * ks + lk]; }, I)
                              : chain([&](int I_, int K, int ks) {
                                  return (l0 && K < I_) ? 0.0 : Er[(I_ * 16 + li) * BP + K * 16 + 4 * ks + lk];

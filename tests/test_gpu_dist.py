@@ -329,3 +329,39 @@ np.savez({str(tmp_path / 'lv.npz')!r}, **out)
         assert rep['iters'] == int(lv[f'i{world}'])
         np.testing.assert_array_equal(X, lv[f'X{world}'])
         np.testing.assert_array_equal(tau, lv[f't{world}'])
+
+
+def _rccl_worker(rank, world, port, out_dir):
+    """One rank over the nccl (RCCL) backend, the configs[3] bench leg's exchange: a
+    one-rank group on this single-GPU box (RCCL wants one device per rank), so every
+    all-reduce of the frame-window protocol runs through RCCL on the device payloads."""
+    import torch
+    import torch.distributed as tdist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    tdist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', 0))
+    try:
+        ctx = _native.Context(0)
+        prob, cams, X0 = _problem(40)
+        table = pkin.build_table(prob.mode)
+        t = torch.arange(4, dtype=torch.float64, device='cuda:0')
+        tdist.all_reduce(t)
+        X, tau, rep = dist.fte_solve_dist(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0)
+        np.savez(os.path.join(out_dir, f'rccl{rank}.npz'), X=X, tau=tau, iters=rep['iters'], t=t.cpu().numpy())
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_fte_dist_over_rccl_one_rank(ctx, tmp_path):
+    """The RCCL exchange of the frame-window solve executes: a one-rank nccl process group
+    (HSA_ENABLE_IPC_MODE_LEGACY=0 as exported on the box) runs dist.fte_solve_dist with every
+    payload all-reduced by RCCL; the result is the single-GPU solve's."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_rccl_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True, start_method='spawn')
+    prob, cams, X0 = _problem(40)
+    table = pkin.build_table(prob.mode)
+    X1, t1, r1 = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0)
+    a = np.load(tmp_path / 'rccl0.npz')
+    np.testing.assert_array_equal(a['t'], np.arange(4.0))
+    assert int(a['iters']) == r1['iters']
+    np.testing.assert_allclose(a['X'], X1, rtol=0, atol=1e-9)
