@@ -8,6 +8,20 @@
 #define __forceinline__ inline
 #endif
 
+// Horner step c + z * acc as one v_fma_f64 with a separate destination. Written plainly, the
+// compiler keeps the (hoisted) polynomial constant in a VGPR and emits v_mov_b64 + v_fmac_f64
+// (the accumulate form ties the addend to the destination): two issue slots per term on the
+// latency-bound LM chains of k_sba_lm.
+__host__ __device__ __forceinline__ double hfma(double z, double acc, double c) {
+#ifdef __HIP_DEVICE_COMPILE__
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(z), "v"(acc), "v"(c));
+  return d;
+#else
+  return std::fma(z, acc, c);
+#endif
+}
+
 // ------------------------------------------------------------------------------------
 // Short-latency f64 math for the per-iteration dependency chains (measured on gfx950,
 // tools/probe/valu_lat_probe.hip: IEEE 1/x 72 cycles, sqrt 109, log1p 569; v_rcp_f64 +
@@ -38,9 +52,10 @@ __host__ __device__ __forceinline__ double rsq_nr(double x) {
 // log1p(t) for t >= 0 (finite): u = 1 + t with its exact rounding error c, u = 2^k m with
 // m in [1/sqrt2, sqrt2), log m = f - f^2/2 + s (f^2/2 + R(s^2)), s = f / (2 + f), f = m - 1
 // (the classic fdlibm reduction and minimax coefficients), one reciprocal, no table.
-__host__ __device__ __forceinline__ double log1p_pos(double t) {
-  const double u = 1.0 + t;
-  const double c = (t >= 1.0 ? 1.0 - (u - t) : t - (u - 1.0)) * rcp_nr(u);
+// log1p_pos with u = 1 + t and ru ~ 1 / u already formed by the caller (k_sba_lm shares that
+// reciprocal with the Cauchy weights)
+__host__ __device__ __forceinline__ double log1p_pos_ur(double t, double u, double ru) {
+  const double c = (t >= 1.0 ? 1.0 - (u - t) : t - (u - 1.0)) * ru;
   int k;
   double m = std::frexp(u, &k);  // [0.5, 1)
   if (m < 0.70710678118654752440) {
@@ -50,11 +65,16 @@ __host__ __device__ __forceinline__ double log1p_pos(double t) {
   const double f = m - 1.0;
   const double s = f * rcp_nr(2.0 + f);
   const double z = s * s, w = z * z;
-  const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
-  const double t2 = z * (6.666666666666735130e-01 +
-                         w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+  const double t1 = w * hfma(w, hfma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
+  const double t2 =
+      z * hfma(w, hfma(w, hfma(w, 1.479819860511658591e-01, 1.818357216161805012e-01), 2.857142874366239149e-01),
+               6.666666666666735130e-01);
   const double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
   return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + (dk * 1.90821492927058770002e-10 + c))) - f);
+}
+__host__ __device__ __forceinline__ double log1p_pos(double t) {
+  const double u = 1.0 + t;
+  return log1p_pos_ur(t, u, rcp_nr(u));
 }
 
 // atan(x) for x >= 0 with one reciprocal: |v| <= tan(pi/8) after
@@ -71,14 +91,19 @@ __host__ __device__ __forceinline__ double atan_pos(double x) {
   const double hi = a ? 0.0 : (c ? 1.57079632679489655800e+00 : 7.85398163397448278999e-01);
   const double lo = a ? 0.0 : (c ? 6.12323399573676603587e-17 : 3.06161699786838301793e-17);
   const double z = v * v, w = z * z;
-  const double s1 = z * (3.33333333333329318027e-01 +
-                         w * (1.42857142725034663711e-01 +
-                              w * (9.09088713343650656196e-02 +
-                                   w * (6.66107313738753120669e-02 +
-                                        w * (4.97687799461593236017e-02 + w * 1.62858201153657823623e-02)))));
-  const double s2 = w * (-1.99999999998764832476e-01 +
-                         w * (-1.11111104054623557880e-01 +
-                              w * (-7.69187620504482999495e-02 +
-                                   w * (-5.83357013379057348645e-02 + w * -3.65315727442169155270e-02))));
+  const double s1 =
+      z * hfma(w,
+               hfma(w,
+                    hfma(w, hfma(w, hfma(w, 1.62858201153657823623e-02, 4.97687799461593236017e-02),
+                                 6.66107313738753120669e-02),
+                         9.09088713343650656196e-02),
+                    1.42857142725034663711e-01),
+               3.33333333333329318027e-01);
+  const double s2 =
+      w * hfma(w,
+               hfma(w, hfma(w, hfma(w, -3.65315727442169155270e-02, -5.83357013379057348645e-02),
+                            -7.69187620504482999495e-02),
+                    -1.11111104054623557880e-01),
+               -1.99999999998764832476e-01);
   return hi + ((v - v * (s1 + s2)) + lo);
 }

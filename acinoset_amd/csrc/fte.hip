@@ -1623,14 +1623,17 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
     // diagonal update and tile inverse as soon as R_k,k+1 is flagged, takes each later R_kK at
     // its flag, and arrives at this step's barrier inside its inverse (after 4 scalar steps),
     // when the pivot wave's row panel is done. Every wave still passes one barrier per step.
-    const bool early = dwave && wave == k + 1;
+#ifndef CR_EARLY_PIVOT
+#define CR_EARLY_PIVOT 1
+#endif
+    const bool early = CR_EARLY_PIVOT && dwave && wave == k + 1;
     if (!early) __syncthreads();
     if (dwave) {
       if (wave == k + 1) {
         // next pivot: its diagonal tile first, then its inverse with the remaining row
         // updates (MFMA) slotted between the pivot steps (VALU)
         PROFA(44 + k, k + 1);
-        cr_flag_wait(&s_rflag[k & 1][k + 1], k + 1);
+        if (CR_EARLY_PIVOT) cr_flag_wait(&s_rflag[k & 1][k + 1], k + 1);
         {
           dbl4 acc = t[k + 1];
 #pragma unroll
@@ -1643,10 +1646,10 @@ __global__ __launch_bounds__(1024) void k_cr_level(FteDims d, int s, int a0, int
           constexpr int S = decltype(sc)::value;
           const int K = k + 2 + S / 4, ks = S % 4;  // constants once the k loop is unrolled
           if (K < NB) {
-            if (ks == 0) cr_flag_wait(&s_rflag[k & 1][K], k + 1);
+            if (CR_EARLY_PIVOT && ks == 0) cr_flag_wait(&s_rflag[k & 1][K], k + 1);
             t[K] = mfma64(-Ck[(wave * 16 + li) * TS + 4 * ks + lk], Rk[(4 * ks + lk) * BP + K * 16 + li], t[K]);
           }
-          if constexpr (S == 3) __syncthreads();  // this wave's arrival at step k's barrier
+          if constexpr (CR_EARLY_PIVOT && S == 3) __syncthreads();  // this wave's arrival at step k's barrier
         });
 #pragma unroll
         for (int q = 0; q < 4; ++q) t[k + 1][q] = v[q];

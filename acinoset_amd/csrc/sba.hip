@@ -127,20 +127,24 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     double Fl = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      ProjOut o;  // slots without an observation: the null camera, exact zero contributions
+      // slots without an observation: the null camera, exact zero contributions
+      double pu, pv, J[6];
       if constexpr (HOIST)
-        fisheye_project<true>(cr[s], X0, X1, X2, o);
+        fisheye_uvj(cr[s], X0, X1, X2, pu, pv, J);
       else
-        fisheye_project<true>(oc[s], X0, X1, X2, o);
-      const double r[2] = {o.u - ou[s], o.v - ov[s]};
+        fisheye_uvj(oc[s], X0, X1, X2, pu, pv, J);
+      const double r[2] = {pu - ou[s], pv - ov[s]};
       const double zu = r[0] * r[0] * if2, zv = r[1] * r[1] * if2;
-      Fl += log1p_pos(zu + zv + zu * zv);  // log1p(zu) + log1p(zv) with one logarithm
+      // log1p(zu) + log1p(zv) with one logarithm, and the two Cauchy weights 1 / (1 + z) from
+      // the logarithm's own reciprocal of (1 + zu)(1 + zv)
+      const double t = zu + zv + zu * zv, u1 = 1.0 + t, ru = rcp_nr(u1);
+      Fl += log1p_pos_ur(t, u1, ru);
 #pragma unroll
       for (int d = 0; d < 2; ++d) {
         const double z = d ? zv : zu;
-        const double w = rcp_nr(1.0 + z);                   // rho'(z): gradient weight
+        const double w = (d ? 1.0 + zu : 1.0 + zv) * ru;    // rho'(z): gradient weight
         const double wh = fmax((1.0 - z) * w * w, 0.1 * w);  // rho' + 2 z rho'' (Triggs), floored
-        const double j0 = o.J[3 * d], j1 = o.J[3 * d + 1], j2 = o.J[3 * d + 2];
+        const double j0 = J[3 * d], j1 = J[3 * d + 1], j2 = J[3 * d + 2];
         const double hj0 = wh * j0, hj1 = wh * j1, hj2 = wh * j2;
         Ho[0] += hj0 * j0;
         Ho[1] += hj0 * j1;
