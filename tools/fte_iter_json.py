@@ -5,6 +5,7 @@ launch, in iteration order) -> {frames, kernel_us_per_iter, hbm_bytes_per_iter, 
     python tools/fte_iter_json.py fte_traffic_iter_10k.log 10000 out.json"""
 import json
 import re
+import os
 import sys
 
 rows = []
@@ -26,6 +27,6 @@ out = {'frames': int(sys.argv[2]), 'kernel_us_per_iter': tot_us, 'hbm_bytes_per_
        'kernels': rows,
        'by_kernel': {k: {'us': v[0], 'share': v[0] / tot_us, 'hbm_bytes': v[1]} for k, v in by.items()},
        'dominant': {'kernel': dom[0], 'us': dom[1][0], 'share': dom[1][0] / tot_us, 'hbm_bytes': dom[1][1]},
-       'source': sys.argv[1]}
+       'source': os.path.basename(sys.argv[1])}
 json.dump(out, open(sys.argv[3], 'w'), indent=1)
 print(json.dumps(out['dominant']), f"{out['hbm_bytes_per_iter'] / 1e9:.3f} GB/iter, {tot_us:.0f} us/iter")
