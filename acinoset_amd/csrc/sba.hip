@@ -9,7 +9,8 @@
 // Mapping: one point = one aligned group of G lanes (G = next pow2 of the observation
 // slots, <= 64) — lane l owns slot l (+ j*G). Observations are an (n_pts, K) slot tensor
 // (slot = camera for the dense core.sba layout) read once, coalesced, into registers;
-// the camera records are staged in LDS. Each LM iteration: every lane projects its
+// the camera records are staged in LDS (the HOIST instance loads each lane's record into its
+// registers instead). Each LM iteration: every lane projects its
 // observation(s) and forms its contribution to the gradient g = sum rho'(z) r J (3), the
 // Gauss-Newton matrix H = sum max(rho' + 2 z rho'', 0.1 rho') J^T J (6; Triggs-corrected,
 // which converges quadratically where IRLS weights only converge linearly) and the Cauchy
@@ -32,8 +33,13 @@ struct SbaParams {
 };
 
 // HOIST: each lane keeps its camera record in registers for the whole LM loop instead of
-// re-reading it from LDS in every projection (188 VGPRs: 2 waves per SIMD), chosen for
+// re-reading it from LDS in every projection (198 VGPRs: 2 waves per SIMD), chosen for
 // grids of at most 2 waves per SIMD, where nothing else would fill the SIMD anyway.
+// The other instances are not occupancy-bound either: <4, 3> (the configs[4] shape) holds 186
+// VGPRs, 2 waves per SIMD, and register budgets for 2 / 3 / 4 waves per SIMD
+// (amdgpu_waves_per_eu) ran it in 0.270 / 0.273 / 0.454 ms against 0.268-0.272 unconstrained
+// (profiles/r06/bench_sba_w*_r06h.log): three independent slot chains per lane already keep the
+// VALU issuing, and the 4-wave budget spills.
 template <int G, int S, bool CAMID, bool HOIST>
 __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams, int C, int K,
                                                 const double2* __restrict__ uv,
@@ -71,16 +77,26 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     x1 = pts_in[3 * p + 1];
     x2 = pts_in[3 * p + 2];
   }
-  for (int i = threadIdx.x; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
   // the null camera (record C): R = 0, t = (0, 0, 1), K = 0. Slots without an observation
   // project through it to u = v = 0 with a zero Jacobian, so with a zero observation they add
   // exact zeros to every sum: linearize() needs no branch around its projection
-  if (threadIdx.x < ACS_CAM_STRIDE) s_cam[C * ACS_CAM_STRIDE + threadIdx.x] = threadIdx.x == 19 ? 1.0 : 0.0;
-  __syncthreads();
-  if (!live) return;  // whole group leaves together
+  double cr[HOIST ? S : 1][ACS_CAM_STRIDE];
+  if constexpr (HOIST) {
+    // S = 1 and slot = camera: the lane's record is loaded from global memory (L2-resident,
+    // C x 160 B) in the same round trip as the observation, straight into its registers; no
+    // LDS copy and no barrier ahead of the LM loop
+    const double* cg = cams + (size_t)(lane < C ? lane : C - 1) * ACS_CAM_STRIDE;
+#pragma unroll
+    for (int i = 0; i < ACS_CAM_STRIDE; ++i) cr[0][i] = cg[i];
+    if (!live) return;  // whole group leaves together
+  } else {
+    for (int i = threadIdx.x; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
+    if (threadIdx.x < ACS_CAM_STRIDE) s_cam[C * ACS_CAM_STRIDE + threadIdx.x] = threadIdx.x == 19 ? 1.0 : 0.0;
+    __syncthreads();
+    if (!live) return;  // whole group leaves together
+  }
 
   double ou[S], ov[S];
-  double cr[HOIST ? S : 1][ACS_CAM_STRIDE];
   const double* oc[S];
   bool ok[S];
   int mine = 0;
@@ -94,7 +110,7 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     oc[s] = s_cam + (ok[s] ? cam : C) * ACS_CAM_STRIDE;
     if constexpr (HOIST) {
 #pragma unroll
-      for (int i = 0; i < ACS_CAM_STRIDE; ++i) cr[s][i] = oc[s][i];
+      for (int i = 0; i < ACS_CAM_STRIDE; ++i) cr[s][i] = ok[s] ? cr[s][i] : (i == 19 ? 1.0 : 0.0);
     }
     mine += ok[s] ? 1 : 0;
   }
