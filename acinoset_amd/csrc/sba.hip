@@ -141,6 +141,11 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
     for (int i = 0; i < 6; ++i) Ho[i] = 0.0;
     go[0] = go[1] = go[2] = 0.0;
     double Fl = 0.0;
+    // S > 1: the lane's slots share one logarithm too. With T = prod_s (1 + t_s) - 1 formed as
+    // T + t + T t (exact algebra, relative rounding only), sum_s log1p(t_s) = log1p(T), and
+    // prod_s 1 / (1 + t_s) is the reciprocal it needs. An empty slot (t = 0, 1 / (1 + t) = 1)
+    // leaves both unchanged exactly.
+    double Tl = 0.0, rTl = 1.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       // slots without an observation: the null camera, exact zero contributions
@@ -154,7 +159,12 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
       // log1p(zu) + log1p(zv) with one logarithm, and the two Cauchy weights 1 / (1 + z) from
       // the logarithm's own reciprocal of (1 + zu)(1 + zv)
       const double t = zu + zv + zu * zv, u1 = 1.0 + t, ru = rcp_nr(u1);
-      Fl += log1p_pos_ur(t, u1, ru);
+      if constexpr (S == 1) {
+        Fl += log1p_pos_ur(t, u1, ru);
+      } else {
+        Tl = s == 0 ? t : fma(Tl, t, Tl + t);
+        rTl = s == 0 ? ru : rTl * ru;
+      }
 #pragma unroll
       for (int d = 0; d < 2; ++d) {
         const double z = d ? zv : zu;
@@ -174,6 +184,7 @@ __global__ __launch_bounds__(256) void k_sba_lm(const double* __restrict__ cams,
         go[2] += wr * j2;
       }
     }
+    if constexpr (S > 1) Fl = log1p_pos_ur(Tl, 1.0 + Tl, rTl);
 #pragma unroll
     for (int i = 0; i < 6; ++i) Ho[i] = group_sum<G>(Ho[i]);
 #pragma unroll
