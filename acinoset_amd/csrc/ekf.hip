@@ -302,6 +302,120 @@ __device__ void ekf_fk_point(const SkelView& sk, const double* ss, double eps, c
   out[2] = p2;
 }
 
+// ekf_fk_point's table walk for one (pose q, marker l) item of a one-joint skeleton, resolved
+// once per kernel: the joint's rotations (axis, row of its sine in ekf_fk_trig_trans's table
+// for pose q) and the node chain's offsets, in walk order. ekf_point_eval then repeats
+// ekf_fk_point's arithmetic in the same order from registers, with every table read of a frame
+// issued at once (the walk was a chain of dependent LDS loads per frame). Same bits.
+// ok = false: the chain is longer than EKF_PLAN_D or leaves joint 0, and the caller walks the
+// table as before. (Tried, r06l: each item forming its own sines / cosines and translation,
+// which drops the trig table's phase and barrier: the FK/proj phase went 2.8 -> 2.5 us, but
+// the extra live state slowed the later phases by 1.1 us per frame.)
+#define EKF_PLAN_D 2
+struct EkfPointPlan {
+  bool ok;
+  int nrot, nstep, tr;       // tr: rw offset of the pose's root / world translation
+  int ax[3], sci[3];
+  int op[EKF_PLAN_D];        // offset parameter of each step (-1: the table offset)
+  double off[EKF_PLAN_D][3];
+};
+
+__device__ inline EkfPointPlan ekf_point_plan(const SkelView& sk, int q, int l) {
+  EkfPointPlan pl;
+  const int* jt = sk.joints;
+  const int moved = q - 1;
+  pl.nrot = jt[1] < 3 ? jt[1] : 3;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const int p = r < pl.nrot ? jt[5 + r] : 0;
+    pl.ax[r] = r < pl.nrot ? jt[2 + r] : 0;
+    pl.sci[r] = (p == moved ? 2 : 0) * FK_MAXP + p;
+  }
+  // the node chain in walk order, with compile-time indices only (a runtime index would put
+  // the plan in scratch memory)
+  bool live = sk.J == 1 && jt[0] < 0 && jt[1] <= 3, done = false;
+  int node = sk.outn[l], base = -1;
+  pl.nstep = 0;
+#pragma unroll
+  for (int s = 0; s <= EKF_PLAN_D; ++s) {
+    int b = -1, fr = 0, op = -1;
+    double o0 = 0.0, o1 = 0.0, o2 = 0.0;
+    if (live && !done) {
+      const int* nd = sk.nodes + 4 * node;
+      b = nd[0];
+      fr = nd[1];
+      op = nd[2];
+      o0 = sk.off[3 * node];
+      o1 = sk.off[3 * node + 1];
+      o2 = sk.off[3 * node + 2];
+      if (b == -2 || b == -1) {
+        done = true;
+        base = b;
+      } else if (s == EKF_PLAN_D || fr != 0) {
+        live = false;
+      } else {
+        pl.nstep = s + 1;
+        node = b;
+      }
+    }
+    if (s < EKF_PLAN_D) {
+      pl.op[s] = live && !done ? op : -1;  // a chain step (not its end)
+      pl.off[s][0] = o0;
+      pl.off[s][1] = o1;
+      pl.off[s][2] = o2;
+    }
+  }
+  pl.ok = live && done;
+  pl.tr = q * 6 + (base == -2 ? 3 : 0);
+  return pl;
+}
+
+template <bool F32>
+__device__ __forceinline__ void ekf_point_eval(const EkfPointPlan& pl, const double* ss, double eps, const double* sc,
+                                               const double* rw, int q, double* out) {
+  // every table value of the frame first: the joint's sines / cosines, the offset
+  // parameters, the translation
+  double sn[3], cs[3], xo[EKF_PLAN_D], t[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    sn[r] = sc[pl.sci[r]];
+    cs[r] = sc[pl.sci[r] + FK_MAXP];
+  }
+#pragma unroll
+  for (int s = 0; s < EKF_PLAN_D; ++s) xo[s] = pl.op[s] >= 0 ? ekf_xq<F32>(ss, q, pl.op[s], eps) : 0.0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = rw[pl.tr + i];
+  double Mm[9];  // G of joint 0 (ekf_fk_point's G_of; no parent)
+#pragma unroll
+  for (int col = 0; col < 3; ++col) {
+    double v[3] = {col == 0 ? 1.0 : 0.0, col == 1 ? 1.0 : 0.0, col == 2 ? 1.0 : 0.0};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      if (r >= pl.nrot) break;
+      double w[3];
+      act_rot_vec(pl.ax[r], sn[r], cs[r], v, w);
+      v[0] = w[0];
+      v[1] = w[1];
+      v[2] = w[2];
+    }
+    Mm[col] = v[0];
+    Mm[3 + col] = v[1];
+    Mm[6 + col] = v[2];
+  }
+  double p0 = 0.0, p1 = 0.0, p2 = 0.0;
+#pragma unroll
+  for (int s = 0; s < EKF_PLAN_D; ++s) {
+    if (s >= pl.nstep) break;
+    const double o0 = pl.op[s] >= 0 ? xo[s] : pl.off[s][0], o1 = pl.off[s][1], o2 = pl.off[s][2];
+    p0 += Mm[0] * o0 + Mm[1] * o1 + Mm[2] * o2;
+    p1 += Mm[3] * o0 + Mm[4] * o1 + Mm[5] * o2;
+    p2 += Mm[6] * o0 + Mm[7] * o1 + Mm[8] * o2;
+  }
+  out[0] = p0 + t[0];
+  out[1] = p1 + t[1];
+  out[2] = p2 + t[2];
+}
+
 // Row / column of the flat index e = tid, tid + nth, ... over rows of nc columns, stepped
 // without an integer division per element (nth / nc and nth % nc once per loop).
 struct Walk2 {
@@ -1046,6 +1160,16 @@ __global__ __launch_bounds__(512) void k_ekf_filter(EkfDims d, const int* __rest
 // (tests/test_gpu_ekf.py; tools/ekf_drift.py: the same drift against the oracle as the
 // 8-wave kernel over 250 frames).
 #define EKF_W1_P 6
+// A / B switch (tools/gpu_r06m.sh): 0 = Q, the measurements and the likelihoods read from
+// global memory inside each frame, as before round 6
+#ifndef EKF_W1_PREFETCH
+#define EKF_W1_PREFETCH 1
+#endif
+// A / B switch (tools/gpu_r06n.sh): 0 = the one-joint FK's trig tables formed at the start of
+// the FK / projection phase, behind their own barrier
+#ifndef EKF_W1_TRIG_EARLY
+#define EKF_W1_TRIG_EARLY 1
+#endif
 
 // LDS doubles of k_ekf_filter_w1
 __host__ __device__ inline size_t ekf_w1_lds(const EkfDims& d) {
@@ -1162,7 +1286,7 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
   double* sRl = sCam + (size_t)d.C * ACS_CAM_STRIDE;     // skeleton table (reals, then ints)
   int* sI = reinterpret_cast<int*>(sRl + d.n_reals);
 #ifdef EKF_PROFILE
-  unsigned long long s_prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = 0;
+  unsigned long long s_prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = 0, s_sub = 0;
 #define EKF_TICK1(k)                                                              \
   do {                                                                            \
     __syncthreads();                                                              \
@@ -1205,8 +1329,42 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
       ea = t - nA;
     }
   }
+  // one-joint skeletons with one (pose, observation) item per thread: the item's table walk
+  // resolved once (ekf_point_plan); otherwise ekf_fk_point walks it every frame
+  EkfPointPlan pl;
+  pl.ok = false;
+  if constexpr (!AH) {
+    if (sk.J == 1 && (P + 1) * CL <= nth && tid < (P + 1) * CL) pl = ekf_point_plan(sk, tid / CL, (tid % CL) % d.L);
+  }
+  // no global load on a frame's chain: Q in registers (the predict phase's elements of this
+  // thread), this thread's measurement row loaded one frame ahead, its camera's weights formed
+  // once (the same expressions, so the same bits)
+  constexpr int QR = (n * n + 64 * NW - 1) / (64 * NW);
+  double qreg[QR];
+#pragma unroll
+  for (int k = 0; k < QR; ++k) qreg[k] = tid + k * nth < n * n ? Q[tid + k * nth] : 0.0;
+  const bool pf = EKF_W1_PREFETCH && m <= nth;
+  // the trig tables formed inside the prediction when the second covariance pass (P n threads,
+  // rounded up to a wave) leaves enough threads idle for their 2 P + 2 (P + 1) items
+  const int trig_t0 = ((P * n + 63) / 64) * 64;
+  const bool trig_early = EKF_W1_TRIG_EARLY && !AH && sk.J == 1 && trig_t0 + 4 * P + 2 <= nth;
+  double m_nx = 0.0, l_nx = 0.0, w_rb = 0.0, s2_rb = 0.0;
+  const double w_mx = 1.0 / (d.maxpix * d.maxpix), s2_mx = d.maxpix * d.maxpix;
+  if (pf && tid < m) {
+    const double rb = rbase[(tid >> 1) / d.L];
+    w_rb = 1.0 / (rb * rb);
+    s2_rb = rb * rb;
+    const size_t f0 = (size_t)seq * d.N;
+    m_nx = meas[f0 * fstride * 2 + tid];
+    l_nx = lik[f0 * fstride + (tid >> 1)];
+  }
   for (int i = 0; i < d.N; ++i) {
     const size_t fo = (size_t)seq * d.N + i;
+    const double m_cur = m_nx, l_cur = l_nx;
+    if (pf && tid < m && i + 1 < d.N) {
+      m_nx = meas[(fo + 1) * fstride * 2 + tid];
+      l_nx = lik[(fo + 1) * fstride + (tid >> 1)];
+    }
     EKF_TICK1(0);
     // ---- 1. prediction (k_ekf_filter's arithmetic) ------------------------------------
     double sn = 0.0;
@@ -1229,6 +1387,11 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
     for (Walk2 w(tid, nth, n); w.e < P * n; w.next())
       sP[w.r * LDP + w.c] += sT * sP[(w.r + P) * LDP + w.c] + h2 * sP[(w.r + 2 * P) * LDP + w.c];
     __syncthreads();
+    // the one-joint FK's trig / translation tables from the predicted state (visible from here)
+    // by threads the covariance passes leave idle (visible to the FK items after the next
+    // barriers)
+    if (trig_early && tid >= trig_t0)
+      ekf_fk_trig_trans<F32>(sk, ss, d.eps, fkb, fkb + 4 * FK_MAXP, tid - trig_t0, nth - trig_t0);
     for (Walk2 w(tid, nth, n); w.e < P * n; w.next()) sP[(P + w.r) * LDP + w.c] += sT * sP[(w.r + 2 * P) * LDP + w.c];
     __syncthreads();
     for (Walk2 w(tid, nth, P); w.e < P * n; w.next())
@@ -1236,10 +1399,15 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
     __syncthreads();
     for (Walk2 w(tid, nth, P); w.e < P * n; w.next()) sP[w.r * LDP + P + w.c] += sT * sP[w.r * LDP + w.c + 2 * P];
     __syncthreads();
-    for (Walk2 w(tid, nth, n); w.e < n * n; w.next()) {
-      const double v = sP[w.r * LDP + w.c] + Q[w.e];
-      sP[w.r * LDP + w.c] = v;
-      Ppred[fo * n * n + w.e] = v;
+#pragma unroll
+    for (int k = 0; k < QR; ++k) {
+      const int e = tid + k * nth;
+      if (e < n * n) {
+        const int r = e / n, c = e - r * n;
+        const double v = sP[r * LDP + c] + (EKF_W1_PREFETCH ? qreg[k] : Q[e]);
+        sP[r * LDP + c] = v;
+        Ppred[fo * n * n + e] = v;
+      }
     }
     EKF_TICK1(1);
     // ---- 2. measurement model ---------------------------------------------------------
@@ -1263,13 +1431,21 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
       // observation) item computes its marker from them and projects it
       double* sc = fkb;                      // 4 x FK_MAXP
       double* rw = sc + 4 * FK_MAXP;         // (P+1) x 6
-      ekf_fk_trig_trans<F32>(sk, ss, d.eps, sc, rw, tid, nth);
-      __syncthreads();
+      if (!trig_early) {
+        ekf_fk_trig_trans<F32>(sk, ss, d.eps, sc, rw, tid, nth);
+        __syncthreads();
+      }
+#ifdef EKF_PROFILE
+      s_sub += clock64() - t_last;  // the trig / translation tables' share of the FK/proj phase
+#endif
       for (int e = tid; e < (P + 1) * CL; e += nth) {
         const int q = e / CL, o = e - q * CL;
         const int c = o / d.L, l = o - c * d.L;
         double x[3];
-        ekf_fk_point<F32>(sk, ss, d.eps, sc, rw, q, l, x);
+        if (pl.ok)
+          ekf_point_eval<F32>(pl, ss, d.eps, sc, rw, q, x);
+        else
+          ekf_fk_point<F32>(sk, ss, d.eps, sc, rw, q, l, x);
         ProjOut po;
         fisheye_project<false>(sCam + c * ACS_CAM_STRIDE, x[0], x[1], x[2], po);
         hp[(size_t)q * m + 2 * o] = po.u;
@@ -1292,13 +1468,19 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
     EKF_TICK1(2);
     for (int r = tid; r < m; r += nth) {
       const int o = r >> 1, c = o / d.L;
-      double e = meas[fo * fstride * 2 + r] - hp[r];
+      double e = (pf ? m_cur : meas[fo * fstride * 2 + r]) - hp[r];
       if (!isfinite(e)) e = (e != e) ? 0.0 : (e > 0 ? 1.7976931348623157e308 : -1.7976931348623157e308);
-      const double lk = lik[fo * fstride + o];
-      const double sd = (lk < d.thresh) ? d.maxpix : rbase[c];
+      const double lk = pf ? l_cur : lik[fo * fstride + o];
+      const bool mx = lk < d.thresh;
       sr[r] = e;
-      sw[r] = 1.0 / (sd * sd);
-      sd2[r] = sd * sd;
+      if (pf) {
+        sw[r] = mx ? w_mx : w_rb;
+        sd2[r] = mx ? s2_mx : s2_rb;
+      } else {
+        const double sd = mx ? d.maxpix : rbase[c];
+        sw[r] = 1.0 / (sd * sd);
+        sd2[r] = sd * sd;
+      }
     }
     // H rows (P entries in registers, stored together); analytic: both rows of an
     // observation from one d pos / d x_q
@@ -1519,8 +1701,10 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
     __syncthreads();
   }
 #ifdef EKF_PROFILE
-  if (tid == 0 && ekf_prof)
+  if (tid == 0 && ekf_prof) {
     for (int k = 0; k < 8; ++k) ekf_prof[seq * 8 + k] = s_prof[k];
+    if (seq == 0) ekf_prof[8] = s_sub;  // the profiling tool's ninth slot (one sequence)
+  }
 #endif
 #undef EKF_TICK1
   if ((tid & 63) == 0 && nout) atomicAdd(reinterpret_cast<unsigned long long*>(&s_nout), (unsigned long long)nout);

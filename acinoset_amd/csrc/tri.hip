@@ -91,11 +91,9 @@ __device__ void dlt_null4(double A[16], double out[4]) {
   for (int i = 0; i < 4; ++i) out[i] = V[i * 4 + best];
 }
 
-__device__ void triangulate_one(const double* ca, const double* cb, double ua, double va, double ub, double vb,
+// the DLT of one pair from both views' undistorted points
+__device__ void triangulate_und(const double* ca, const double* cb, double xa, double ya, double xb, double yb,
                                 double X[3]) {
-  double xa, ya, xb, yb;
-  fisheye_undistort(ca, ua, va, xa, ya);
-  fisheye_undistort(cb, ub, vb, xb, yb);
   // P = [R | t]; rows: x*P2 - P0, y*P2 - P1
   const double* Ra = ca + 8;
   const double* ta = ca + 17;
@@ -115,6 +113,14 @@ __device__ void triangulate_one(const double* ca, const double* cb, double ua, d
   X[0] = h[0] / h[3];
   X[1] = h[1] / h[3];
   X[2] = h[2] / h[3];
+}
+
+__device__ void triangulate_one(const double* ca, const double* cb, double ua, double va, double ub, double vb,
+                                double X[3]) {
+  double xa, ya, xb, yb;
+  fisheye_undistort(ca, ua, va, xa, ya);
+  fisheye_undistort(cb, ub, vb, xb, yb);
+  triangulate_und(ca, cb, xa, ya, xb, yb, X);
 }
 
 __global__ __launch_bounds__(256) void k_tri_pairs(const double* __restrict__ cams, int n_cams,
@@ -143,16 +149,30 @@ __global__ __launch_bounds__(256) void k_tri_dense(const double* __restrict__ ca
   if (p >= n_pts) return;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
   int n = 0;
+  // every observed view undistorted once: camera c's point serves the pairs (c - 1, c) and
+  // (c, c + 1) (triangulate_one undistorted it for both); camera 0's is kept for the last pair
+  const bool m0 = mask[p * C] != 0;
+  double x0 = 0.0, y0 = 0.0;
+  if (m0) fisheye_undistort(cams, uv[p * C * 2], uv[p * C * 2 + 1], x0, y0);
+  double xa = x0, ya = y0;
+  bool ma = m0;
   for (int c = 0; c < C; ++c) {
     const int c2 = (c + 1) % C;
-    if (!mask[p * C + c] || !mask[p * C + c2]) continue;
-    double X[3];
-    triangulate_one(cams + c * ACS_CAM_STRIDE, cams + c2 * ACS_CAM_STRIDE, uv[(p * C + c) * 2], uv[(p * C + c) * 2 + 1],
-                    uv[(p * C + c2) * 2], uv[(p * C + c2) * 2 + 1], X);
-    s0 += X[0];
-    s1 += X[1];
-    s2 += X[2];
-    ++n;
+    const bool mb = mask[p * C + c2] != 0;
+    double xb = x0, yb = y0;
+    if (c2 != 0 && mb)
+      fisheye_undistort(cams + c2 * ACS_CAM_STRIDE, uv[(p * C + c2) * 2], uv[(p * C + c2) * 2 + 1], xb, yb);
+    if (ma && mb) {
+      double X[3];
+      triangulate_und(cams + c * ACS_CAM_STRIDE, cams + c2 * ACS_CAM_STRIDE, xa, ya, xb, yb, X);
+      s0 += X[0];
+      s1 += X[1];
+      s2 += X[2];
+      ++n;
+    }
+    xa = xb;
+    ya = yb;
+    ma = mb;
   }
   const double nan = __builtin_nan("");
   out[3 * p] = n ? s0 / n : nan;

@@ -1,7 +1,8 @@
-"""A/B of the default-model RTS gains between two builds of the library: the smoothed states of
-a 12-camera ring clip (float64 and reference numerics), saved to OUT.npz. Run once per build
-(ACINOSET_HIP_LIB=<lib> python tools/ekf_gain_ab.py OUT.npz [frames]) and compare the files
-with --compare A.npz B.npz (bit-identical expected for a reorganised k_ekf_gain_t)."""
+"""A/B of the EKF between two builds of the library: the filtered and smoothed states of a
+12-camera ring clip (float64 and reference numerics), saved to OUT.npz. Run once per build
+(ACINOSET_HIP_LIB=<lib> python tools/ekf_gain_ab.py OUT.npz [frames] [mode]; mode 'default' (the
+RTS gains' A/B of round 5) or 'head') and compare the files with --compare A.npz B.npz
+(bit-identical expected for a reorganised kernel)."""
 import os
 import sys
 
@@ -25,11 +26,13 @@ from test_gpu_ekf import _setup_ring  # noqa: E402
 cekf = importlib.import_module('acinoset_amd.core.ekf')  # the module (the package re-exports a function of that name)
 
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 60
+mode = sys.argv[3] if len(sys.argv) > 3 else 'default'
 ctx = _native.Context(0)
-scene, seq, s0, cp, covs = _setup_ring('default', frames)
+scene, seq, s0, cp, covs = _setup_ring(mode, frames)
 out = {}
 for ref in (False, True):
-    r = cekf.run(seq.uv, seq.likelihood, cp, 'default', 90.0, s0, ref_numerics=ref, cal_covs=covs, ctx=ctx)
+    r = cekf.run(seq.uv, seq.likelihood, cp, mode, 90.0, s0, ref_numerics=ref, cal_covs=covs, ctx=ctx)
     out[f'x_smooth_ref{int(ref)}'] = r['x_smooth']
+    out[f'x_est_ref{int(ref)}'] = r['x_est']
 np.savez(sys.argv[1], **out)
 print('saved', sys.argv[1], {k: v.shape for k, v in out.items()})

@@ -23,7 +23,7 @@ n_cams = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 N = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 jac = sys.argv[4] if len(sys.argv) > 4 else 'fd'
 ctx = _native.Context(0)
-buf = torch.zeros(8, dtype=torch.int64, device='cuda')
+buf = torch.zeros(9, dtype=torch.int64, device='cuda')
 ctx.lib.acs_ekf_prof.argtypes = [C.c_void_p]
 ctx.lib.acs_ekf_prof(C.c_void_p(buf.data_ptr()))
 scene = synth.load_scene_file() if n_cams == 6 else synth.ring_scene(n_cams)
@@ -38,9 +38,12 @@ s0[0, P:2 * P] = (seq.x[1] - seq.x[0]) / seq.Ts
 ctx.ekf_run(table, cams, seq.uv[None], seq.likelihood[None],
             90.0, 0.5, float(scene.res[0]), cekf.measurement_std(n_cams, covs), cekf.process_covariance(P, 1 / 90.),
             cekf.initial_covariance(mode), s0, ref_numerics=jac == 'fd', jacobian=jac)
-v = buf.cpu().numpy() / N
+v9 = buf.cpu().numpy() / N
+v, sub = v9[:8], v9[8]
 names = ["predict+PFPt", "FK/proj", "H build", "A,G,b,outl", "aug", "GJ", "update", "store+FK-only"]
 print(f'{mode}, {n_cams} cams, {N} frames, one sequence, H: {jac}')
 for nm, x in zip(names, v):
     print(f'{nm:14s} {x:10.0f} cycles/frame  ({x / 2.4e3:.1f} us @2.4GHz)')
 print(f'{"total":14s} {v.sum():10.0f} cycles/frame  ({v.sum() / 2.4e3:.1f} us @2.4GHz)')
+if sub:  # k_ekf_filter_w1, one-joint skeletons: the trig / translation tables inside FK/proj
+    print(f'{"  FK/proj: trig":14s} {sub:10.0f} cycles/frame  ({sub / 2.4e3:.1f} us @2.4GHz)')
