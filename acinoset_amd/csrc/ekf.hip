@@ -1682,23 +1682,26 @@ __global__ __launch_bounds__(64 * NW) void k_ekf_filter_w1(EkfDims d, const int*
     __syncthreads();
     EKF_TICK1(6);
     // ---- 6. s += P[:, x] Z_b ; P -= P[:, x] Z_G ---------------------------------------
+    // (the outputs stored by the threads that form them: no store phase and no second barrier;
+    // 8.35 -> 8.19 us per frame, profiles/r06/bench_ekf_*_r06s.log)
     if (tid < n) {
       double v = 0.0;
 #pragma unroll
       for (int k = 0; k < P; ++k) v += sPx[tid * P + k] * sZ[k * NZ1 + n];
-      ss[tid] += v;
+      const double x = ss[tid] + v;
+      ss[tid] = x;
+      xest[fo * n + tid] = x;
     }
     for (Walk2 w(tid, nth, n); w.e < n * n; w.next()) {
       double v = 0.0;
 #pragma unroll
       for (int k = 0; k < P; ++k) v = fma(sPx[w.r * P + k], sZ[k * NZ1 + w.c], v);
-      sP[w.r * LDP + w.c] -= v;
+      const double x = sP[w.r * LDP + w.c] - v;
+      sP[w.r * LDP + w.c] = x;
+      Pest[fo * n * n + w.e] = x;
     }
     __syncthreads();
     EKF_TICK1(7);
-    if (tid < n) xest[fo * n + tid] = ss[tid];
-    for (Walk2 w(tid, nth, n); w.e < n * n; w.next()) Pest[fo * n * n + w.e] = sP[w.r * LDP + w.c];
-    __syncthreads();
   }
 #ifdef EKF_PROFILE
   if (tid == 0 && ekf_prof) {
