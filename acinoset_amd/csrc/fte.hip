@@ -644,8 +644,6 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
     const int ti = gi - (P + 6);
     if (ti >= 0 && ti < d.Cg) Tc[(size_t)k * tc_stride(d.Cg) + d.Cg * d.Cg + ti] = gacc;
   }
-  const double tot = block_sum(rho, s_red);
-  if (tid == 0) Floc[k] = tot;
   if (Fq) {  // the model stencil ending at row k + 2 (rows k-1 .. k+2), as k_fte_cost
     double q = 0.0;
     if (k >= 1) {
@@ -655,8 +653,15 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
         q += qinv[p] * sm * sm;
       }
     }
-    q = block_sum(q, s_red);
-    if (tid == 0) Fq[k] = q;
+    double v[2] = {rho, q};  // both sums on one set of barriers (each bit-identical to its block_sum)
+    block_sums<2>(v, s_red);
+    if (tid == 0) {
+      Floc[k] = v[0];
+      Fq[k] = v[1];
+    }
+  } else {
+    const double tot = block_sum(rho, s_red);
+    if (tid == 0) Floc[k] = tot;
   }
   LPROF(59);
 #ifdef FTE_PROFILE
