@@ -254,11 +254,11 @@ __device__ double block_max(double v, double* s_red) {
 __host__ __device__ __forceinline__ int tc_stride(int Cg) { return Cg * Cg + Cg; }
 
 struct LinLds {
-  int cam, am, qt, ac, cf, uni, tabR, tabI, total;
+  int cam, am, qt, ac, cf, uni, xr, tabR, tabI, total;
 };
 // dynamic LDS of k_fte_linearize (doubles): QW = the compact width of the Q rows (the
 // shift / delay columns 0..2 and P..NZ-1), nint / nreal the skeleton table's sizes
-__host__ __device__ __forceinline__ LinLds lin_lds(int C, int L, int NZP, int QW, int nint, int nreal) {
+__host__ __device__ __forceinline__ LinLds lin_lds(int C, int L, int P, int NZP, int QW, int nint, int nreal) {
   LinLds o;
   int p = 0;
   o.cam = p;
@@ -275,6 +275,8 @@ __host__ __device__ __forceinline__ LinLds lin_lds(int C, int L, int NZP, int QW
               // Q (3 LIN_MC x QW) | the block sums' scratch (256)
   const int a = 9 * LIN_OCH, b = 3 * LIN_MC * (2 * (NZP + 1) + QW);
   p += a > b ? (a > 256 ? a : 256) : (b > 256 ? b : 256);
+  o.xr = p;  // the frame's pose stencil: rows f - 3 .. f of X (FK reads row f, the model term all four)
+  p += 4 * P;
   o.tabR = p;  // skeleton table: reals, then ints
   p += nreal;
   o.tabI = p;
@@ -336,18 +338,16 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
     Floc += hb * d.N;
     Tc += hb * d.N * tc_stride(d.Cg);
   }
-  const int k = blockIdx.x + k0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
   const int P = d.P, C = d.C, L = d.L, NZ = d.NZ;
   const int NZP = (NZ + 15) & ~15, LD = NZP + 1, NT = NZP >> 4;
   const int cur = force ? 0 : (spec ? st->cur ^ 1 : st->cur);
   const double* X = Xbuf + (size_t)cur * d.M * P;
-  const double* tau = taubuf + (size_t)cur * d.NT + (d.var ? (size_t)k * C : 0);
   extern __shared__ double lds[];
   const int QW = 3 + NZ - P;  // compact Q rows: columns 0..2 and P..NZ-1
-  const LinLds lo = lin_lds(C, L, NZP, QW, d.nint, d.nreal);
+  const LinLds lo = lin_lds(C, L, P, NZP, QW, d.nint, d.nreal);
   double *s_cam = lds + lo.cam, *s_am = lds + lo.am, *s_qt = lds + lo.qt, *s_ac = lds + lo.ac, *s_cf = lds + lo.cf,
-         *s_u = lds + lo.uni;
+         *s_u = lds + lo.uni, *s_xr = lds + lo.xr;
   double* s_red = s_u;  // the block sums at the end (the operand rows are dead by then)
   int* s_tabI = reinterpret_cast<int*>(lds + lo.tabI);
   double* s_tabR = lds + lo.tabR;
@@ -356,11 +356,19 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
   __shared__ double s_dx[3], s_ddx[3];
   LPROF_T0
   // every input load in flight before the one barrier: the skeleton table (sizes from the
-  // host: no dependent header load), the cameras, the frame's position rows
+  // host: no dependent header load), the cameras, the frame's pose stencil rows f - 3 .. f (an
+  // LDS copy: FK reads row f, the model term all four; from global memory their round trip sat
+  // at FK's start and again before the closing sums) and the root's velocity / acceleration
   skel_copy(I, Rl, s_tabI, s_tabR, d.nint, d.nreal, tid, blockDim.x);
-  const int f = k + 2;
   for (int i = tid; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
+  const int k = blockIdx.x + k0;
+  const double* tau = taubuf + (size_t)cur * d.NT + (d.var ? (size_t)k * C : 0);
+  const int f = k + 2;
   for (int i = lo.am + tid; i < lo.cf; i += blockDim.x) lds[i] = 0.0;
+  for (int i = tid; i < 4 * P; i += blockDim.x) {
+    const int fr = f - 3 + i / P;  // row f - 3 is read by the model term only (k >= 1)
+    s_xr[i] = fr >= 0 ? X[(size_t)fr * P + i % P] : 0.0;
+  }
   if (tid < 3) {
     const double x0 = X[f * P + tid], x1 = X[(f - 1) * P + tid], x2 = X[(f - 2) * P + tid];
     s_dx[tid] = (x0 - x1) / d.Ts;
@@ -370,7 +378,7 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
   const SkelView s = skel_view(s_tabI, s_tabR);
   LPROF(61);
   LPROF(62);
-  fk_frame(s, X + f * P, fk, tid, blockDim.x);
+  fk_frame(s, s_xr + 3 * P, fk, tid, blockDim.x);
   __syncthreads();
   if (tid < P) fk_deriv_prep(s, fk, fkd, tid);  // read after the barriers of phase (a)
   LPROF(56);
@@ -649,7 +657,7 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
     if (k >= 1) {
       const double its2 = 1.0 / (d.Ts * d.Ts);
       for (int p = tid; p < P; p += blockDim.x) {
-        const double sm = (X[f * P + p] - 3.0 * X[(f - 1) * P + p] + 3.0 * X[(f - 2) * P + p] - X[(f - 3) * P + p]) * its2;
+        const double sm = (s_xr[3 * P + p] - 3.0 * s_xr[2 * P + p] + 3.0 * s_xr[P + p] - s_xr[p]) * its2;
         q += qinv[p] * sm * sm;
       }
     }
@@ -675,7 +683,7 @@ typedef void (*LinKernel)(FteDims, const int*, const double*, const double*, con
 static LinKernel lin_kernel(int nwg) { return nwg > 4 * 256 ? k_fte_linearize<5> : k_fte_linearize<4>; }
 
 static size_t lin_lds_bytes(const FteDims& d) {
-  return sizeof(double) * (size_t)lin_lds(d.C, d.L, (d.NZ + 15) & ~15, 3 + d.NZ - d.P, d.nint, d.nreal).total;
+  return sizeof(double) * (size_t)lin_lds(d.C, d.L, d.P, (d.NZ + 15) & ~15, 3 + d.NZ - d.P, d.nint, d.nreal).total;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2716,6 +2724,15 @@ struct FteBuffers {
   FteState* st;
 };
 
+// k_fte_linearize over frames [k0, k0 + nk) (spec: at the trial state, with the model terms in Fq)
+static void fte_launch_lin(const FteDims& d, hipStream_t s, const FteBuffers& b, int force, int k0, int nk, int spec,
+                           double* Fq, const double* qinv) {
+  const LinKernel kf = lin_kernel(nk);
+  const size_t lds = lin_lds_bytes(d);
+  hipLaunchKernelGGL(kf, dim3(nk), dim3(256), lds, s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
+                     b.st, force, k0, b.Hloc, b.gloc, b.Floc, spec, Fq, qinv, b.Tc);
+}
+
 struct FteSetup {
   FteState* snap = nullptr;  // pinned host slots the LM kernel writes its state into
   FteDims d;
@@ -3075,8 +3092,7 @@ static void cr_launch_assemble_build(const FteDims& d, hipStream_t s, const FteB
 static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
   const FteDims& d = S.d;
   FteBuffers& b = S.b;
-  hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X, b.tau,
-                     b.st, force, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr, b.Tc);
+  fte_launch_lin(d, s, b, force, 0, d.N, 0, (double*)nullptr, (const double*)nullptr);
   hipLaunchKernelGGL(k_fte_assemble, dim3(d.M), dim3(256), 0, s, d, b.X, b.tau, b.qinv, b.st, force, 0, 0, INT_MAX,
                      b.Hloc, b.gloc, b.Ab, b.gb, b.Bt, b.gmaxp, b.Adiag, 1);
 }
@@ -3145,8 +3161,7 @@ static void fte_enqueue_iteration(FteSetup& S, hipStream_t s, const FteOptsDev& 
                        b.normp, 1, 0, 1);
   // speculative linearisation at the trial state: its measurement terms and the model terms
   // are the trial cost (no separate cost pass)
-  hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
-                     b.X, b.tau, b.st, 0, 0, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv, b.Tc);
+  fte_launch_lin(d, s, b, 0, 0, d.N, 1, b.Fq, b.qinv);
   hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(FTE_LM_THREADS), 0, s, d, b.st, o, 0, b.Floc, b.Fq, b.normp, 1, S.snap);
 }
 
@@ -3584,8 +3599,7 @@ int acs_fte_solve(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints, const 
   hipLaunchKernelGGL(k_fte_lm, dim3(1), dim3(FTE_LM_THREADS), 0, s, d, b.st, o, 1, b.Fm, b.Fq, b.normp, 0);
   // the linearisation of the initial state (buffer cur = 0); later ones are speculative
   if (op.max_iters > 0)
-    hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w,
-                       b.X, b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr, b.Tc);
+    fte_launch_lin(d, s, b, 1, 0, d.N, 0, (double*)nullptr, (const double*)nullptr);
   ACS_HIP(ctx, hipGetLastError());
   // enqueue the iterations one ahead of the host: the host reads iteration n's status
   // snapshot (pinned slot n & 1, published with its iteration count, fte_snapshot) while
@@ -3773,8 +3787,7 @@ int acs_fte_debug_blocks(acs_ctx* ctx, const int32_t* skel_ints, int64_t n_ints,
   st0.lam = lam;
   st0.relin = 1;
   ACS_HIP(ctx, hipMemcpyAsync(b.st, &st0, sizeof(st0), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(lin_kernel(d.N), dim3(d.N), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams, b.meas, b.w, b.X,
-                     b.tau, b.st, 1, 0, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr, (const double*)nullptr, b.Tc);
+  fte_launch_lin(d, s, b, 1, 0, d.N, 0, (double*)nullptr, (const double*)nullptr);
   const int L = std::min((int)levels, d.nlev);
   // as the solve stores it (upper tiles) unless the assembled D itself is asked for
   cr_launch_assemble_build(d, s, b, 0, -1, 0, INT_MAX, -1, -1, nullptr, nullptr, L == 0 || !fte_d_upper(d) ? 1 : 0);
@@ -3983,9 +3996,7 @@ int acs_fte_dist_init(acs_fte_dist* h, double* payload) {
                      (const double*)b.Fm, (const double*)b.Fq, 0, 0, (const double*)nullptr, p3);
   // the linearisation of the starting state (copy 0); later ones are speculative (phase 3)
   if (h->a0 < d.nblk && h->k_hi > h->k_lo)
-    hipLaunchKernelGGL(lin_kernel(h->k_hi - h->k_lo), dim3(h->k_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
-                       b.meas, b.w, b.X, b.tau, b.st, 1, h->k_lo, b.Hloc, b.gloc, b.Floc, 0, (double*)nullptr,
-                       (const double*)nullptr, b.Tc);
+    fte_launch_lin(d, s, b, 1, h->k_lo, h->k_hi - h->k_lo, 0, (double*)nullptr, (const double*)nullptr);
   ACS_HIP(ctx, hipGetLastError());
   return dist_phase1_body(h, payload);
 }
@@ -4130,8 +4141,7 @@ static int dist_phase3_body(acs_fte_dist* h, double* p3) {
   // accepted step needs no new linearisation in phase 1
   const int l_hi = std::min(h->k_hi + 1, d.N);
   if (h->a0 < d.nblk && l_hi > h->k_lo)
-    hipLaunchKernelGGL(lin_kernel(l_hi - h->k_lo), dim3(l_hi - h->k_lo), dim3(256), lin_lds_bytes(d), s, d, b.I, b.Rl, b.cams,
-                       b.meas, b.w, b.X, b.tau, b.st, 0, h->k_lo, b.Hloc, b.gloc, b.Floc, 1, b.Fq, b.qinv, b.Tc);
+    fte_launch_lin(d, s, b, 0, h->k_lo, l_hi - h->k_lo, 1, b.Fq, b.qinv);
   const int q0 = std::max(h->k_lo + 1, 1), q1 = l_hi;
   const int t_hi = std::min(h->bend, d.nblk - 1) + 1;
   hipLaunchKernelGGL(k_dist_cost_pack, dim3(1), dim3(256), 0, s, b.st, 1, d.N, h->k_lo, h->k_hi, q0,
