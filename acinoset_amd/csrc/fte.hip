@@ -693,77 +693,160 @@ static size_t lin_lds_bytes(const FteDims& d) {
 // from the local blocks of frames f-2 (own rows), f-1 (prev) and f (prev2) that are owned
 // (lo <= k < hi), plus the exact third-difference model term of the stencils starting in
 // [lo, hi). Threads t < nth of the calling group work; every thread of the workgroup must
-// call it (it holds barriers). Fixed accumulation order (own, prev, prev2, model).
+// call it (it holds barriers). Fixed accumulation order per element: 0 + own + prev + prev2 +
+// model (a term that is not owned adds +0.0, which is exact: no partial sum is -0.0).
+// Every global load (own / prev / prev2 blocks, gradients, the stencil rows of X) is issued in
+// one round. Each element's own term is added where it is stored; after one barrier, thread
+// p < P finishes the diagonal entries of row p (prev / prev2 for p < 3, then the model term)
+// and the next threads the other entries that prev / prev2 touch (rows < 3 of blocks dd = 0, 1
+// and of B), with the terms they loaded in that round. (It was zero-fill, then one barrier and
+// one dependent global round trip per term: own, prev, prev2, model.)
 __device__ void assemble_row(const FteDims& d, int f, const double* __restrict__ X, const double* __restrict__ qinv,
                              int lo, int hi, const double* __restrict__ Hloc, const double* __restrict__ gloc,
                              double* A, double* g, double* B, int t, int nth) {
-  const int P = d.P, Cg = d.Cg, N = d.N;
-  for (int i = t; i < 4 * P * P; i += nth) A[i] = 0.0;
-  for (int i = t; i < P * Cg; i += nth) B[i] = 0.0;
-  for (int i = t; i < P; i += nth) g[i] = 0.0;
+  const int P = d.P, Cg = d.Cg, N = d.N, PP = P * P;
   const int kown = f - 2, kprev = f - 1, kprev2 = f;
   auto owned = [&](int k) { return k >= 0 && k < N && k >= lo && k < hi; };
-  __syncthreads();
-  if (owned(kown)) {
-    const double* H = Hloc + (size_t)kown * FTE_NZP * FTE_NZP;
-    for (int i = t; i < P * P; i += nth) {
-      const int r = i / P, c = i % P;
-      A[r * P + c] += H[r * FTE_NZP + c];
-    }
-    for (int i = t; i < P * 3; i += nth) {
-      const int r = i / 3, c = i % 3;
-      A[1 * P * P + r * P + c] += H[r * FTE_NZP + P + c];
-      A[2 * P * P + r * P + c] += H[r * FTE_NZP + P + 3 + c];
-    }
-    for (int i = t; i < P * Cg; i += nth) {
-      const int r = i / Cg, c = i % Cg;
-      B[r * Cg + c] += H[r * FTE_NZP + P + 6 + c];
-    }
-    for (int i = t; i < P; i += nth) g[i] += gloc[(size_t)kown * FTE_NZP + i];
-  }
-  __syncthreads();
-  if (owned(kprev)) {
-    const double* H = Hloc + (size_t)kprev * FTE_NZP * FTE_NZP;
-    for (int i = t; i < 9; i += nth) {
-      const int r = i / 3, c = i % 3;
-      A[r * P + c] += H[(P + r) * FTE_NZP + P + c];
-      A[1 * P * P + r * P + c] += H[(P + r) * FTE_NZP + P + 3 + c];
-    }
-    for (int i = t; i < 3 * Cg; i += nth) {
-      const int r = i / Cg, c = i % Cg;
-      B[r * Cg + c] += H[(P + r) * FTE_NZP + P + 6 + c];
-    }
-    for (int i = t; i < 3; i += nth) g[i] += gloc[(size_t)kprev * FTE_NZP + P + i];
-  }
-  __syncthreads();
-  if (owned(kprev2)) {
-    const double* H = Hloc + (size_t)kprev2 * FTE_NZP * FTE_NZP;
-    for (int i = t; i < 9; i += nth) {
-      const int r = i / 3, c = i % 3;
-      A[r * P + c] += H[(P + 3 + r) * FTE_NZP + P + 3 + c];
-    }
-    for (int i = t; i < 3 * Cg; i += nth) {
-      const int r = i / Cg, c = i % Cg;
-      B[r * Cg + c] += H[(P + 3 + r) * FTE_NZP + P + 6 + c];
-    }
-    for (int i = t; i < 3; i += nth) g[i] += gloc[(size_t)kprev2 * FTE_NZP + P + 3 + i];
-  }
-  __syncthreads();
-  // model term: stencils m in [3, M-1], s_m = (X_m - 3X_{m-1} + 3X_{m-2} - X_{m-3}) / Ts^2
+  const bool oo = owned(kown), op = owned(kprev), op2 = owned(kprev2);
+  const double* Ho = Hloc + (size_t)(oo ? kown : 0) * FTE_NZP * FTE_NZP;
+  const double* Hp = Hloc + (size_t)(op ? kprev : 0) * FTE_NZP * FTE_NZP;
+  const double* Hp2 = Hloc + (size_t)(op2 ? kprev2 : 0) * FTE_NZP * FTE_NZP;
   const double cf[4] = {1.0, -3.0, 3.0, -1.0};
   const double its2 = 1.0 / (d.Ts * d.Ts);
-  for (int p = t; p < P; p += nth) {
-    double gm = 0.0;
-    double hd[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int i = 0; i < 4; ++i) {
-      const int m = f + i;
-      if (m < 3 || m > d.M - 1 || m - 3 < lo || m - 3 >= hi) continue;
-      const double sm = (X[m * P + p] - 3.0 * X[(m - 1) * P + p] + 3.0 * X[(m - 2) * P + p] - X[(m - 3) * P + p]) * its2;
-      gm += 2.0 * qinv[p] * cf[i] * its2 * sm;
-      for (int dd = 0; dd < 4 && i + dd < 4; ++dd) hd[dd] += 2.0 * qinv[p] * cf[i] * cf[i + dd] * its2 * its2;
+  // model stencil m = f + i (rows m-3 .. m) is in the row's sums iff 3 <= m <= M-1, lo <= m-3 < hi
+  auto mvalid = [&](int i) {
+    const int m = f + i;
+    return !(m < 3 || m > d.M - 1 || m - 3 < lo || m - 3 >= hi);
+  };
+  // the second-round work of this thread and its loads: t < P the gradient entry and the
+  // diagonal of row t; then the off-diagonal entries (r, c < 3) of blocks dd = 0, 1 (6 each),
+  // then rows < 3 of B (3 Cg)
+  const int nOff = P + 12, nS = nOff + 3 * Cg;
+  double sg[3] = {0.0, 0.0, 0.0}, dg[3] = {0.0, 0.0, 0.0}, sq = 0.0, sx[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) sx[j] = 0.0;
+  int se = -1;  // the entry of A (< 4 PP) or B (>= 4 PP) thread t >= P finishes
+  if (t < P) {
+    sg[0] = oo ? gloc[(size_t)kown * FTE_NZP + t] : 0.0;
+    if (t < 3) {
+      sg[1] = op ? gloc[(size_t)kprev * FTE_NZP + P + t] : 0.0;
+      sg[2] = op2 ? gloc[(size_t)kprev2 * FTE_NZP + P + 3 + t] : 0.0;
+      dg[0] = op ? Hp[(P + t) * FTE_NZP + P + t] : 0.0;           // block 0, prev
+      dg[1] = op2 ? Hp2[(P + 3 + t) * FTE_NZP + P + 3 + t] : 0.0;  // block 0, prev2
+      dg[2] = op ? Hp[(P + t) * FTE_NZP + P + 3 + t] : 0.0;       // block 1, prev
     }
-    g[p] += gm;
-    for (int dd = 0; dd < 4; ++dd) A[dd * P * P + p * P + p] += hd[dd];
+    sq = qinv[t];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {  // rows f - 3 .. f + 3
+      const int row = f - 3 + j;
+      sx[j] = (row >= 0 && row <= d.M - 1) ? X[(size_t)row * P + t] : 0.0;
+    }
+  } else if (t < nOff) {
+    const int dd = (t - P) / 6, w = (t - P) % 6, r = w / 2, c = (w % 2 < r) ? w % 2 : w % 2 + 1;  // c != r
+    se = dd * PP + r * P + c;
+    if (dd == 0) {
+      dg[0] = op ? Hp[(P + r) * FTE_NZP + P + c] : 0.0;
+      dg[1] = op2 ? Hp2[(P + 3 + r) * FTE_NZP + P + 3 + c] : 0.0;
+    } else {
+      dg[0] = op ? Hp[(P + r) * FTE_NZP + P + 3 + c] : 0.0;
+    }
+  } else if (t < nS) {
+    const int w = t - nOff, r = w / Cg, c = w % Cg;
+    se = 4 * PP + w;
+    dg[0] = op ? Hp[(P + r) * FTE_NZP + P + 6 + c] : 0.0;
+    dg[1] = op2 ? Hp2[(P + 3 + r) * FTE_NZP + P + 6 + c] : 0.0;
+  }
+  // entries with an own term (block 0, columns < 3 of blocks 1, 2, and B): loads of a batch
+  // before its stores (k_fte_assemble's A is global memory)
+  const int n1 = PP + 6 * P, n2 = n1 + P * Cg;
+  constexpr int NBT = 4;
+  for (int e0 = t; e0 < n2; e0 += NBT * nth) {
+    double ov[NBT];
+#pragma unroll
+    for (int j = 0; j < NBT; ++j) {
+      const int u = e0 + j * nth;
+      double v = 0.0;
+      if (oo && u < n2) {
+        if (u < PP) {
+          const int r = u / P, c = u - r * P;
+          v = Ho[r * FTE_NZP + c];
+        } else if (u < n1) {
+          const int w = u - PP, r = w / 6, cc = w - 6 * r;  // block 1 + cc / 3, column cc % 3
+          v = Ho[r * FTE_NZP + P + cc];
+        } else {
+          const int w = u - n1, r = w / Cg, c = w - r * Cg;
+          v = Ho[r * FTE_NZP + P + 6 + c];
+        }
+      }
+      ov[j] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < NBT; ++j) {
+      const int u = e0 + j * nth;
+      if (u >= n2) break;
+      double v = 0.0;
+      v += ov[j];
+      if (u < PP) {
+        A[u] = v;
+      } else if (u < n1) {
+        const int w = u - PP, r = w / 6, cc = w - 6 * r;
+        A[(1 + cc / 3) * PP + r * P + cc % 3] = v;
+      } else {
+        B[u - n1] = v;
+      }
+    }
+  }
+  // entries with no own term: columns >= 3 of blocks 1, 2, and block 3
+  const int Q = P * (P - 3), n3 = 2 * Q + PP;
+  for (int u = t; u < n3; u += nth) {
+    int e;
+    if (u < 2 * Q) {
+      const int dd = 1 + u / Q, w = u - (dd - 1) * Q, r = w / (P - 3), c = 3 + w - r * (P - 3);
+      e = dd * PP + r * P + c;
+    } else {
+      e = 3 * PP + (u - 2 * Q);
+    }
+    A[e] = 0.0;
+  }
+  if (t < P) {  // the gradient entry: own, prev, prev2, then the model term's stencils
+    double gm = 0.0;
+    for (int i = 0; i < 4; ++i) {
+      if (!mvalid(i)) continue;
+      // stencil m = f + i reads rows m .. m - 3 = sx[i + 3] .. sx[i]
+      const double sm = (sx[i + 3] - 3.0 * sx[i + 2] + 3.0 * sx[i + 1] - sx[i]) * its2;
+      gm += 2.0 * sq * cf[i] * its2 * sm;
+    }
+    double v = 0.0;
+    v += sg[0];
+    v += sg[1];
+    v += sg[2];
+    v += gm;
+    g[t] = v;
+  }
+  __syncthreads();
+  if (t < P) {
+#pragma unroll
+    for (int dd = 0; dd < 4; ++dd) {
+      double* a = A + dd * PP + t * P + t;
+      double v = *a;
+      if (dd == 0) {
+        v += dg[0];
+        v += dg[1];
+      } else if (dd == 1) {
+        v += dg[2];
+      }
+      double h = 0.0;  // the model term's diagonal entry (stencils in ascending order)
+      for (int i = 0; i + dd < 4; ++i)
+        if (mvalid(i)) h += 2.0 * sq * cf[i] * cf[i + dd] * its2 * its2;
+      v += h;
+      *a = v;
+    }
+  } else if (se >= 0) {
+    double* a = se < 4 * PP ? A + se : B + (se - 4 * PP);
+    double v = *a;
+    v += dg[0];
+    v += dg[1];
+    *a = v;
   }
   __syncthreads();
 }
@@ -1029,7 +1112,7 @@ __global__ __launch_bounds__(1024) void k_cr_build(FteDims d, const FteState* __
 // damped in the reduced system with the summed raw diagonals), and the raw diagonal and
 // gradient of every row written to rdiag / graw (row layout f P + p) for the payload.
 template <int NB>
-__global__ __launch_bounds__(1024) void k_cr_assemble_build(FteDims d, const double* __restrict__ Xbuf,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_cr_assemble_build(FteDims d, const double* __restrict__ Xbuf,
                                                             const double* __restrict__ qinv,
                                                             const FteState* __restrict__ st,
                                                             const double* __restrict__ Hloc,
