@@ -701,6 +701,21 @@ static size_t lin_lds_bytes(const FteDims& d) {
 // and the next threads the other entries that prev / prev2 touch (rows < 3 of blocks dd = 0, 1
 // and of B), with the terms they loaded in that round. (It was zero-fill, then one barrier and
 // one dependent global round trip per term: own, prev, prev2, model.)
+// Compact row storage (CMP, k_cr_assemble_build's LDS rows): blocks 1 and 2 are zero outside their
+// columns < 3 and the diagonal, block 3 outside the diagonal, so a row keeps block 0 whole, the
+// columns < 3 of blocks 1, 2 (P x 3 each), and the diagonals of blocks 1..3 (rows >= 3 of blocks
+// 1, 2 and all of block 3 are read from there): PP + 9P doubles instead of 4 PP.
+struct RowCmp {
+  static __host__ __device__ __forceinline__ int size(int P) { return P * P + 9 * P; }
+  // entry (dd, r, c) of a compact row, or -1 for a structural zero
+  static __device__ __forceinline__ int at(int P, int dd, int r, int c) {
+    if (dd == 0) return r * P + c;
+    if (dd <= 2 && c < 3) return P * P + 3 * P * (dd - 1) + 3 * r + c;
+    if (r == c && (dd == 3 || r >= 3)) return P * P + 6 * P + P * (dd - 1) + r;
+    return -1;
+  }
+};
+template <bool CMP>
 __device__ void assemble_row(const FteDims& d, int f, const double* __restrict__ X, const double* __restrict__ qinv,
                              int lo, int hi, const double* __restrict__ Hloc, const double* __restrict__ gloc,
                              double* A, double* g, double* B, int t, int nth) {
@@ -790,14 +805,18 @@ __device__ void assemble_row(const FteDims& d, int f, const double* __restrict__
         A[u] = v;
       } else if (u < n1) {
         const int w = u - PP, r = w / 6, cc = w - 6 * r;
-        A[(1 + cc / 3) * PP + r * P + cc % 3] = v;
+        if constexpr (CMP)
+          A[PP + 3 * P * (cc / 3) + 3 * r + cc % 3] = v;
+        else
+          A[(1 + cc / 3) * PP + r * P + cc % 3] = v;
       } else {
         B[u - n1] = v;
       }
     }
   }
-  // entries with no own term: columns >= 3 of blocks 1, 2, and block 3
-  const int Q = P * (P - 3), n3 = 2 * Q + PP;
+  // entries with no own term: columns >= 3 of blocks 1, 2, and block 3 (the compact rows keep
+  // only their diagonals, which the second round writes)
+  const int Q = P * (P - 3), n3 = CMP ? 0 : 2 * Q + PP;
   for (int u = t; u < n3; u += nth) {
     int e;
     if (u < 2 * Q) {
@@ -827,8 +846,9 @@ __device__ void assemble_row(const FteDims& d, int f, const double* __restrict__
   if (t < P) {
 #pragma unroll
     for (int dd = 0; dd < 4; ++dd) {
-      double* a = A + dd * PP + t * P + t;
-      double v = *a;
+      double* a = A + (CMP ? RowCmp::at(P, dd, t, t) : dd * PP + t * P + t);
+      // (compact rows: the diagonal of blocks 1, 2 past row 2 and of block 3 was not stored)
+      double v = (CMP && dd > 0 && (dd == 3 || t >= 3)) ? 0.0 : *a;
       if (dd == 0) {
         v += dg[0];
         v += dg[1];
@@ -842,7 +862,12 @@ __device__ void assemble_row(const FteDims& d, int f, const double* __restrict__
       *a = v;
     }
   } else if (se >= 0) {
-    double* a = se < 4 * PP ? A + se : B + (se - 4 * PP);
+    int ea = se;
+    if (CMP && se < 4 * PP) {
+      const int dd = se / PP, r = (se - dd * PP) / P;
+      ea = RowCmp::at(P, dd, r, se - dd * PP - r * P);
+    }
+    double* a = se < 4 * PP ? A + ea : B + (se - 4 * PP);
     double v = *a;
     v += dg[0];
     v += dg[1];
@@ -905,7 +930,7 @@ __global__ __launch_bounds__(256) void k_fte_assemble(FteDims d, const double* _
     s_ti[j][c] = ti;
     s_tg[j][c] = tg;
   }
-  assemble_row(d, f, X, qinv, lo, hi, Hloc, gloc, A, g, B, tid, nth);
+  assemble_row<false>(d, f, X, qinv, lo, hi, Hloc, gloc, A, g, B, tid, nth);
   double mx = 0.0;
   for (int i = tid; i < P; i += nth) mx = fmax(mx, fabs(g[i]));
   double mt = 0.0;
@@ -1111,43 +1136,60 @@ __global__ __launch_bounds__(1024) void k_cr_build(FteDims d, const FteState* __
 // rank owns (lowest row in [lo, hi)), the chain ends end_l / end_r left undamped (they are
 // damped in the reduced system with the summed raw diagonals), and the raw diagonal and
 // gradient of every row written to rdiag / graw (row layout f P + p) for the payload.
-template <int NB>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_cr_assemble_build(FteDims d, const double* __restrict__ Xbuf,
-                                                            const double* __restrict__ qinv,
-                                                            const FteState* __restrict__ st,
-                                                            const double* __restrict__ Hloc,
-                                                            const double* __restrict__ gloc, double* __restrict__ Dc,
-                                                            double* __restrict__ Ec, double* __restrict__ GBc,
-                                                            double* __restrict__ gmaxp, int b0, int lo, int hi,
-                                                            int end_l, int end_r, double* __restrict__ rdiag,
-                                                            double* __restrict__ graw, int d_full) {
+// TH threads per block (16 x 16 TH / 1024 waves per SIMD's register budget): 1024 when the grid
+// fits the chip in one round of two blocks per CU (each row assembled by 320 threads: the
+// shortest block), 512 for larger grids (four blocks per CU hide each other's latency:
+// 10,000 frames 111.8 -> 99.4 us; at 1,000 frames the 512-thread block takes 21.9 us against
+// 17.8, profiles/r06/fte_kernel_totals_*_r06y.log)
+template <int NB, int TH>
+__global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(8))) void k_cr_assemble_build(
+    FteDims d, const double* __restrict__ Xbuf, const double* __restrict__ qinv, const FteState* __restrict__ st,
+    const double* __restrict__ Hloc, const double* __restrict__ gloc, double* __restrict__ Dc,
+    double* __restrict__ Ec, double* __restrict__ GBc, double* __restrict__ gmaxp, int b0, int lo, int hi,
+    int end_l, int end_r, double* __restrict__ rdiag, double* __restrict__ graw, int d_full) {
   if (st->status != 0) return;
-  constexpr int BP = 16 * NB, NE = (BP * BP + 1023) / 1024;
+  constexpr int BP = 16 * NB;
   const int i = blockIdx.x + b0, tid = threadIdx.x;
   const bool damp = i != end_l && i != end_r;
-  const int P = d.P, PP = P * P, GR = d.GR, Cg = d.Cg;
+  const int P = d.P, GR = d.GR, Cg = d.Cg;
   const int cur = st->cur;
   Hloc += (size_t)cur * d.N * FTE_NZP * FTE_NZP;
   gloc += (size_t)cur * d.N * FTE_NZP;
   const double* X = Xbuf + (size_t)cur * d.M * P;
   const double lam = st->lam;
   extern __shared__ double lds[];
-  const int rowsz = 4 * PP + P + P * Cg;  // per row: A (4 P x P), g (P), B (P x Cg)
+  // per row: A (4 P x P; CMP: the compact layout, RowCmp), g (P), B (P x Cg). CMP (the 512-thread
+  // instance): 26 KB for the three rows at P = 26, six cameras instead of 69 KB, so four blocks
+  // share a CU. The 1024-thread instance keeps the full rows: the compact layout's index
+  // arithmetic cost it 17.3 -> 19.5 us per block (profiles/r06/fte_kernel_totals_*_r06z.log).
+  constexpr bool CMP = TH < 1024;
+  const int asz = CMP ? RowCmp::size(P) : 4 * P * P;
+  const int rowsz = asz + P + P * Cg;
   auto rowA = [&](int a) { return lds + (size_t)a * rowsz; };
-  auto rowg = [&](int a) { return lds + (size_t)a * rowsz + 4 * PP; };
-  auto rowB = [&](int a) { return lds + (size_t)a * rowsz + 4 * PP + P; };
+  auto rowg = [&](int a) { return lds + (size_t)a * rowsz + asz; };
+  auto rowB = [&](int a) { return lds + (size_t)a * rowsz + asz + P; };
+  // block (dd) entry (r, c) of row a (zero where the compact layout stores nothing)
+  auto rowAt = [&](int a, int dd, int r, int c) {
+    if constexpr (CMP) {
+      const int e = RowCmp::at(P, dd, r, c);
+      return e >= 0 ? rowA(a)[e] : 0.0;
+    } else {
+      return rowA(a)[dd * P * P + r * P + c];
+    }
+  };
   __shared__ int s_a[BP], s_p[BP];
-  if (tid < BP) {
-    s_a[tid] = tid / P;
-    s_p[tid] = tid - (tid / P) * P;
+  for (int r = tid; r < BP; r += blockDim.x) {
+    s_a[r] = r / P;
+    s_p[r] = r - (r / P) * P;
   }
   {
-    const int grp = tid / 320, a = grp < 3 ? grp : 0;
+    constexpr int GT = TH / 3 / 32 * 32;  // threads per row (320, 160)
+    const int grp = tid / GT, a = grp < 3 ? grp : 0;
     const int f = 3 * i + a;
     const bool act = grp < 3 && f < d.M;
-    // inactive threads (the 64 spare ones, rows past the sequence) start past every loop
-    assemble_row(d, f, X, qinv, lo, hi, Hloc, gloc, rowA(a), rowg(a), rowB(a), act ? tid - 320 * grp : 1 << 30,
-                 320);
+    // inactive threads (the spare ones, rows past the sequence) start past every loop
+    assemble_row<CMP>(d, f, X, qinv, lo, hi, Hloc, gloc, rowA(a), rowg(a), rowB(a), act ? tid - GT * grp : 1 << 30,
+                      GT);
   }
   if (rdiag && tid < 3 * d.P) {
     const int a = tid / d.P, p = tid - a * d.P, f = 3 * i + a;
@@ -1167,9 +1209,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   double* D = Dc + (size_t)i * BP * BP;
   double* E = Ec + (size_t)i * BP * BP;
   double* G = GBc + (size_t)i * BP * GR;
+  constexpr int NE = (BP * BP + TH - 1) / TH;
 #pragma unroll
   for (int q = 0; q < NE; ++q) {
-    const int e = tid + 1024 * q;
+    const int e = tid + TH * q;
     if (e >= BP * BP) continue;
     const int r = e / BP, c = e - (e / BP) * BP;
     const int ar = s_a[r], pr = s_p[r], ac = s_a[c], pc = s_p[c];
@@ -1177,7 +1220,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const bool rin = r < 3 * P && fr < d.M, cin = c < 3 * P && fc < d.M;
     double dv = 0.0, ev = 0.0;
     if (rin && cin) {
-      double v = (ar >= ac) ? rowA(ar)[(ar - ac) * PP + pr * P + pc] : rowA(ac)[(ac - ar) * PP + pc * P + pr];
+      double v = (ar >= ac) ? rowAt(ar, ar - ac, pr, pc) : rowAt(ac, ac - ar, pc, pr);
       if (r == c && damp) v += lam * fmax(v, 1e-12);
       dv = v;
     } else if (r == c) {
@@ -1187,7 +1230,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const int fe = 3 * (i - 1) + ac;
     if (i > 0 && rin && c < 3 * P && fe < d.M) {
       const int dist = 3 + ar - ac;
-      if (dist <= 3) ev = rowA(ar)[dist * PP + pr * P + pc];
+      if (dist <= 3) ev = rowAt(ar, dist, pr, pc);
     }
     // D is symmetric by construction (element (r, c) and (c, r) are the same row-block entry):
     // the single-GPU solve stores its upper 16 x 16 tiles only and the levels that read it as
@@ -1215,8 +1258,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   }
 }
 
-static size_t asm_build_lds_bytes(const FteDims& d) {
-  return sizeof(double) * 3 * (size_t)(4 * d.P * d.P + d.P + d.P * d.Cg);
+static size_t asm_build_lds_bytes(const FteDims& d, bool cmp) {
+  return sizeof(double) * 3 * (size_t)((cmp ? RowCmp::size(d.P) : 4 * d.P * d.P) + d.P + d.P * d.Cg);
 }
 
 static void cr_launch_build(const FteDims& d, hipStream_t s, int nblk, const FteState* st, const double* Ab,
@@ -3157,10 +3200,21 @@ static void cr_launch_assemble_build(const FteDims& d, hipStream_t s, const FteB
                                      double* rdiag = nullptr, double* graw = nullptr, int d_full = 0) {
   if (nblk < 0) nblk = d.nblk;
   if (nblk <= 0) return;
-#define CR_ABUILD(nb)                                                                                          \
-  hipLaunchKernelGGL((k_cr_assemble_build<nb>), dim3(nblk), dim3(1024), asm_build_lds_bytes(d), s, d, b.X, \
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }();
+  const bool wide = nblk > 2 * n_cu;  // more than one round of 1024-thread blocks
+#define CR_ABUILD_(nb, th)                                                                                  \
+  hipLaunchKernelGGL((k_cr_assemble_build<nb, th>), dim3(nblk), dim3(th), asm_build_lds_bytes(d, th < 1024), s, d, b.X, \
                      b.qinv, b.st, b.Hloc, b.gloc, b.Dc, b.Ec, b.GBc, b.gmaxp, b0, lo, hi, end_l, end_r, rdiag, graw, \
                      d_full)
+#define CR_ABUILD(nb)         \
+  if (wide)                   \
+    CR_ABUILD_(nb, 512);      \
+  else                        \
+    CR_ABUILD_(nb, 1024)
   switch (d.BP >> 4) {
     case 1: CR_ABUILD(1); break;
     case 2: CR_ABUILD(2); break;
@@ -3170,6 +3224,7 @@ static void cr_launch_assemble_build(const FteDims& d, hipStream_t s, const FteB
     default: CR_ABUILD(6); break;
   }
 #undef CR_ABUILD
+#undef CR_ABUILD_
 }
 
 static void fte_enqueue_linearize(FteSetup& S, hipStream_t s, int force) {
