@@ -19,7 +19,11 @@ for line in open(sys.argv[2]):
             break
         continue
     name, grid, us = m.group(1), int(m.group(3)), float(m.group(4))
-    e = pl.get(f'{name}@{grid * BLOCK.get(name, 256)}')
+    block = BLOCK.get(name, 256)
+    targs = [a.strip() for a in (m.group(2) or '<>')[1:-1].split(',')]
+    if name == 'k_cr_assemble_build' and len(targs) == 2:  # <NB, threads> since round 6
+        block = int(targs[1])
+    e = pl.get(f'{name}@{grid * block}')
     if e is None:
         rows.append((name, grid, us, None, None))
         continue

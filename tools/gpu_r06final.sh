@@ -5,4 +5,4 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${TAG:-r06final} bash tools/gpu_r06d.sh || exit $?
 cp gpurun_out/fte_iter_1k.json gpurun_out/fte_iter_10k.json profiles/r06/
-TAG=${TAG:-r06final} STEPS="test smoke bench prof pmc" bash tools/gpu_session.sh
+TAG=${TAG:-r06final} STEPS="test,smoke,bench,prof,pmc" bash tools/gpu_session.sh
