@@ -9,7 +9,9 @@ oracle to solve the whole problem:
 * configs[3] shape (6 cameras x 10,000 frames FTE): the single-GPU solve equals the
   frame-window decomposition of the 8-GPU path run on one GPU (dist.fte_solve_virtual,
   8 emulated ranks: same iterations, X within 1e-9 m), and its reprojection RMS is at
-  the noise level.
+  the noise level. The 2-rank decomposition too: its windows of 1,667 super-blocks take the
+  512-thread compact-row assembly (more blocks than two rounds of the CUs), the 8-rank ones
+  the 1,024-thread instance.
 """
 import numpy as np
 import pytest
@@ -38,6 +40,28 @@ def test_sba_configs4_sample_matches_oracle(ctx):
     assert float(np.abs(pts[sel] - ref).max()) < 1e-7
     # the solution is a better fit to the truth than the perturbed start (2 cm)
     assert np.sqrt(np.mean(np.sum((pts - truth) ** 2, 1))) < 0.5 * np.sqrt(np.mean(np.sum((pts0 - truth) ** 2, 1)))
+
+
+def _configs3_problem(N=10000):
+    scene = synth.load_scene_file()
+    seq = synth.make_sequence(N, scene, mode='default_nolure', seed=77, tau_max=0.004)
+    w = np.where(seq.likelihood > 0.5, 1.0 / 3.0, 0.0)
+    prob = ofte.Problem('default_nolure', seq.uv, w, scene.K, scene.D, scene.R, scene.t, seq.Ts, sd=True,
+                        intermode='vel')
+    cams = _native.pack_cameras(scene.K, scene.D, scene.R, scene.t)
+    X0 = ofte.initial_state(prob, np.arange(N), seq.pos3d[:, 0, 0])
+    return prob, cams, X0, pkin.build_table('default_nolure')
+
+
+def test_fte_configs3_single_equals_2_window_decomposition(ctx):
+    prob, cams, X0, table = _configs3_problem()
+    X1, t1, r1 = ctx.fte_solve(table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0)
+    assert r1['status_name'] in ('ftol', 'xtol', 'gtol') and r1['n_bad_pivots'] == 0, r1
+    Xd, td, rd = dist.fte_solve_virtual(ctx, table, cams, prob.meas, prob.w, prob.Ts, prob.qinv, X0, world=2)
+    assert rd['iters'] == r1['iters'] and rd['n_accepted'] == r1['n_accepted'], (rd, r1)
+    assert abs(rd['cost_after'] - r1['cost_after']) <= 1e-11 * r1['cost_after']
+    np.testing.assert_allclose(Xd, X1, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(td, t1, rtol=0, atol=1e-12)
 
 
 def test_fte_configs3_single_equals_8_window_decomposition(ctx):

@@ -1,8 +1,8 @@
 """Bit-for-bit A/B of FTE solves between two builds of the library (ACINOSET_HIP_LIB picks the
 one under test): python tools/ab_fte_bits.py save TAG  (writes gpurun_out/fte_bits_TAG.npz),
 python tools/ab_fte_bits.py cmp TAG_A TAG_B. Cases: the single-GPU solve at 1,000 and 10,000
-frames (const delays), the variable-delay solve at 300 frames and the 3-window virtual
-frame-window solve at 600 frames (k_fte_assemble's path)."""
+frames (const delays), the variable-delay solve at 300 frames, the 3-window virtual
+frame-window solve at 600 frames and the 2-window one at 4,000 frames."""
 import os
 import sys
 
@@ -27,6 +27,11 @@ def save(tag):
     seq, cams, meas, w, X0, table, qinv = bench._fte_problem(ctx, 600)
     X, tau, rep = dist.fte_solve_virtual(ctx, table, cams, meas, w, seq.Ts, qinv, X0, world=3)
     res['Xwin'], res['tauwin'] = X, tau
+    # 2 windows of 4,000 frames: 667 super-blocks per rank, more than two rounds of the CUs
+    # (the 512-thread compact-row assembly with the ranks' raw diagonals)
+    seq, cams, meas, w, X0, table, qinv = bench._fte_problem(ctx, 4000)
+    X, tau, rep = dist.fte_solve_virtual(ctx, table, cams, meas, w, seq.Ts, qinv, X0, world=2)
+    res['Xwin2'], res['tauwin2'] = X, tau
     os.makedirs(OUT, exist_ok=True)
     np.savez(os.path.join(OUT, f'fte_bits_{tag}.npz'), **res)
     print(tag, {k: (v.shape, float(np.abs(v).sum())) for k, v in res.items()})
