@@ -355,22 +355,46 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
   __shared__ FkDeriv fkd;
   __shared__ double s_dx[3], s_ddx[3];
   LPROF_T0
-  // every input load in flight before the one barrier: the skeleton table (sizes from the
-  // host: no dependent header load), the cameras, the frame's pose stencil rows f - 3 .. f (an
-  // LDS copy: FK reads row f, the model term all four; from global memory their round trip sat
-  // at FK's start and again before the closing sums) and the root's velocity / acceleration
-  skel_copy(I, Rl, s_tabI, s_tabR, d.nint, d.nreal, tid, blockDim.x);
-  for (int i = tid; i < C * ACS_CAM_STRIDE; i += blockDim.x) s_cam[i] = cams[i];
+  // every input load in flight before the first LDS store and the one barrier: the skeleton
+  // table (sizes from the host: no dependent header load), the cameras, the frame's pose stencil
+  // rows f - 3 .. f (an LDS copy: FK reads row f, the model term all four; from global memory
+  // their round trip sat at FK's start and again before the closing sums), the root's velocity /
+  // acceleration and the shutter delays (slot 6 of each camera's coefficients; after FK they
+  // were a round trip of their own). Each thread gathers its elements into registers first:
+  // copy loops of the form `for (i = tid; ..) lds[i] = g[i]` waited for every load before the
+  // next loop's were issued, a chain of global round trips (2.4-3.3 us to the table staged,
+  // profiles/r06/lin_phases_r06v_*.log). blockDim = 256.
   const int k = blockIdx.x + k0;
   const double* tau = taubuf + (size_t)cur * d.NT + (d.var ? (size_t)k * C : 0);
   const int f = k + 2;
-  for (int i = lo.am + tid; i < lo.cf; i += blockDim.x) lds[i] = 0.0;
-  for (int i = tid; i < 4 * P; i += blockDim.x) {
-    const int fr = f - 3 + i / P;  // row f - 3 is read by the model term only (k >= 1)
-    s_xr[i] = fr >= 0 ? X[(size_t)fr * P + i % P] : 0.0;
-  }
+  constexpr int NTH = 256, NIQ = (FK_MAX_INTS + NTH - 1) / NTH, NCQ = (FTE_MAXC * ACS_CAM_STRIDE + NTH - 1) / NTH;
+  static_assert(3 * FK_MAXN <= NTH && 4 * FK_MAXP <= NTH && FTE_MAXC <= NTH, "one element per thread");
+  int iv[NIQ];
+  double cv[NCQ], rv = 0.0, xv = 0.0, tv = 0.0, x0 = 0.0, x1 = 0.0, x2 = 0.0;
+#pragma unroll
+  for (int q = 0; q < NIQ; ++q) iv[q] = tid + NTH * q < d.nint ? I[tid + NTH * q] : 0;
+  if (tid < d.nreal) rv = Rl[tid];
+#pragma unroll
+  for (int q = 0; q < NCQ; ++q) cv[q] = tid + NTH * q < C * ACS_CAM_STRIDE ? cams[tid + NTH * q] : 0.0;
+  const int fr = f - 3 + tid / P;  // row f - 3 is read by the model term only (k >= 1)
+  if (tid < 4 * P && fr >= 0) xv = X[(size_t)fr * P + tid % P];
+  if (tid < C && d.Ct) tv = tau[tid];
   if (tid < 3) {
-    const double x0 = X[f * P + tid], x1 = X[(f - 1) * P + tid], x2 = X[(f - 2) * P + tid];
+    x0 = X[f * P + tid];
+    x1 = X[(f - 1) * P + tid];
+    x2 = X[(f - 2) * P + tid];
+  }
+  for (int i = lo.am + tid; i < lo.cf; i += blockDim.x) lds[i] = 0.0;
+#pragma unroll
+  for (int q = 0; q < NIQ; ++q)
+    if (tid + NTH * q < d.nint) s_tabI[tid + NTH * q] = iv[q];
+  if (tid < d.nreal) s_tabR[tid] = rv;
+#pragma unroll
+  for (int q = 0; q < NCQ; ++q)
+    if (tid + NTH * q < C * ACS_CAM_STRIDE) s_cam[tid + NTH * q] = cv[q];
+  if (tid < 4 * P) s_xr[tid] = xv;
+  if (tid < C) s_cf[7 * tid + 6] = tv;
+  if (tid < 3) {
     s_dx[tid] = (x0 - x1) / d.Ts;
     s_ddx[tid] = (x0 - 2.0 * x1 + x2) / (d.Ts * d.Ts);
   }
@@ -383,7 +407,7 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
   if (tid < P) fk_deriv_prep(s, fk, fkd, tid);  // read after the barriers of phase (a)
   LPROF(56);
   if (tid < C) {
-    const double tc = d.Ct ? tau[tid] : 0.0;
+    const double tc = s_cf[7 * tid + 6];
     const ShiftCoef sc = shift_coef(d.im, tc, d.Ts);
     double* cf = s_cf + 7 * tid;
     cf[0] = sc.own;
@@ -414,11 +438,14 @@ __global__ __launch_bounds__(256, WPC) void k_fte_linearize(FteDims d, const int
         if (d.im >= 1) sh[i] += s_dx[i] * tc;
         if (d.im == 2) sh[i] += s_ddx[i] * (tc * tc);
       }
+      // the weight and both measurements in one round trip, issued before the projection (the
+      // measurements loaded only where the weight is nonzero waited for the weight's load first;
+      // the select gives the same values)
+      const size_t mi = ((size_t)k * C + c) * L + l;
+      const double wt = wts[mi], mu0 = meas[2 * mi], mv0 = meas[2 * mi + 1];
       ProjOut po;
       fisheye_project<true, true>(s_cam + c * ACS_CAM_STRIDE, p[0] + sh[0], p[1] + sh[1], p[2] + sh[2], po);
-      const size_t mi = ((size_t)k * C + c) * L + l;
-      const double wt = wts[mi];
-      const double mu = wt != 0.0 ? meas[2 * mi] : 0.0, mv = wt != 0.0 ? meas[2 * mi + 1] : 0.0;
+      const double mu = wt != 0.0 ? mu0 : 0.0, mv = wt != 0.0 ? mv0 : 0.0;
       const bool ok = wt != 0.0;
       double* z = s_u + 9 * tid;
       for (int i = 0; i < 9; ++i) z[i] = 0.0;
@@ -2679,10 +2706,10 @@ __global__ __launch_bounds__(64) void k_fte_cost(FteDims d, const int* __restric
       if (d.im == 2) p[i] += s_ddx[i] * (tc * tc);
     }
     ProjOut po;
-    fisheye_project<false, true>(cams + c * ACS_CAM_STRIDE, p[0], p[1], p[2], po);
     const size_t mi = ((size_t)k * C + c) * L + l;
-    const double wt = wts[mi];
-    const double mu = wt != 0.0 ? meas[2 * mi] : 0.0, mv = wt != 0.0 ? meas[2 * mi + 1] : 0.0;
+    const double wt = wts[mi], mu0 = meas[2 * mi], mv0 = meas[2 * mi + 1];  // one round trip
+    fisheye_project<false, true>(cams + c * ACS_CAM_STRIDE, p[0], p[1], p[2], po);
+    const double mu = wt != 0.0 ? mu0 : 0.0, mv = wt != 0.0 ? mv0 : 0.0;
     rho += redescending(wt * (po.u - mu), d.la, d.lb, d.lc).f + redescending(wt * (po.v - mv), d.la, d.lb, d.lc).f;
   }
   double q = 0.0;
