@@ -763,40 +763,107 @@ __device__ void assemble_row(const FteDims& d, int f, const double* __restrict__
   // the second-round work of this thread and its loads: t < P the gradient entry and the
   // diagonal of row t; then the off-diagonal entries (r, c < 3) of blocks dd = 0, 1 (6 each),
   // then rows < 3 of B (3 Cg)
-  const int nOff = P + 12, nS = nOff + 3 * Cg;
   double sg[3] = {0.0, 0.0, 0.0}, dg[3] = {0.0, 0.0, 0.0}, sq = 0.0, sx[7];
 #pragma unroll
   for (int j = 0; j < 7; ++j) sx[j] = 0.0;
-  int se = -1;  // the entry of A (< 4 PP) or B (>= 4 PP) thread t >= P finishes
-  if (t < P) {
-    sg[0] = oo ? gloc[(size_t)kown * FTE_NZP + t] : 0.0;
-    if (t < 3) {
-      sg[1] = op ? gloc[(size_t)kprev * FTE_NZP + P + t] : 0.0;
-      sg[2] = op2 ? gloc[(size_t)kprev2 * FTE_NZP + P + 3 + t] : 0.0;
-      dg[0] = op ? Hp[(P + t) * FTE_NZP + P + t] : 0.0;           // block 0, prev
-      dg[1] = op2 ? Hp2[(P + 3 + t) * FTE_NZP + P + 3 + t] : 0.0;  // block 0, prev2
-      dg[2] = op ? Hp[(P + t) * FTE_NZP + P + 3 + t] : 0.0;       // block 1, prev
-    }
-    sq = qinv[t];
+  int se = -1;  // the entry of A (< 4 PP) or B (>= 4 PP) a second-round thread finishes
+  if constexpr (CMP) {
+    // The gradient specials are threads t < P (the first wave of the row's group); the others
+    // start at the second wave (S0), each with one load pair at offsets formed by selects, so no
+    // wave holds two of these load branches (the compiler waited for a branch's loads before the
+    // next branch's, a round trip per branch of one wave).
+    constexpr int S0 = 64;
+    const int nS1 = 12 + 3 * Cg;  // nth >= S0 + nS1 (<= 124: 16 delays)
+    if (t < P) {
+      // every load unconditional (valid clamped addresses), the terms that do not apply selected
+      // to zero after: nested load branches were waited for one after the other
+      const int t3 = t < 3 ? t : 0;
+      const size_t ko = oo ? kown : 0, kp = op ? kprev : 0, kp2 = op2 ? kprev2 : 0;
+      const double g0 = gloc[ko * FTE_NZP + t], g1 = gloc[kp * FTE_NZP + P + t3], g2 = gloc[kp2 * FTE_NZP + P + 3 + t3];
+      const double h0 = Hp[(P + t3) * FTE_NZP + P + t3];           // block 0, prev
+      const double h1 = Hp2[(P + 3 + t3) * FTE_NZP + P + 3 + t3];  // block 0, prev2
+      const double h2 = Hp[(P + t3) * FTE_NZP + P + 3 + t3];       // block 1, prev
+      sq = qinv[t];
+      double xr[7];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {  // rows f - 3 .. f + 3
-      const int row = f - 3 + j;
-      sx[j] = (row >= 0 && row <= d.M - 1) ? X[(size_t)row * P + t] : 0.0;
+      for (int j = 0; j < 7; ++j) {  // rows f - 3 .. f + 3
+        const int row = f - 3 + j;
+        xr[j] = X[(size_t)(row < 0 ? 0 : (row > d.M - 1 ? d.M - 1 : row)) * P + t];
+      }
+      sg[0] = oo ? g0 : 0.0;
+      sg[1] = (op && t < 3) ? g1 : 0.0;
+      sg[2] = (op2 && t < 3) ? g2 : 0.0;
+      dg[0] = (op && t < 3) ? h0 : 0.0;
+      dg[1] = (op2 && t < 3) ? h1 : 0.0;
+      dg[2] = (op && t < 3) ? h2 : 0.0;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        const int row = f - 3 + j;
+        sx[j] = (row >= 0 && row <= d.M - 1) ? xr[j] : 0.0;
+      }
+    } else if (t >= S0 && t < S0 + nS1) {
+      // off-diagonal entries (r, c < 3, c != r) of block dd = 0 (prev and prev2 terms) and dd = 1
+      // (prev), then rows < 3 of B (prev and prev2): prev at column P + ca of row P + r, prev2 at
+      // column P + cb of row P + 3 + r
+      const int w = t - S0;
+      int r, ca, cb;
+      bool p2on;
+      if (w < 12) {
+        const int dd = w / 6, ww = w % 6;
+        r = ww / 2;
+        const int c = (ww % 2 < r) ? ww % 2 : ww % 2 + 1;  // c != r
+        se = dd * PP + r * P + c;
+        ca = dd == 0 ? c : 3 + c;
+        cb = 3 + c;
+        p2on = dd == 0;
+      } else {
+        const int wb = w - 12;
+        r = wb / Cg;
+        const int c = wb - r * Cg;
+        se = 4 * PP + wb;
+        ca = 6 + c;
+        cb = 6 + c;
+        p2on = true;
+      }
+      const double a1 = Hp[(P + r) * FTE_NZP + P + ca], a2 = Hp2[(P + 3 + r) * FTE_NZP + P + cb];
+      dg[0] = op ? a1 : 0.0;
+      dg[1] = (op2 && p2on) ? a2 : 0.0;
     }
-  } else if (t < nOff) {
-    const int dd = (t - P) / 6, w = (t - P) % 6, r = w / 2, c = (w % 2 < r) ? w % 2 : w % 2 + 1;  // c != r
-    se = dd * PP + r * P + c;
-    if (dd == 0) {
-      dg[0] = op ? Hp[(P + r) * FTE_NZP + P + c] : 0.0;
-      dg[1] = op2 ? Hp2[(P + 3 + r) * FTE_NZP + P + 3 + c] : 0.0;
-    } else {
-      dg[0] = op ? Hp[(P + r) * FTE_NZP + P + 3 + c] : 0.0;
+  } else {
+    // the 1,024-thread rows (and k_fte_assemble) keep the branch per special kind: the
+    // regrouped form above costs them 6 spilled VGPRs within 64, and 17.3 -> 17.9 us at 1,000
+    // frames (profiles/r06/fte_kernel_totals_*_r06ze.log)
+    const int nOff = P + 12, nS = nOff + 3 * Cg;
+    if (t < P) {
+      sg[0] = oo ? gloc[(size_t)kown * FTE_NZP + t] : 0.0;
+      if (t < 3) {
+        sg[1] = op ? gloc[(size_t)kprev * FTE_NZP + P + t] : 0.0;
+        sg[2] = op2 ? gloc[(size_t)kprev2 * FTE_NZP + P + 3 + t] : 0.0;
+        dg[0] = op ? Hp[(P + t) * FTE_NZP + P + t] : 0.0;           // block 0, prev
+        dg[1] = op2 ? Hp2[(P + 3 + t) * FTE_NZP + P + 3 + t] : 0.0;  // block 0, prev2
+        dg[2] = op ? Hp[(P + t) * FTE_NZP + P + 3 + t] : 0.0;       // block 1, prev
+      }
+      sq = qinv[t];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {  // rows f - 3 .. f + 3
+        const int row = f - 3 + j;
+        sx[j] = (row >= 0 && row <= d.M - 1) ? X[(size_t)row * P + t] : 0.0;
+      }
+    } else if (t < nOff) {
+      const int dd = (t - P) / 6, w = (t - P) % 6, r = w / 2, c = (w % 2 < r) ? w % 2 : w % 2 + 1;  // c != r
+      se = dd * PP + r * P + c;
+      if (dd == 0) {
+        dg[0] = op ? Hp[(P + r) * FTE_NZP + P + c] : 0.0;
+        dg[1] = op2 ? Hp2[(P + 3 + r) * FTE_NZP + P + 3 + c] : 0.0;
+      } else {
+        dg[0] = op ? Hp[(P + r) * FTE_NZP + P + 3 + c] : 0.0;
+      }
+    } else if (t < nS) {
+      const int w = t - nOff, r = w / Cg, c = w % Cg;
+      se = 4 * PP + w;
+      dg[0] = op ? Hp[(P + r) * FTE_NZP + P + 6 + c] : 0.0;
+      dg[1] = op2 ? Hp2[(P + 3 + r) * FTE_NZP + P + 6 + c] : 0.0;
     }
-  } else if (t < nS) {
-    const int w = t - nOff, r = w / Cg, c = w % Cg;
-    se = 4 * PP + w;
-    dg[0] = op ? Hp[(P + r) * FTE_NZP + P + 6 + c] : 0.0;
-    dg[1] = op2 ? Hp2[(P + 3 + r) * FTE_NZP + P + 6 + c] : 0.0;
   }
   // entries with an own term (block 0, columns < 3 of blocks 1, 2, and B): loads of a batch
   // before its stores (k_fte_assemble's A is global memory)
@@ -806,22 +873,35 @@ __device__ void assemble_row(const FteDims& d, int f, const double* __restrict__
     double ov[NBT];
 #pragma unroll
     for (int j = 0; j < NBT; ++j) {
+      // the entry's offset in the own block by selects, then one unconditional load from a valid
+      // address (frame 0's block when not owned, offset 0 past the row's entries) and a select:
+      // a load per branch made the compiler wait for each before the next (k_cr_assemble_build's
+      // ISA), four round trips per batch instead of one
       const int u = e0 + j * nth;
-      double v = 0.0;
-      if (oo && u < n2) {
-        if (u < PP) {
-          const int r = u / P, c = u - r * P;
-          v = Ho[r * FTE_NZP + c];
-        } else if (u < n1) {
-          const int w = u - PP, r = w / 6, cc = w - 6 * r;  // block 1 + cc / 3, column cc % 3
-          v = Ho[r * FTE_NZP + P + cc];
-        } else {
-          const int w = u - n1, r = w / Cg, c = w - r * Cg;
-          v = Ho[r * FTE_NZP + P + 6 + c];
-        }
+      int r, col;
+      if (u < PP) {
+        r = u / P;
+        col = u - r * P;
+      } else if (u < n1) {
+        const int w = u - PP;  // block 1 + cc / 3, column cc % 3
+        r = w / 6;
+        col = P + (w - 6 * r);
+      } else {
+        const int w = u - n1;
+        r = w / (Cg > 0 ? Cg : 1);
+        col = P + 6 + (w - r * Cg);
       }
-      ov[j] = v;
+      ov[j] = Ho[u < n2 ? r * FTE_NZP + col : 0];
     }
+    // every load of the batch issued before the first use: the compiler otherwise moved each
+    // load under its select's condition and waited for it there (the compact-row instance only:
+    // the 1,024-thread rows measured 17.1 -> 17.5 us at 1,000 frames with it, r06ze2)
+    if constexpr (CMP) {
+#pragma unroll
+      for (int j = 0; j < NBT; ++j) asm volatile("" ::"v"(ov[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < NBT; ++j) ov[j] = (oo && e0 + j * nth < n2) ? ov[j] : 0.0;
 #pragma unroll
     for (int j = 0; j < NBT; ++j) {
       const int u = e0 + j * nth;
